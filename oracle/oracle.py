@@ -1,0 +1,297 @@
+"""Python harness of the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may
+import this module. The product package (``python-raytracer_amd/rtx``) never does.
+
+It restates the JSON side of the reference's ``scene_parser.load_scene``
+(provided/scene_parser.py:50-163, defaults at :62-142, ``associate_material`` at
+:288-294, ``add_basic_shape`` at :212-258) independently of the product's parser, reads
+OBJ files like ``igl.read_obj`` (provided/geometry/mesh.py:20) and hands everything to
+``rtx_oracle.c`` (the restated render path) through ctypes.
+"""
+import ctypes as C
+import json
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+
+_i = C.POINTER(C.c_int)
+_d = C.POINTER(C.c_double)
+_f = C.POINTER(C.c_float)
+
+
+class _SceneIn(C.Structure):
+    _fields_ = [
+        ("width", C.c_int), ("height", C.c_int),
+        ("cam", C.c_double * 10),
+        ("ambient", C.c_double * 3),
+        ("jitter", C.c_int), ("samples", C.c_int),
+        ("focal_length", C.c_double), ("aperture", C.c_double),
+        ("dof_samples", C.c_int),
+        ("motion_time", C.c_double),
+        ("motion_samples", C.c_int), ("motion_final", C.c_int),
+        ("n_lights", C.c_int),
+        ("light_type", _i), ("light_colour", _d), ("light_vector", _d), ("light_power", _d),
+        ("n_mats", C.c_int),
+        ("mat_diffuse", _d), ("mat_specular", _d), ("mat_hardness", _d), ("mat_type", _i),
+        ("mat_tint", _d), ("mat_refr", _d),
+        ("n_objs", C.c_int),
+        ("obj_type", _i), ("obj_nmat", _i), ("obj_mat", _i), ("obj_has_speed", _i),
+        ("obj_speed", _d), ("obj_a", _d), ("obj_b", _d), ("obj_c", _d), ("obj_box_mode", _i),
+        ("obj_scalar", _d), ("obj_flat", _i),
+        ("mesh_vert_off", _i), ("mesh_nverts", _i), ("mesh_face_off", _i), ("mesh_nfaces", _i),
+        ("verts", _d), ("faces", _i),
+    ]
+
+
+def build(force=False):
+    """Compile rtx_oracle.c with gcc (oracle/Makefile recipe)."""
+    if force or not os.path.exists(LIB_PATH) or \
+            os.path.getmtime(LIB_PATH) < os.path.getmtime(os.path.join(HERE, "rtx_oracle.c")):
+        subprocess.check_call(["make", "-s", "-C", HERE])
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = C.CDLL(build())
+        _lib.oracle_render.argtypes = [C.POINTER(_SceneIn), C.c_int, C.c_int, _d, _d, C.POINTER(C.c_longlong)]
+        _lib.oracle_object_intersect.argtypes = [C.POINTER(_SceneIn), C.c_int, C.c_double, _f, _f, C.c_int,
+                                                 _d, _f, _f, _i, _i]
+        _lib.oracle_closest_batch.argtypes = [C.POINTER(_SceneIn), C.c_double, C.c_int, _f, _f,
+                                              _d, _i, _i, _i, _f, _f]
+        _lib.oracle_shadow_batch.argtypes = [C.POINTER(_SceneIn), C.c_double, C.c_int, _f, _f, _d, _i]
+    return _lib
+
+
+# ------------------------------------------------------------------ JSON restatement
+_MAT_TYPES = {"diffuse": 0, "mirror": 1, "refractive": 2}
+
+
+def _read_obj(path):
+    """igl.read_obj restated for the triangle OBJ files the reference uses."""
+    V, F = [], []
+    with open(path) as f:
+        for line in f:
+            p = line.split()
+            if not p:
+                continue
+            if p[0] == "v":
+                V.append([float(x) for x in p[1:4]])
+            elif p[0] == "f":
+                F.append([int(x.split("/")[0]) - 1 for x in p[1:4]])
+    return np.array(V, dtype=np.float64).reshape(-1, 3), np.array(F, dtype=np.int32).reshape(-1, 3)
+
+
+def _vec(v):
+    return [float(v[0]), float(v[1]), float(v[2])]
+
+
+class OracleScene:
+    """A scene JSON dictionary converted to the oracle's C input struct."""
+
+    def __init__(self, data, base_dir=None):
+        self._keep = []
+        s = _SceneIn()
+        cam = data["camera"]
+        s.cam[:] = _vec(cam["position"]) + _vec(cam["lookAt"]) + _vec(cam["up"]) + [float(cam["fov"])]
+        res = data.get("resolution", [1080, 720])
+        s.width, s.height = int(res[0]), int(res[1])
+        s.ambient[:] = _vec(data.get("ambient", [0, 0, 0]))
+        try:
+            jitter, samples = data["AA"]["jitter"], data["AA"]["samples"]
+        except KeyError:
+            jitter, samples = False, 1
+        s.jitter, s.samples = int(bool(jitter)), int(samples)
+        try:
+            fl, ap, ds = data["DOF"]["focal_length"], data["DOF"]["aperture"], data["DOF"]["samples"]
+        except KeyError:
+            fl, ap, ds = 1, 0, 1
+        s.focal_length, s.aperture, s.dof_samples = float(fl), float(ap), int(ds)
+        try:
+            mt, ms, mf = data["motion"]["time"], data["motion"]["samples"], data["motion"]["final"]
+        except KeyError:
+            mt, ms, mf = 0, 1, 0
+        s.motion_time, s.motion_samples, s.motion_final = float(mt), int(ms), int(mf)
+
+        lt, lc, lv, lp = [], [], [], []
+        try:
+            for L in data["lights"]:
+                t = L["type"]
+                col = _vec(L["colour"])
+                if t == "point":
+                    vec, pw, code = _vec(L["position"]), float(L["power"]), 0
+                elif t == "directional":
+                    vec, pw, code = _vec(L["direction"]), 1.0, 1
+                else:
+                    continue
+                L["name"]  # noqa: B018  (KeyError semantics of scene_parser.py:109)
+                lt.append(code); lc += col; lv += vec; lp.append(pw)
+        except KeyError:
+            lt, lc, lv, lp = [], [], [], []
+        s.n_lights = len(lt)
+        s.light_type, s.light_colour = self._ai(lt), self._ad(lc)
+        s.light_vector, s.light_power = self._ad(lv), self._ad(lp)
+
+        ids, md, msp, mh, mty, mti, mr = [], [], [], [], [], [], []
+        for m in data["materials"]:
+            ids.append(m["ID"])
+            m["name"]  # noqa: B018
+            mty.append(_MAT_TYPES.get(m.get("type", "diffuse"), 0))
+            md += _vec(m.get("diffuse", [0, 0, 0]))
+            msp += _vec(m.get("specular", [0, 0, 0]))
+            mh.append(float(m.get("hardness", 32)))
+            mti.append(float(m.get("tint", 0.0)))
+            mr.append(float(m.get("refr_index", 1.0)))
+        s.n_mats = len(ids)
+        s.mat_diffuse, s.mat_specular, s.mat_hardness = self._ad(md), self._ad(msp), self._ad(mh)
+        s.mat_type, s.mat_tint, s.mat_refr = self._ai(mty), self._ad(mti), self._ad(mr)
+
+        ot, on, om, ohs, osp, oa, ob, oc, obm, osc, ofl = ([] for _ in range(11))
+        mvo, mnv, mfo, mnf = [], [], [], []
+        allv, allf = [np.zeros((0, 3))], [np.zeros((0, 3), np.int32)]
+        nv_total = nf_total = 0
+        for g in data["objects"]:
+            gt = g["type"]
+            g["name"]  # noqa: B018
+            if gt not in ("sphere", "plane", "box", "mesh"):
+                if gt == "node":
+                    raise NotImplementedError("oracle: hierarchy nodes are not restated yet")
+                continue
+            mats = [k for i in g.get("materials", []) for k, mid in enumerate(ids) if mid == i]
+            if not mats:
+                raise IndexError("object %r has no material (reference raises IndexError)" % g["name"])
+            pos = _vec(g.get("position", [0, 0, 0]))
+            sp = g.get("speed")
+            a, b, c, bm, sc, fl_, vo, nv, fo, nf = pos, [0.0] * 3, [0.0] * 3, 0, 0.0, 0, 0, 0, 0, 0
+            if gt == "sphere":
+                code, sc = 0, float(g["radius"])
+            elif gt == "plane":
+                code, b = 1, _vec(g["normal"])
+                if "texture" in g:
+                    raise NotImplementedError("oracle: textures are not restated yet")
+            elif gt == "box":
+                code = 2
+                if "texture" in g:
+                    raise NotImplementedError("oracle: textures are not restated yet")
+                if "size" in g:
+                    b = _vec(g["size"])
+                else:
+                    bm, c, b = 1, _vec(g["min"]), _vec(g["max"])
+            else:
+                code = 3
+                path = g["filepath"]
+                if base_dir is not None and not os.path.exists(path):
+                    path = os.path.join(base_dir, path)
+                V, F = _read_obj(path)
+                sc, fl_ = float(g["scale"]), int(bool(g.get("flat_shaded", False)))
+                vo, nv, fo, nf = nv_total, len(V), nf_total, len(F)
+                allv.append(V); allf.append(F)
+                nv_total += nv; nf_total += nf
+            ot.append(code); on.append(len(mats)); om += (mats + [0, 0, 0, 0])[:4]
+            ohs.append(0 if sp is None else 1); osp += [0.0] * 3 if sp is None else _vec(sp)
+            oa += a; ob += b; oc += c; obm.append(bm); osc.append(sc); ofl.append(fl_)
+            mvo.append(vo); mnv.append(nv); mfo.append(fo); mnf.append(nf)
+        s.n_objs = len(ot)
+        s.obj_type, s.obj_nmat, s.obj_mat, s.obj_has_speed = self._ai(ot), self._ai(on), self._ai(om), self._ai(ohs)
+        s.obj_speed, s.obj_a, s.obj_b, s.obj_c = self._ad(osp), self._ad(oa), self._ad(ob), self._ad(oc)
+        s.obj_box_mode, s.obj_scalar, s.obj_flat = self._ai(obm), self._ad(osc), self._ai(ofl)
+        s.mesh_vert_off, s.mesh_nverts = self._ai(mvo), self._ai(mnv)
+        s.mesh_face_off, s.mesh_nfaces = self._ai(mfo), self._ai(mnf)
+        s.verts = self._ad(np.concatenate(allv).ravel())
+        s.faces = self._ai(np.concatenate(allf).ravel())
+        self.s = s
+        self.width, self.height = s.width, s.height
+        self.n_samples = s.samples * s.dof_samples * (s.motion_samples + s.motion_final)
+        self.jitter = bool(s.jitter)
+        self.spp_rays = s.samples * s.dof_samples
+
+    def _ad(self, x):
+        a = np.ascontiguousarray(np.asarray(x, dtype=np.float64).ravel())
+        if a.size == 0:
+            a = np.zeros(1)
+        self._keep.append(a)
+        return a.ctypes.data_as(_d)
+
+    def _ai(self, x):
+        a = np.ascontiguousarray(np.asarray(x, dtype=np.int32).ravel())
+        if a.size == 0:
+            a = np.zeros(1, np.int32)
+        self._keep.append(a)
+        return a.ctypes.data_as(_i)
+
+    # -------------------------------------------------------------- render paths
+    def render(self, subimage=0, tasks=1, noise=None, tallies=False):
+        """Scene.render(subimage, tasks) -> (strip_w, H, 3) float64 (scene.py:35-79)."""
+        W, H = self.width, self.height
+        base, extra = divmod(W, tasks)
+        ncol = base + (1 if subimage < extra else 0)
+        out = np.zeros((ncol, H, 3), dtype=np.float64)
+        nz = None
+        if self.jitter:
+            if noise is None:
+                raise ValueError("jittered scene: pass the replayed np.random stream as noise")
+            nz = np.ascontiguousarray(noise, dtype=np.float64).ravel()
+            need = ncol * H * self.spp_rays * 3
+            if nz.size < need:
+                raise ValueError("noise stream too short: %d < %d" % (nz.size, need))
+        tl = (C.c_longlong * 13)()
+        rc = lib().oracle_render(C.byref(self.s), subimage, tasks, out.ctypes.data_as(_d),
+                                 None if nz is None else nz.ctypes.data_as(_d), tl)
+        if rc != 0:
+            raise RuntimeError("oracle_render failed: %d" % rc)
+        if tallies:
+            return out, list(tl)
+        return out
+
+    def object_intersect(self, obj, time, o, d, max_hits=256):
+        t = np.zeros(max_hits); n = np.zeros((max_hits, 3), np.float32); p = np.zeros((max_hits, 3), np.float32)
+        m = np.zeros(max_hits, np.int32); sb = np.zeros(max_hits, np.int32)
+        o = np.ascontiguousarray(o, np.float32); d = np.ascontiguousarray(d, np.float32)
+        k = lib().oracle_object_intersect(C.byref(self.s), obj, float(time), o.ctypes.data_as(_f),
+                                          d.ctypes.data_as(_f), max_hits, t.ctypes.data_as(_d),
+                                          n.ctypes.data_as(_f), p.ctypes.data_as(_f),
+                                          m.ctypes.data_as(_i), sb.ctypes.data_as(_i))
+        k = min(k, max_hits)
+        return t[:k], n[:k], p[:k], m[:k], sb[:k]
+
+    def closest(self, time, o, d):
+        o = np.ascontiguousarray(o, np.float32).reshape(-1, 3); d = np.ascontiguousarray(d, np.float32).reshape(-1, 3)
+        n = len(o)
+        t = np.zeros(n); ob = np.zeros(n, np.int32); sb = np.zeros(n, np.int32); m = np.zeros(n, np.int32)
+        nn = np.zeros((n, 3), np.float32); pp = np.zeros((n, 3), np.float32)
+        lib().oracle_closest_batch(C.byref(self.s), float(time), n, o.ctypes.data_as(_f), d.ctypes.data_as(_f),
+                                   t.ctypes.data_as(_d), ob.ctypes.data_as(_i), sb.ctypes.data_as(_i),
+                                   m.ctypes.data_as(_i), nn.ctypes.data_as(_f), pp.ctypes.data_as(_f))
+        return t, ob, sb, m, nn, pp
+
+    def shadow(self, time, o, d, t_max):
+        o = np.ascontiguousarray(o, np.float32).reshape(-1, 3); d = np.ascontiguousarray(d, np.float32).reshape(-1, 3)
+        tm = np.ascontiguousarray(np.broadcast_to(np.asarray(t_max, np.float64), (len(o),)))
+        occ = np.zeros(len(o), np.int32)
+        lib().oracle_shadow_batch(C.byref(self.s), float(time), len(o), o.ctypes.data_as(_f),
+                                  d.ctypes.data_as(_f), tm.ctypes.data_as(_d), occ.ctypes.data_as(_i))
+        return occ
+
+
+def to_png_array(image):
+    """main.py:325-327: rot90(k=1, axes=(0, 1)) then truncating uint8 conversion."""
+    return (np.rot90(image, k=1, axes=(0, 1)) * 255).astype(np.uint8)
+
+
+def load_bundle(name, **edits):
+    """A scene dictionary from assets/scenes.json with optional edits (resolution, AA ...)."""
+    repo = os.path.dirname(HERE)
+    with open(os.path.join(repo, "assets", "scenes.json")) as f:
+        sc = json.load(f)[name]
+    for k, v in edits.items():
+        sc[k] = v
+    return sc, os.path.join(repo, "assets")
