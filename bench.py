@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X render path (BASELINE.json metric: Mrays/sec + frame ms,
+TwoSpheresPlane 1920x1080).
+
+One step = one 1920x1080 1-spp frame of TwoSpheresPlane rendered by each rank (the
+primary sample is the reference's unit: its tqdm bar counts W*H*aa*dof*|times|,
+provided/scene.py:45,71). With N ranks the job renders N frames per step, one per GPU
+(frame-parallel weak scaling; no data-path collective). ``--rowblock`` additionally times
+the north-star strong-scaling form: one frame split into row blocks across ranks and
+gathered to rank 0 over RCCL.
+
+Launch: python bench.py [--steps K --warmup W]          (N = 1)
+        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "python-raytracer_amd"))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "Mrays/sec + frame ms, TwoSpheresPlane 1920×1080 @1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+CONFIGS = {
+    # name: (bundled scene, resolution, (aa, dof) or None, description)
+    "tsp1080": ("TwoSpheresPlane", (1920, 1080), (1, None), "TwoSpheresPlane 1920x1080 1spp (primary + shadow rays)"),
+    "tm1080": ("TorusMesh", (1920, 1080), (1, None), "TorusMesh 1920x1080 1spp (128-triangle mesh)"),
+    "mr1080": ("MirrorRefraction", (1920, 1080), (1, None), "MirrorRefraction 1920x1080 1spp (reflect/refract chains)"),
+    "dof4k": ("DepthOfField", (3840, 2160), (2, 32), "DepthOfField 3840x2160 AA2 x DOF32 = 64spp, jittered"),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--config", default="tsp1080", choices=sorted(CONFIGS))
+    p.add_argument("--rowblock", action="store_true", help="also time row-block + RCCL gather of one frame")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def make_scene(cfg):
+    import rtx
+    name, res, spp, _ = CONFIGS[cfg]
+    kw = dict(resolution=res, spp=spp)
+    if cfg == "dof4k":
+        kw["AA"] = {"jitter": True, "samples": spp[0]}
+    return rtx.load_bundled_scene(name, **kw)
+
+
+def cpu_baseline(cfg, budget_s):
+    """The oracle (C restatement of the reference, one core) on the same workload:
+    full frames, repeated until the budget is used (whole frames only)."""
+    from oracle import oracle as O
+    name, res, spp, _ = CONFIGS[cfg]
+    d, base = O.load_bundle(name)
+    d["resolution"] = list(res)
+    if spp is not None:
+        d.setdefault("AA", {"jitter": False, "samples": 1})["samples"] = spp[0]
+    osc = O.OracleScene(d, base)
+    W, H = res
+    rows = H
+    if cfg in ("tm1080", "dof4k"):
+        rows = max(1, H // 16)  # deterministic sub-sample for the slow configs
+    nsamp = 0
+    frames = 0
+    t0 = time.perf_counter()
+    noise = None
+    while True:
+        if cfg in ("tm1080", "dof4k"):
+            # a 1/16-height strip of the frame: columns subset via tasks=16, subimage 0
+            ncol = len(np.array_split(np.arange(W), 16)[0])
+            if osc.jitter:
+                noise = np.random.RandomState(0).rand(ncol * H * osc.spp_rays * 3)
+            osc.render(0, 16, noise=noise)
+            nsamp += ncol * H * osc.n_samples
+            sample = "columns 0..%d of %dx%d (1/16 of the frame) per repeat" % (ncol - 1, W, H)
+        else:
+            osc.render()
+            nsamp += W * rows * osc.n_samples
+            sample = "full %dx%d frame(s)" % (W, H)
+        frames += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": nsamp / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
+            "sample": "%s x %d repeats in %.1f s (oracle/rtx_oracle.c, gcc -O2, 1 thread)" % (sample, frames, dt)}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            sys.exit("--gpus %d needs torch.distributed.run with %d processes" % (a.gpus, a.gpus))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import rtx  # noqa: F401
+    from rtx.scene import split_rows
+
+    sc = make_scene(a.config)
+    W, H = sc.vc.width, sc.vc.height
+    spp = sc.samples_per_pixel
+    stream = torch.cuda.current_stream()
+    fb = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+
+    # ray-segment census for the algorithmic byte model (separate counting launch)
+    cnt = torch.zeros(16, dtype=torch.int64, device="cuda")
+    sc.render_device(out=fb, counters=cnt)
+    c = cnt.cpu().numpy()
+    cast_rays = int(c[:10].sum())
+    shadow_rays = int(c[10])
+    segments = cast_rays + shadow_rays
+    b_alg = 32 * segments + 12 * W * H  # 32 B per segment + 12 B/pixel fp32 RGB
+
+    for _ in range(a.warmup):
+        sc.render_device(out=fb)
+    torch.cuda.synchronize()
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record(stream)
+        sc.render_device(out=fb, stream=stream)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    wall = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
+    kern = torch.tensor([sum(e0.elapsed_time(e1) for e0, e1 in evs) / len(evs)], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(wall, op=dist.ReduceOp.MAX)
+        dist.all_reduce(kern, op=dist.ReduceOp.MAX)
+    wall_s = float(wall.item())
+    kern_ms = float(kern.item())
+    ms_per_step = wall_s * 1e3 / a.steps
+    samples_per_step = world * W * H * spp
+    value = samples_per_step * a.steps / wall_s / 1e6
+
+    rowblock = None
+    if a.rowblock and world > 1:
+        from rtx.distributed import render_frame
+        for _ in range(3):
+            render_frame(sc, rank, world, dtype=torch.uint8)
+        torch.cuda.synchronize()
+        dist.barrier()
+        r0 = time.perf_counter()
+        nrb = max(5, a.steps // 2)
+        for _ in range(nrb):
+            render_frame(sc, rank, world, dtype=torch.uint8)
+        torch.cuda.synchronize()
+        dist.barrier()
+        rb = torch.tensor([time.perf_counter() - r0], dtype=torch.float64, device="cuda")
+        dist.all_reduce(rb, op=dist.ReduceOp.MAX)
+        rb_ms = float(rb.item()) * 1e3 / nrb
+        rowblock = {"ms_per_frame": rb_ms, "Mrays_s": W * H * spp / rb_ms / 1e3, "scaling": "strong",
+                    "gather": "uint8 row blocks to rank 0 (torch.distributed.gather, RCCL)",
+                    "rows_per_rank": split_rows(H, world, 0)[1]}
+
+    if rank == 0:
+        achieved = b_alg / (kern_ms * 1e-3) / 1e9
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms_per_step, 5), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32 vectors + fp64 scalars (reference numerics)", "data": "synthetic",
+            "config": {"workload": CONFIGS[a.config][3], "width": W, "height": H, "spp": spp,
+                       "frames_per_step": world,
+                       "parallelism": "frame-parallel (one frame per rank per step)" if world > 1 else "single GPU"},
+            "frame_ms": round(kern_ms, 5),
+            "segments_per_frame": segments, "cast_rays_per_frame": cast_rays, "shadow_rays_per_frame": shadow_rays,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "model": "B_alg = 32 B x ray segments + 12 B x pixels per frame (SURVEY.md 8d) / kernel time",
+                         "bytes_alg_per_frame": b_alg},
+        }
+        if rowblock:
+            out["rowblock"] = rowblock
+        if world == 1 and not a.no_cpu_baseline and a.cpu_seconds > 0:
+            out["cpu_baseline"] = cpu_baseline(a.config, a.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

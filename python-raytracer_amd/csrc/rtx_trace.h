@@ -1,0 +1,513 @@
+// rtx_trace.h — per-ray math of the MI355X render path (device code; also compiled for
+// the host in the tests-only emulation build, tests/native/).
+//
+// Numerics contract: PyGLM vec3 arithmetic is IEEE fp32, Python
+// scalars are fp64. Every expression below keeps the reference's operation order and
+// is compiled with -ffp-contract=off, so no multiply-add is fused. Citations are to
+// SpacewaIker/python-raytracer @ 2025-02-14.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define RTX_HD __host__ __device__ __forceinline__
+
+namespace rtx {
+
+constexpr int kMaxDepth = 10;  // cast_ray(max_recursion=10) (scene.py:81)
+
+// ------------------------------------------------------------------ fp32 vec3 (PyGLM)
+struct f3 {
+    float x, y, z;
+};
+RTX_HD f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+RTX_HD f3 ld3(const float* p) { return f3{p[0], p[1], p[2]}; }
+RTX_HD f3 add(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+RTX_HD f3 sub(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+RTX_HD f3 mul(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+RTX_HD f3 scale(f3 a, float s) { return f3{a.x * s, a.y * s, a.z * s}; }
+RTX_HD f3 divs(f3 a, float s) { return f3{a.x / s, a.y / s, a.z / s}; }
+RTX_HD f3 neg(f3 a) { return f3{-a.x, -a.y, -a.z}; }
+// glm::dot: tmp = a * b; tmp.x + tmp.y + tmp.z (left to right)
+RTX_HD float dot(f3 a, f3 b) {
+    float px = a.x * b.x, py = a.y * b.y, pz = a.z * b.z;
+    float s = px + py;
+    return s + pz;
+}
+RTX_HD f3 cross(f3 a, f3 b) {
+    return f3{a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y};
+}
+// glm::normalize = v * inversesqrt(dot(v, v)), inversesqrt(x) = 1 / sqrt(x)
+RTX_HD f3 normalize(f3 v) {
+    float inv = 1.0f / sqrtf(dot(v, v));
+    return scale(v, inv);
+}
+RTX_HD bool is_zero(f3 v) { return v.x == 0.0f && v.y == 0.0f && v.z == 0.0f; }
+// glm::reflect(I, N) = I - N * dot(N, I) * 2
+RTX_HD f3 reflect(f3 I, f3 N) { return sub(I, scale(scale(N, dot(N, I)), 2.0f)); }
+// glm::refract(I, N, eta), T = float
+RTX_HD f3 refract(f3 I, f3 N, float eta) {
+    float d = dot(N, I);
+    float k = 1.0f - eta * eta * (1.0f - d * d);
+    if (!(k >= 0.0f)) return f3{0.0f, 0.0f, 0.0f};
+    float s = eta * d + sqrtf(k);
+    return sub(scale(I, eta), scale(N, s));
+}
+// Python max(0.0, x) and the clamp max(0.0, min(1.0, x)) of scene.py:113-115
+RTX_HD float pos_part(float x) { return x > 0.0f ? x : 0.0f; }
+RTX_HD float clamp01(float x) {
+    float m = x < 1.0f ? x : 1.0f;
+    return m > 0.0f ? m : 0.0f;
+}
+RTX_HD f3 clamp01(f3 c) { return f3{clamp01(c.x), clamp01(c.y), clamp01(c.z)}; }
+
+// ------------------------------------------------------------------ device scene records
+// Library-internal layouts (not ABI). Derived values are computed once on the host by
+// rtx_api.hip with the same fp32 operation order as the reference computes them per ray.
+struct alignas(16) DObj {
+    int32_t type, nmat, mat0, mat1;
+    int32_t has_speed, tri_begin, tri_count, bv_type;
+    int32_t flat, pad0, pad1, pad2;
+    float a[4];       // sphere centre | plane point | box minpos
+    float b[4];       // plane normal | box maxpos
+    float c[4];       // plane width axis
+    float e[4];       // plane height axis
+    float speed[4];
+    float bv_a[4];    // mesh BV AABB min | sphere centre
+    float bv_b[4];    // mesh BV AABB max
+    double r2;        // sphere radius ** 2
+    double bv_r2;     // mesh BV sphere radius ** 2
+};
+
+struct alignas(16) DTri {
+    float v0[3], v1[3], v2[3];
+    float e01[3], e12[3], e20[3];  // v1 - v0, v2 - v1, v0 - v2 (mesh.py:99-101)
+    float n[3];                    // normalize(cross(v1 - v0, v2 - v0)) (mesh.py:86)
+    float nu[3];                   // cross(v1 - v0, v2 - v0) (mesh.py:134)
+};
+
+struct alignas(16) DTriN {
+    float n0[4], n1[4], n2[4];     // smooth vertex normals (mesh.py:53-70)
+};
+
+struct alignas(16) DMat {
+    float diffuse[4];
+    float specular[4];
+    float tint, omt;               // f32(tint), f32(1 - tint)       (scene.py:104,108)
+    float eta_in, eta_out;         // f32(refr_index), f32(1 / refr_index) (scene.py:191,194)
+    int32_t type, hard_int, hard_is_int, pad;
+    double hardness;
+};
+
+struct alignas(16) DLight {
+    int32_t type, pad0, pad1, pad2;
+    float vec[4];                  // light.vector
+    float negvec[4];               // -light.vector
+    float ndir[4];                 // normalize(-light.vector) (directional, scene.py:173)
+    float cp[4];                   // light.colour * f32(light.power) (scene.py:183)
+};
+
+enum : int32_t { OBJ_SPHERE = 0, OBJ_PLANE = 1, OBJ_BOX = 2, OBJ_MESH = 3 };
+enum : int32_t { MAT_DIFFUSE = 0, MAT_MIRROR = 1, MAT_REFRACTIVE = 2 };
+enum : int32_t { LIGHT_POINT = 0, LIGHT_DIRECTIONAL = 1 };
+enum : int32_t { BV_AABB = 0, BV_SPHERE = 1 };
+
+struct SceneView {
+    const DObj* __restrict__ objs;
+    const DTri* __restrict__ tris;
+    const DTriN* __restrict__ trins;
+    const DMat* __restrict__ mats;
+    const DLight* __restrict__ lights;
+    int32_t n_objs, n_lights;
+    float ambient[4];
+};
+
+// ------------------------------------------------------------------ counters
+struct Tally {
+    uint32_t cast[kMaxDepth];
+    uint32_t shadow, shade, tri;
+};
+
+template <bool COUNT>
+RTX_HD void tally_inc(Tally& t, uint32_t Tally::*field) {
+    if (COUNT) (t.*field)++;
+}
+
+// ------------------------------------------------------------------ geometry helpers
+RTX_HD f3 moved(const DObj& o, const float* p, float time) {
+    // `p + self.speed * self.scene.current_time` (simple_geometry.py:21-24, :106-109, :189-194)
+    f3 q = ld3(p);
+    if (o.has_speed) q = add(q, scale(ld3(o.speed), time));
+    return q;
+}
+
+// Ray.getPoint(t) = origin + direction * t, t cast to fp32 (helperclasses.py:21-22)
+RTX_HD f3 get_point(f3 o, f3 d, double t) { return add(o, scale(d, (float)t)); }
+
+// Closest-hit record: t (fp64, as the reference compares it), object, sub-index
+// (box: entry slab label; mesh: face index).
+struct Hit {
+    double t;
+    int32_t obj;
+    int32_t sub;
+};
+
+// Sphere quadratic (simple_geometry.py:29-39); returns false when disc < 0.
+RTX_HD bool sphere_roots(f3 o, f3 d, f3 c, double r2, double& b, double& s, double& two_a) {
+    double a = (double)dot(d, d);
+    f3 oc = sub(o, c);
+    b = 2.0 * (double)dot(d, oc);
+    double cc = (double)dot(oc, oc) - r2;
+    double disc = b * b - 4.0 * a * cc;
+    if (disc < 0.0) return false;
+    s = sqrt(disc);
+    two_a = 2.0 * a;
+    return true;
+}
+
+// AABB slabs (simple_geometry.py:196-226; bounding_volumes.py:61-91). Returns false if
+// a zero-direction slab rejects the ray; otherwise the entry start (max of starts, first
+// wins), its label, and the exit end (min of ends, first wins), all fp64.
+RTX_HD bool box_slabs(f3 o, f3 d, f3 mn, f3 mx, double& start, int& label, double& end) {
+    const float ro[3] = {o.x, o.y, o.z};
+    const float rd[3] = {d.x, d.y, d.z};
+    const float lo[3] = {mn.x, mn.y, mn.z};
+    const float hi[3] = {mx.x, mx.y, mx.z};
+    double s_best = 0.0, e_best = 0.0;
+    int l_best = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        double s, e;
+        if (rd[k] == 0.0f) {
+            if (!((double)lo[k] < (double)ro[k] && (double)ro[k] < (double)hi[k])) return false;
+            s = -INFINITY;
+            e = INFINITY;
+        } else {
+            double t1 = ((double)lo[k] - (double)ro[k]) / (double)rd[k];
+            double t2 = ((double)hi[k] - (double)ro[k]) / (double)rd[k];
+            s = t2 < t1 ? t2 : t1;  // AAInterval: start = min(t1, t2)
+            e = t2 > t1 ? t2 : t1;  //             end = max(t1, t2)
+        }
+        if (k == 0) {
+            s_best = s; e_best = e; l_best = 0;
+        } else {
+            if (s > s_best) { s_best = s; l_best = k; }
+            if (e < e_best) e_best = e;
+        }
+    }
+    start = s_best;
+    label = l_best;
+    end = e_best;
+    return true;
+}
+
+// Mesh bounding volume (bounding_volumes.py:18-37 sphere, :49-83 AABB).
+RTX_HD bool mesh_bv(const DObj& ob, f3 o, f3 d) {
+    if (ob.bv_type == BV_AABB) {
+        double start, end;
+        int label;
+        if (!box_slabs(o, d, ld3(ob.bv_a), ld3(ob.bv_b), start, label, end)) return false;
+        return !(start > end || start < 0.0);
+    }
+    double b, s, two_a;
+    if (!sphere_roots(o, d, ld3(ob.bv_a), ob.bv_r2, b, s, two_a)) return false;
+    if ((-b - s) / two_a > 0.0) return true;
+    return (-b + s) / two_a > 0.0;
+}
+
+// ------------------------------------------------------------------ closest hit
+// All objects in scene order; the first strict minimum wins (scene.py:86-94).
+template <bool MESH, bool COUNT>
+RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl) {
+    Hit h{INFINITY, -1, 0};
+    for (int oi = 0; oi < S.n_objs; ++oi) {
+        const DObj& ob = S.objs[oi];
+        const int32_t type = ob.type;
+        if (type == OBJ_SPHERE) {  // simple_geometry.py:20-46
+            double b, s, two_a;
+            if (sphere_roots(o, d, moved(ob, ob.a, time), ob.r2, b, s, two_a)) {
+                double t1 = (-b - s) / two_a;
+                if (t1 > 0.0) {
+                    if (t1 < h.t) { h.t = t1; h.obj = oi; h.sub = 0; }
+                } else {
+                    double t2 = (-b + s) / two_a;
+                    if (t2 > 0.0 && t2 < h.t) { h.t = t2; h.obj = oi; h.sub = 1; }
+                }
+            }
+        } else if (type == OBJ_PLANE) {  // simple_geometry.py:105-120
+            f3 n = ld3(ob.b);
+            float denom = dot(d, n);
+            if (fabs((double)denom) > 1e-4) {
+                double t = (double)dot(sub(moved(ob, ob.a, time), o), n) / (double)denom;
+                if (t >= 0.0 && t < h.t) { h.t = t; h.obj = oi; h.sub = 0; }
+            }
+        } else if (type == OBJ_BOX) {  // simple_geometry.py:188-249 (entry precedes exit)
+            double start, end;
+            int label;
+            if (box_slabs(o, d, moved(ob, ob.a, time), moved(ob, ob.b, time), start, label, end)) {
+                if (!(start > end || start < 0.0) && start < h.t) { h.t = start; h.obj = oi; h.sub = label; }
+            }
+        } else if (MESH && type == OBJ_MESH) {  // mesh.py:72-119
+            if (mesh_bv(ob, o, d)) {
+                const int32_t f0 = ob.tri_begin, nf = ob.tri_count;
+                for (int f = 0; f < nf; ++f) {
+                    const DTri& T = S.tris[f0 + f];
+                    tally_inc<COUNT>(tl, &Tally::tri);
+                    f3 n = ld3(T.n);
+                    float denom = dot(d, n);
+                    if (fabs((double)denom) < 1e-4) continue;
+                    f3 v0 = ld3(T.v0);
+                    double t = (double)dot(sub(v0, o), n) / (double)denom;
+                    if (t < 0.0) continue;
+                    f3 p = get_point(o, d, t);
+                    float b0 = dot(cross(ld3(T.e01), sub(p, v0)), n);
+                    float b1 = dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n);
+                    float b2 = dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n);
+                    if (b0 >= 0.0f && b1 >= 0.0f && b2 >= 0.0f && t < h.t) { h.t = t; h.obj = oi; h.sub = f; }
+                }
+            }
+        }
+    }
+    return h;
+}
+
+// ------------------------------------------------------------------ shadow any-hit
+template <bool MESH, bool COUNT>
+RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, Tally& tl) {
+    for (int oi = 0; oi < S.n_objs; ++oi) {
+        const DObj& ob = S.objs[oi];
+        const int32_t type = ob.type;
+        if (type == OBJ_SPHERE) {  // simple_geometry.py:48-72 (shadow_epsilon 1e-3)
+            double b, s, two_a;
+            if (sphere_roots(o, d, moved(ob, ob.a, time), ob.r2, b, s, two_a)) {
+                double t = (-b - s) / two_a;
+                if (1e-3 < t && t < t_max) return true;
+                t = (-b + s) / two_a;
+                if (1e-3 < t && t < t_max) return true;
+            }
+        } else if (type == OBJ_PLANE) {  // simple_geometry.py:122-131
+            f3 n = ld3(ob.b);
+            float denom = dot(d, n);
+            if (fabs((double)denom) > 1e-4) {
+                double t = (double)dot(sub(moved(ob, ob.a, time), o), n) / (double)denom;
+                if (1e-4 < t && t < t_max) return true;
+            }
+        } else if (type == OBJ_BOX) {  // simple_geometry.py:251-294
+            double start, end;
+            int label;
+            if (box_slabs(o, d, moved(ob, ob.a, time), moved(ob, ob.b, time), start, label, end)) {
+                if (!(start > end) && 1e-4 < start && start < t_max) return true;
+            }
+        } else if (MESH && type == OBJ_MESH) {  // mesh.py:121-153 (no t_max test)
+            if (mesh_bv(ob, o, d)) {
+                const int32_t f0 = ob.tri_begin, nf = ob.tri_count;
+                for (int f = 0; f < nf; ++f) {
+                    const DTri& T = S.tris[f0 + f];
+                    tally_inc<COUNT>(tl, &Tally::tri);
+                    f3 n = ld3(T.nu);
+                    float denom = dot(d, n);
+                    if (fabs((double)denom) < 1e-4) continue;
+                    f3 v0 = ld3(T.v0);
+                    double t = (double)dot(sub(v0, o), n) / (double)denom;
+                    if (t < 1e-4) continue;
+                    f3 p = get_point(o, d, t);
+                    if (dot(cross(ld3(T.e01), sub(p, v0)), n) >= 0.0f &&
+                        dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n) >= 0.0f &&
+                        dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n) >= 0.0f)
+                        return true;
+                }
+            }
+        }
+    }
+    return false;
+}
+
+// ------------------------------------------------------------------ hit record
+// Plane.get_material (simple_geometry.py:133-148): checker by floor of the projected
+// coordinates, Python modulo.
+RTX_HD int32_t plane_material(const DObj& ob, f3 point, float time) {
+    if (ob.nmat == 1) return ob.mat0;
+    f3 position = moved(ob, ob.a, time);
+    f3 n = ld3(ob.b);
+    point = sub(point, scale(n, dot(sub(point, position), n)));
+    float x = dot(sub(point, position), ld3(ob.c));
+    float z = dot(sub(point, position), ld3(ob.e));
+    double dx = floor((double)position.x - (double)x);
+    double dz = floor((double)position.z - (double)z);
+    int64_t s = (int64_t)dx + (int64_t)dz;
+    return (s & 1) ? ob.mat1 : ob.mat0;  // (dx + dz) % 2 with Python modulo
+}
+
+// Barycentric smooth normal (mesh.py:103-113; igl.barycentric_coordinates_tri on fp32 rows).
+RTX_HD f3 smooth_normal(const DTri& T, const DTriN& N, f3 p) {
+    f3 a = ld3(T.v0), b = ld3(T.v1), c = ld3(T.v2);
+    f3 v0 = sub(b, a), v1 = sub(c, a), v2 = sub(p, a);
+    float d00 = dot(v0, v0), d01 = dot(v0, v1), d11 = dot(v1, v1);
+    float d20 = dot(v2, v0), d21 = dot(v2, v1);
+    float den = d00 * d11 - d01 * d01;
+    float v = (d11 * d20 - d01 * d21) / den;
+    float w = (d00 * d21 - d01 * d20) / den;
+    float u = (1.0f - v) - w;
+    f3 n = add(add(scale(ld3(N.n0), u), scale(ld3(N.n1), v)), scale(ld3(N.n2), w));
+    return normalize(n);
+}
+
+struct Surface {
+    f3 position, normal;
+    int32_t mat;
+};
+
+template <bool MESH>
+RTX_HD Surface resolve_hit(const SceneView& S, const Hit& h, f3 o, f3 d, float time) {
+    Surface sf;
+    const DObj& ob = S.objs[h.obj];
+    sf.position = get_point(o, d, h.t);
+    sf.mat = ob.mat0;
+    const int32_t type = ob.type;
+    if (type == OBJ_SPHERE) {
+        sf.normal = normalize(sub(sf.position, moved(ob, ob.a, time)));
+    } else if (type == OBJ_PLANE) {
+        sf.normal = ld3(ob.b);
+        sf.mat = plane_material(ob, sf.position, time);
+    } else if (type == OBJ_BOX) {
+        // simple_geometry.py:231-242: entry-slab label and the direction's sign
+        const float dl = h.sub == 0 ? d.x : (h.sub == 1 ? d.y : d.z);
+        float sgn = dl < 0.0f ? 1.0f : (dl > 0.0f ? -1.0f : 0.0f);
+        sf.normal = f3{h.sub == 0 ? sgn : 0.0f, h.sub == 1 ? sgn : 0.0f, h.sub == 2 ? sgn : 0.0f};
+    } else if (MESH) {
+        const DTri& T = S.tris[ob.tri_begin + h.sub];
+        if (ob.flat)
+            sf.normal = ld3(T.n);
+        else
+            sf.normal = smooth_normal(T, S.trins[ob.tri_begin + h.sub], sf.position);
+    }
+    return sf;
+}
+
+// ------------------------------------------------------------------ shading
+// `x ** hardness` (CPython float_pow -> pow) in fp64. Integer exponents use binary
+// exponentiation; the fp32 cast that follows makes it equal to libm pow except when the
+// exact value lies within a few fp64 ulps of an fp32 rounding boundary.
+RTX_HD double spec_pow(double x, const DMat& m) {
+    if (m.hard_is_int) {
+        int n = m.hard_int;
+        double r = 1.0, b = x;
+        while (n > 0) {
+            if (n & 1) r *= b;
+            b *= b;
+            n >>= 1;
+        }
+        return r;
+    }
+    return pow(x, m.hardness);
+}
+
+// _compute_regular_lighting (scene.py:140-187)
+template <bool MESH, bool COUNT>
+RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const DMat& m, float time, Tally& tl) {
+    f3 colour = mk(0.0f, 0.0f, 0.0f);
+    const f3 diffuse = ld3(m.diffuse);
+    tally_inc<COUNT>(tl, &Tally::shade);
+    for (int li = 0; li < S.n_lights; ++li) {
+        const DLight& L = S.lights[li];
+        f3 sdir;
+        double t_max;
+        if (L.type == LIGHT_POINT) {
+            sdir = sub(ld3(L.vec), pos);
+            t_max = 1.0;
+        } else {
+            sdir = ld3(L.negvec);
+            t_max = INFINITY;
+        }
+        tally_inc<COUNT>(tl, &Tally::shadow);
+        if (occluded<MESH, COUNT>(S, pos, sdir, t_max, time, tl)) continue;
+        f3 light_dir = L.type == LIGHT_POINT ? normalize(sdir) : ld3(L.ndir);
+        f3 lambert = scale(diffuse, pos_part(dot(normal, light_dir)));
+        f3 half_vect = normalize(sub(light_dir, dir));
+        float nh = dot(normal, half_vect);
+        double base = nh > 0.0f ? (double)nh : 0.0;
+        f3 specular = scale(ld3(m.specular), (float)spec_pow(base, m));
+        colour = add(colour, mul(ld3(L.cp), add(lambert, specular)));
+    }
+    colour = add(colour, mul(ld3(S.ambient), diffuse));
+    return colour;
+}
+
+// ------------------------------------------------------------------ cast_ray, iteratively
+// scene.py:81-116 + _compute_refraction (:189-209). Secondary rays form a chain (one
+// reflect or refract child per level), so the recursion becomes a loop that records
+// (lighting, tint, 1 - tint) per mirror/refractive level and unwinds bottom-up with the
+// per-level clamp. Frames live in registers: only constant indices touch the arrays.
+template <bool MESH, bool SEC, bool COUNT>
+RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl) {
+    constexpr int NF = SEC ? kMaxDepth : 1;
+    float fr_r[NF], fr_g[NF], fr_b[NF], fr_t[NF], fr_o[NF];
+#pragma unroll
+    for (int k = 0; k < NF; ++k) { fr_r[k] = fr_g[k] = fr_b[k] = fr_t[k] = fr_o[k] = 0.0f; }
+    int nfr = 0;
+    f3 tail = mk(0.0f, 0.0f, 0.0f);
+    bool in_shape = false;
+    for (int level = 0; level < (SEC ? kMaxDepth : 1); ++level) {
+        if (COUNT) tl.cast[level]++;
+        Hit h = closest_hit<MESH, COUNT>(S, o, d, time, tl);
+        if (h.obj < 0) break;  // miss -> black
+        Surface sf = resolve_hit<MESH>(S, h, o, d, time);
+        const DMat& m = S.mats[sf.mat];
+        if (SEC && m.type == MAT_MIRROR) {
+            f3 rdir = reflect(d, sf.normal);
+            f3 L = regular_lighting<MESH, COUNT>(S, d, sf.position, sf.normal, m, time, tl);
+#pragma unroll
+            for (int k = 0; k < NF; ++k)
+                if (k == nfr) { fr_r[k] = L.x; fr_g[k] = L.y; fr_b[k] = L.z; fr_t[k] = m.tint; fr_o[k] = m.omt; }
+            ++nfr;
+            o = add(sf.position, scale(rdir, 0.01f));
+            d = rdir;
+            in_shape = false;
+            continue;
+        }
+        if (SEC && m.type == MAT_REFRACTIVE) {
+            float eta = in_shape ? m.eta_in : m.eta_out;
+            f3 n = in_shape ? neg(sf.normal) : sf.normal;
+            f3 rdir = refract(d, n, eta);
+            f3 L = regular_lighting<MESH, COUNT>(S, d, sf.position, n, m, time, tl);
+#pragma unroll
+            for (int k = 0; k < NF; ++k)
+                if (k == nfr) { fr_r[k] = L.x; fr_g[k] = L.y; fr_b[k] = L.z; fr_t[k] = m.tint; fr_o[k] = m.omt; }
+            ++nfr;
+            if (is_zero(rdir)) break;  // total internal reflection -> black child
+            o = add(sf.position, scale(rdir, 0.0001f));
+            d = rdir;
+            in_shape = !in_shape;
+            continue;
+        }
+        tail = clamp01(regular_lighting<MESH, COUNT>(S, d, sf.position, sf.normal, m, time, tl));
+        break;
+    }
+    if (SEC) {
+#pragma unroll
+        for (int k = NF - 1; k >= 0; --k) {
+            if (k < nfr) {
+                f3 c = add(scale(mk(fr_r[k], fr_g[k], fr_b[k]), fr_t[k]), scale(tail, fr_o[k]));
+                tail = clamp01(c);
+            }
+        }
+    }
+    return tail;
+}
+
+// ------------------------------------------------------------------ Philox4x32-10
+RTX_HD void philox4x32(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+        c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+}  // namespace rtx

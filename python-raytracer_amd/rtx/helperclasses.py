@@ -1,0 +1,132 @@
+"""Value types of the scene description (mirror of provided/helperclasses.py:13-108).
+
+Same class names, constructor arguments and attribute names as the reference, so code
+written against the reference's objects keeps working. Vectors are numpy float32 arrays
+(PyGLM vec3 semantics); scalars are Python floats.
+"""
+import math
+
+import numpy as np
+
+from . import f32 as F
+
+
+class Ray:
+    """helperclasses.py:13-25 (host-side value; the device traces rays in SoA form)."""
+
+    def __init__(self, o, d):
+        self.origin = F.vec3(o)
+        self.direction = F.vec3(d)
+
+    def getDistance(self, point):
+        return float(F.length(F.vec3(point) - self.origin))
+
+    def getPoint(self, t):
+        return self.origin + F.scale(self.direction, t)
+
+    def __repr__(self):
+        return "Ray(origin: %s, dir: %s)" % (self.origin, self.direction)
+
+
+class Material:
+    """helperclasses.py:28-47."""
+
+    def __init__(self, name, specular, diffuse, hardness, ID, mat_type="diffuse", mat_tint=0.0):
+        self.name = name
+        self.specular = F.vec3(specular)
+        self.diffuse = F.vec3(diffuse)
+        self.hardness = hardness
+        self.ID = ID
+        self.mat_type = mat_type
+        self.refr_index = 1.0
+        self.tint = mat_tint
+
+    @staticmethod
+    def default():
+        return Material("default", (0, 0, 0), (0, 0, 0), -1, -1)
+
+    def __repr__(self):
+        return "Material(%s, type: %s, specular: %s, diffuse: %s, hardness: %s, ID: %s)" % (
+            self.name, self.mat_type, self.specular, self.diffuse, self.hardness, self.ID)
+
+
+class Light:
+    """helperclasses.py:50-59."""
+
+    def __init__(self, ltype, name, colour, vector, power):
+        self.type = ltype
+        self.name = name
+        self.colour = F.vec3(colour)
+        self.vector = F.vec3(vector)
+        self.power = power
+
+    def __repr__(self):
+        return "Light(%s, type: %s, colour: %s, vector: %s, power: %s)" % (
+            self.name, self.type, self.colour, self.vector, self.power)
+
+
+class AAInterval:
+    """helperclasses.py:62-66 (the device restates it in rtx_trace.h box_slabs)."""
+
+    def __init__(self, t1, t2, label=None):
+        self.start = min(t1, t2)
+        self.end = max(t1, t2)
+        self.label = label
+
+
+class ViewportCamera:
+    """helperclasses.py:69-108: viewport, camera basis, lens and motion samples."""
+
+    def __init__(self):
+        self.focal_length = 1.0
+        self.aperture = 0.0
+        self.dof_samples = 1
+        self.motion_times = [0]
+
+    def set_viewport(self, width, height):
+        self.width = width
+        self.height = height
+        self.aspect = width / height
+        return self
+
+    def set_camera(self, position, lookat, up, fov):
+        position, lookat, up = F.vec3(position), F.vec3(lookat), F.vec3(up)
+        cam_dir = position - lookat
+        self.position = position
+        self.d = 1.0
+        self.top = self.d * math.tan(math.radians(fov / 2))
+        self.right = self.aspect * self.top
+        self.bottom = -self.top
+        self.left = -self.right
+        self.w = F.normalize(cam_dir)
+        self.u = F.normalize(F.cross(up, self.w))
+        self.v = F.cross(self.w, self.u)
+        return self
+
+    def set_lens(self, focal_length, aperture, dof_samples):
+        self.focal_length = focal_length
+        self.aperture = aperture
+        self.dof_samples = dof_samples
+        return self
+
+    def set_motion(self, time, motion_samples, motion_final):
+        dt = time / motion_samples
+        self.motion_times = [dt * i for i in range(motion_samples)]
+        self.motion_times += [time] * motion_final
+        return self
+
+
+def sunflower(num_points, origin, radius):
+    """Scene._sunflower_spread (scene.py:118-138), evaluated with numpy fp64 scalars as
+    the reference does; points are PyGLM vec3 (float32)."""
+    phi = (1 + np.sqrt(5)) / 2
+    angle_stride = 2 * np.pi / phi
+    out = np.zeros((num_points, 3), dtype=np.float32)
+    ox, oy, oz = float(origin[0]), float(origin[1]), origin[2]
+    for k in range(1, num_points + 1):
+        r = radius * np.sqrt(k - 0.5) / np.sqrt(num_points - 0.5)
+        theta = k * angle_stride
+        x = r * np.cos(theta) + ox
+        y = r * np.sin(theta) + oy
+        out[k - 1] = np.array([x, y, oz], dtype=np.float64).astype(np.float32)
+    return out

@@ -1,0 +1,286 @@
+"""Scene: the reference's render entry point, running on MI355X through librtx.so.
+
+Mirror of provided/scene.py:16-209. ``Scene.render(subimage=0, tasks=1)`` keeps the
+reference's signature and result: a float64 array of shape (strip_width, height, 3),
+indexed [column, row-from-bottom, rgb], where the strip is
+``np.array_split(np.arange(width), tasks)[subimage]`` (scene.py:36-37). The per-pixel
+loops, cast_ray, shading and the intersectors run in HIP kernels (csrc/); this module
+only prepares the reference's scalar tables (pixel x/y running sums, sunflower origins,
+motion times) and moves buffers.
+"""
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _native as N
+from . import f32 as F
+from . import geometry as geom
+from .helperclasses import sunflower
+
+_MAT_CODE = {"diffuse": N.RTX_MAT_DIFFUSE, "mirror": N.RTX_MAT_MIRROR, "refractive": N.RTX_MAT_REFRACTIVE}
+
+DEFAULT_SEED = 0x5EED
+
+
+def _ptr(a, ctype):
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+def strip_columns(width, subimage, tasks):
+    """np.array_split(np.arange(width), tasks)[subimage] as (first column, count)."""
+    if tasks < 1 or not 0 <= subimage < tasks:
+        raise IndexError("subimage %d out of range for %d tasks" % (subimage, tasks))
+    base, extra = divmod(width, tasks)
+    col0 = subimage * base + min(subimage, extra)
+    n = base + (1 if subimage < extra else 0)
+    if n == 0:
+        raise IndexError("index 0 is out of bounds for axis 0 with size 0")  # width[0] on an empty strip
+    return col0, n
+
+
+def split_rows(height, n, k):
+    """np.array_split(np.arange(height), n)[k] as (first row, count): rank k's row block."""
+    base, extra = divmod(height, n)
+    return k * base + min(k, extra), base + (1 if k < extra else 0)
+
+
+class _NativeScene:
+    """Owns an rtx_scene handle (device buffers live until destroy)."""
+
+    def __init__(self, desc):
+        h = C.c_void_p()
+        N.call("rtx_scene_create", C.byref(desc), C.byref(h))
+        self.h = h
+        self.device = torch.cuda.current_device()
+
+    def close(self):
+        if self.h is not None and self.h.value:
+            N.load().rtx_scene_destroy(self.h)
+        self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Scene:
+    def __init__(self, vc, jitter, samples, ambient, lights, materials, objects):
+        self.vc = vc
+        self.jitter = jitter
+        self.samples = samples
+        self.ambient = F.vec3(ambient)
+        self.lights = lights
+        self.materials = materials
+        self.objects = objects
+        self.seed = DEFAULT_SEED      # Philox key for jitter (the reference's RNG is unseeded)
+        self.jitter_noise = None      # optional replayed np.random.rand() stream (parity mode)
+        self._native = None
+        self._cam_key = None
+
+    # ------------------------------------------------------------------ scene upload
+    def scene_desc(self):
+        """Flatten the objects into the rtx_scene_desc ABI arrays (scene order kept)."""
+        mats = list(self.materials)
+        index = {id(m): i for i, m in enumerate(mats)}
+
+        def mat_index(m):
+            if id(m) not in index:
+                index[id(m)] = len(mats)
+                mats.append(m)
+            return index[id(m)]
+
+        objs = (N.rtx_object * max(1, len(self.objects)))()
+        tris = []
+        for i, g in enumerate(self.objects):
+            o = objs[i]
+            o.n_mats = len(g.materials)
+            for k, m in enumerate(g.materials[:2]):
+                o.mat[k] = mat_index(m)
+            o.has_speed = 0 if g.speed is None else 1
+            o.speed = N.f3(g.speed if g.speed is not None else (0, 0, 0))
+            if isinstance(g, geom.Sphere):
+                o.type, o.a, o.radius = N.RTX_SPHERE, N.f3(g.center), float(g.radius)
+            elif isinstance(g, geom.Plane):
+                if g.texture is not None:
+                    raise NotImplementedError("plane textures (SURVEY.md §8f row 2)")
+                o.type, o.a, o.b = N.RTX_PLANE, N.f3(g.point), N.f3(g.normal)
+            elif isinstance(g, geom.AABB):
+                if g.texture is not None:
+                    raise NotImplementedError("box textures (SURVEY.md §8f row 2)")
+                o.type, o.a, o.b = N.RTX_BOX, N.f3(g.minpos), N.f3(g.maxpos)
+            elif isinstance(g, geom.Mesh):
+                o.type = N.RTX_MESH
+                o.tri_begin = sum(len(t) for t in tris)
+                t = g.triangles()
+                o.tri_count = len(t)
+                tris.append(t)
+                o.flat = 1 if g.flat_shaded else 0
+                if g.bv_type == "aabb":
+                    o.bv_type, o.bv_a, o.bv_b = N.RTX_BV_AABB, N.f3(g.bv_min), N.f3(g.bv_max)
+                else:
+                    o.bv_type, o.bv_a, o.bv_radius = N.RTX_BV_SPHERE, N.f3(g.bv_center), float(g.bv_radius)
+            else:
+                raise NotImplementedError("unsupported geometry %r" % (g,))
+        cm = (N.rtx_material * max(1, len(mats)))()
+        for i, m in enumerate(mats):
+            cm[i].diffuse, cm[i].specular = N.f3(m.diffuse), N.f3(m.specular)
+            cm[i].hardness = float(m.hardness)
+            cm[i].type = _MAT_CODE.get(m.mat_type, N.RTX_MAT_DIFFUSE)  # other strings shade as diffuse
+            cm[i].tint, cm[i].refr_index = float(m.tint), float(m.refr_index)
+        cl = (N.rtx_light * max(1, len(self.lights)))()
+        for i, L in enumerate(self.lights):
+            cl[i].type = N.RTX_LIGHT_POINT if L.type == "point" else N.RTX_LIGHT_DIRECTIONAL
+            cl[i].colour, cl[i].vector, cl[i].power = N.f3(L.colour), N.f3(L.vector), float(L.power)
+        tri = np.ascontiguousarray(np.concatenate(tris).astype(np.float32)) if tris else np.zeros((1, 6, 3), np.float32)
+        desc = N.rtx_scene_desc()
+        desc.n_objects, desc.objects = len(self.objects), objs
+        desc.n_materials, desc.materials = len(mats), cm
+        desc.n_lights, desc.lights = len(self.lights), cl
+        desc.n_triangles = sum(len(t) for t in tris)
+        desc.triangles = tri.ctypes.data_as(C.POINTER(N.rtx_triangle))
+        desc.ambient = N.f3(self.ambient)
+        desc._keep = (objs, cm, cl, tri)
+        return desc
+
+    def native(self):
+        if self._native is None or self._native.device != torch.cuda.current_device():
+            self._native = _NativeScene(self.scene_desc())
+            self._cam_key = None
+        return self._native
+
+    # ------------------------------------------------------------------ camera tables
+    def camera_tables(self, subimage=0, tasks=1):
+        """The reference's per-frame scalars (scene.py:36-45, :48-61), evaluated on the host."""
+        vc = self.vc
+        col0, ncols = strip_columns(vc.width, subimage, tasks)
+        dx = (vc.right - vc.left) / vc.width
+        dy = (vc.top - vc.bottom) / vc.height
+        xs = np.empty(ncols, np.float64)
+        x = vc.left + (0.5 + np.int64(col0)) * dx
+        for i in range(ncols):
+            xs[i] = x
+            x += dx
+        ys = np.empty(vc.height, np.float64)
+        y = vc.bottom + 0.5 * dy
+        for j in range(vc.height):
+            ys[j] = y
+            y += dy
+        dof = sunflower(vc.dof_samples, vc.position, vc.aperture)
+        aa = np.stack([sunflower(self.samples, dof[k], 2 * (dx + dy)) for k in range(vc.dof_samples)])
+        return dict(col0=col0, ncols=ncols, xs=xs.astype(np.float32), ys=ys.astype(np.float32),
+                    dof=np.ascontiguousarray(dof), aa=np.ascontiguousarray(aa),
+                    times=np.asarray(vc.motion_times, np.float64), jscale=0.1 * (dx + dy))
+
+    def camera_desc(self, subimage=0, tasks=1):
+        """rtx_camera_desc for the strip; returns (desc, tables). The tables own the
+        memory the descriptor points at: keep them alive while the descriptor is used."""
+        t = self.camera_tables(subimage, tasks)
+        vc = self.vc
+        d = N.rtx_camera_desc()
+        d.width, d.height, d.col0, d.ncols = vc.width, vc.height, t["col0"], t["ncols"]
+        d.xs, d.ys = _ptr(t["xs"], C.c_float), _ptr(t["ys"], C.c_float)
+        d.position, d.u, d.v, d.w = N.f3(vc.position), N.f3(vc.u), N.f3(vc.v), N.f3(vc.w)
+        d.d, d.focal_length = float(vc.d), float(vc.focal_length)
+        d.n_dof, d.n_aa = vc.dof_samples, self.samples
+        d.dof_origins, d.aa_origins = _ptr(t["dof"], C.c_float), _ptr(t["aa"], C.c_float)
+        d.n_times, d.times = len(t["times"]), _ptr(t["times"], C.c_double)
+        d.jitter_scale, d.seed = float(t["jscale"]), int(self.seed) & 0xFFFFFFFFFFFFFFFF
+        if not self.jitter:
+            d.jitter = N.RTX_JITTER_OFF
+        elif self.jitter_noise is not None:
+            need = t["ncols"] * vc.height * vc.dof_samples * self.samples * 3
+            noise = np.asarray(self.jitter_noise, np.float64).ravel()
+            if noise.size < need:
+                raise ValueError("jitter_noise too short: %d < %d" % (noise.size, need))
+            t["noise"] = np.ascontiguousarray(noise[:need].astype(np.float32))
+            d.jitter, d.noise = N.RTX_JITTER_REPLAY, _ptr(t["noise"], C.c_float)
+        else:
+            d.jitter = N.RTX_JITTER_PHILOX
+        return d, t
+
+    def _set_camera(self, subimage, tasks):
+        key = (subimage, tasks, self.jitter, self.seed, id(self.jitter_noise))
+        nat = self.native()
+        if self._cam_key == key:
+            return self._cam_info
+        d, t = self.camera_desc(subimage, tasks)
+        N.call("rtx_camera_set", nat.h, C.byref(d))
+        self._cam_key = key
+        self._cam_info = t
+        return t
+
+    # ------------------------------------------------------------------ rendering
+    def render_device(self, subimage=0, tasks=1, row0=0, nrows=None, out=None, counters=None, stream=None):
+        """Render image rows [row0, row0 + nrows) (row 0 = top) of the strip into a float32
+        CUDA tensor [nrows, strip_width, 3] (the rot90'd reference image). Asynchronous
+        on ``stream`` (default: torch's current stream)."""
+        t = self._set_camera(subimage, tasks)
+        if nrows is None:
+            nrows = self.vc.height - row0
+        if out is None:
+            out = torch.empty((nrows, t["ncols"], 3), dtype=torch.float32, device="cuda")
+        if tuple(out.shape) != (nrows, t["ncols"], 3) or out.dtype != torch.float32 or not out.is_cuda \
+                or not out.is_contiguous():
+            raise ValueError("out must be a contiguous float32 CUDA tensor of shape %s" % ((nrows, t["ncols"], 3),))
+        if counters is not None and (counters.numel() < N.RTX_COUNTERS or counters.dtype != torch.int64
+                                     or not counters.is_cuda):
+            raise ValueError("counters must be an int64 CUDA tensor with >= %d entries" % N.RTX_COUNTERS)
+        st = stream if stream is not None else torch.cuda.current_stream()
+        N.call("rtx_render", self._native.h, int(row0), int(nrows), C.c_void_p(out.data_ptr()),
+               C.c_void_p(counters.data_ptr() if counters is not None else 0), C.c_void_p(st.cuda_stream))
+        return out
+
+    def render(self, subimage: int = 0, tasks: int = 1) -> np.ndarray:
+        """scene.py:35-79 — returns float64 (strip_width, height, 3), [column, row-from-bottom]."""
+        fb = self.render_device(subimage, tasks)
+        img = fb.cpu().numpy()
+        return np.ascontiguousarray(np.transpose(img[::-1], (1, 0, 2))).astype(np.float64)
+
+    def render_rgb8(self, subimage=0, tasks=1):
+        """main.py:325-327 on the device: (rot90(image) * 255).astype(uint8), (H, W, 3)."""
+        fb = self.render_device(subimage, tasks)
+        out = torch.empty(fb.shape, dtype=torch.uint8, device=fb.device)
+        N.call("rtx_fb_to_rgb8", C.c_void_p(fb.data_ptr()), C.c_void_p(out.data_ptr()), int(fb.numel()),
+               C.c_void_p(torch.cuda.current_stream().cuda_stream))
+        return out.cpu().numpy()
+
+    # ------------------------------------------------------------------ Geometry ABI (batched)
+    def intersect(self, origins, directions, time=0.0):
+        """Closest hit of rays [n, 3] (Geometry.intersect over all objects + min by time,
+        scene.py:86-94). Returns dict of numpy arrays: t (inf on miss), obj (-1), mat (-1),
+        normal [n, 3], position [n, 3]."""
+        nat = self.native()
+        o = torch.as_tensor(np.ascontiguousarray(np.asarray(origins, np.float32).reshape(-1, 3).T)).cuda()
+        d = torch.as_tensor(np.ascontiguousarray(np.asarray(directions, np.float32).reshape(-1, 3).T)).cuda()
+        n = o.shape[1]
+        t = torch.empty(n, dtype=torch.float64, device="cuda")
+        ob = torch.empty(n, dtype=torch.int32, device="cuda")
+        m = torch.empty(n, dtype=torch.int32, device="cuda")
+        nn = torch.empty((3, n), dtype=torch.float32, device="cuda")
+        pp = torch.empty((3, n), dtype=torch.float32, device="cuda")
+        vp = C.c_void_p
+        N.call("rtx_intersect", nat.h, n, vp(o.data_ptr()), vp(d.data_ptr()), float(time), vp(t.data_ptr()),
+               vp(ob.data_ptr()), vp(m.data_ptr()), vp(nn.data_ptr()), vp(pp.data_ptr()),
+               vp(torch.cuda.current_stream().cuda_stream))
+        return dict(t=t.cpu().numpy(), obj=ob.cpu().numpy(), mat=m.cpu().numpy(),
+                    normal=nn.cpu().numpy().T.copy(), position=pp.cpu().numpy().T.copy())
+
+    def occluded(self, origins, directions, t_max, time=0.0):
+        """Shadow any-hit (Geometry.shadow_intersect over all objects, scene.py:160-164)."""
+        nat = self.native()
+        o = torch.as_tensor(np.ascontiguousarray(np.asarray(origins, np.float32).reshape(-1, 3).T)).cuda()
+        d = torch.as_tensor(np.ascontiguousarray(np.asarray(directions, np.float32).reshape(-1, 3).T)).cuda()
+        n = o.shape[1]
+        tm = torch.as_tensor(np.ascontiguousarray(np.broadcast_to(np.asarray(t_max, np.float64), (n,)))).cuda()
+        occ = torch.empty(n, dtype=torch.uint8, device="cuda")
+        vp = C.c_void_p
+        N.call("rtx_occluded", nat.h, n, vp(o.data_ptr()), vp(d.data_ptr()), vp(tm.data_ptr()), float(time),
+               vp(occ.data_ptr()), vp(torch.cuda.current_stream().cuda_stream))
+        return occ.cpu().numpy().astype(bool)
+
+    @property
+    def samples_per_pixel(self):
+        return self.samples * self.vc.dof_samples * len(self.vc.motion_times)

@@ -1,0 +1,55 @@
+"""Shared helpers for the parity tests."""
+import numpy as np
+
+from oracle import oracle as O
+
+
+def oracle_render(name, res=None, subimage=0, tasks=1, noise=None, tallies=False, **edits):
+    d, base = O.load_bundle(name)
+    if res is not None:
+        d["resolution"] = list(res)
+    for k, v in edits.items():
+        if k == "flat_shaded":
+            for g in d["objects"]:
+                if g["type"] == "mesh":
+                    g["flat_shaded"] = v
+        else:
+            d[k] = v
+    return O.OracleScene(d, base).render(subimage, tasks, noise=noise, tallies=tallies)
+
+
+def product_scene(name, res=None, **edits):
+    import rtx
+    from rtx.io import bundled_scene_dict
+    d = bundled_scene_dict(name, resolution=res)
+    for k, v in edits.items():
+        if k == "flat_shaded":
+            for g in d["objects"]:
+                if g["type"] == "mesh":
+                    g["flat_shaded"] = v
+        else:
+            d[k] = v
+    return rtx.load_scene(d, verbose=False)
+
+
+def compare(img, ref):
+    """Parity statistics of a rendered float image against the oracle's."""
+    assert img.shape == ref.shape, (img.shape, ref.shape)
+    d = np.abs(img - ref).max(axis=2)
+    png = np.abs(O.to_png_array(img).astype(int) - O.to_png_array(ref).astype(int)).max(axis=2)
+    return dict(frac_diff=float((d > 0).mean()), max_abs=float(d.max()), mean_abs=float(d.mean()),
+                png_frac_diff=float((png > 0).mean()), png_max=int(png.max()))
+
+
+# Parity bar (north_star: "within a stated fp32 tolerance of the reference"):
+# the fp32 framebuffer is expected bit-identical; we allow at most 0.1% of pixels to
+# differ (fp64 pow/sqrt last-ulp effects flipping an fp32 rounding or a silhouette)
+# and a mean absolute difference of at most 1e-4 per pixel.
+MAX_FRAC_DIFF = 1e-3
+MAX_MEAN_ABS = 1e-4
+
+
+def assert_parity(img, ref, what=""):
+    s = compare(img, ref)
+    assert s["frac_diff"] <= MAX_FRAC_DIFF and s["mean_abs"] <= MAX_MEAN_ABS, "%s parity: %s" % (what, s)
+    return s

@@ -1,0 +1,76 @@
+"""Tests-only harness: the device source run on the host CPU (tests/native/rtx_hostemu.hip)."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "native", "rtx_hostemu.hip")
+LIB = os.path.join(HERE, "native", "librtx_hostemu.so")
+DEPS = [SRC, os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_api.hip"),
+        os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_trace.h"),
+        os.path.join(HERE, "..", "include", "rtx.h")]
+
+
+def build():
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(p) for p in DEPS):
+        subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-O2", "-std=c++17", "-ffp-contract=off", "-fopenmp",
+                               "-fPIC", "-shared", "-o", LIB, SRC])
+    return LIB
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = C.CDLL(build())
+        vp = C.c_void_p
+        _lib.rtx_hostemu_render.argtypes = [vp, vp, C.c_int32, C.c_int32, vp, vp, C.c_int]
+        _lib.rtx_hostemu_intersect.argtypes = [vp, C.c_int64, vp, vp, C.c_double, vp, vp, vp, vp, vp]
+        _lib.rtx_hostemu_occluded.argtypes = [vp, C.c_int64, vp, vp, vp, C.c_double, vp]
+        _lib.rtx_hostemu_last_error.restype = C.c_char_p
+    return _lib
+
+
+def _chk(rc):
+    if rc != 0:
+        raise RuntimeError("hostemu failed %d: %s" % (rc, lib().rtx_hostemu_last_error().decode()))
+
+
+def render(scene, subimage=0, tasks=1, threads=8):
+    """Same result layout as Scene.render(): float64 (strip_w, H, 3). Returns (image, counters)."""
+    sd = scene.scene_desc()
+    cd, tables = scene.camera_desc(subimage, tasks)
+    H = scene.vc.height
+    fb = np.zeros((H, cd.ncols, 3), np.float32)
+    cnt = np.zeros(16, np.uint64)
+    _chk(lib().rtx_hostemu_render(C.addressof(sd), C.addressof(cd), 0, H, fb.ctypes.data, cnt.ctypes.data, threads))
+    img = np.ascontiguousarray(np.transpose(fb[::-1], (1, 0, 2))).astype(np.float64)
+    return img, cnt
+
+
+def intersect(scene, o, d, time=0.0):
+    sd = scene.scene_desc()
+    o = np.ascontiguousarray(np.asarray(o, np.float32).reshape(-1, 3).T)
+    d = np.ascontiguousarray(np.asarray(d, np.float32).reshape(-1, 3).T)
+    n = o.shape[1]
+    t = np.zeros(n); ob = np.zeros(n, np.int32); m = np.zeros(n, np.int32)
+    nn = np.zeros((3, n), np.float32); pp = np.zeros((3, n), np.float32)
+    _chk(lib().rtx_hostemu_intersect(C.addressof(sd), n, o.ctypes.data, d.ctypes.data, time, t.ctypes.data,
+                                     ob.ctypes.data, m.ctypes.data, nn.ctypes.data, pp.ctypes.data))
+    return dict(t=t, obj=ob, mat=m, normal=nn.T.copy(), position=pp.T.copy())
+
+
+def occluded(scene, o, d, t_max, time=0.0):
+    sd = scene.scene_desc()
+    o = np.ascontiguousarray(np.asarray(o, np.float32).reshape(-1, 3).T)
+    d = np.ascontiguousarray(np.asarray(d, np.float32).reshape(-1, 3).T)
+    n = o.shape[1]
+    tm = np.ascontiguousarray(np.broadcast_to(np.asarray(t_max, np.float64), (n,)))
+    occ = np.zeros(n, np.uint8)
+    _chk(lib().rtx_hostemu_occluded(C.addressof(sd), n, o.ctypes.data, d.ctypes.data, tm.ctypes.data, time,
+                                    occ.ctypes.data))
+    return occ.astype(bool)

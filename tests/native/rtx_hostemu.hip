@@ -1,0 +1,124 @@
+// rtx_hostemu.hip — TESTS ONLY. Runs the device source of librtx.so (rtx_api.hip +
+// rtx_trace.h, unchanged) on the host CPU so kernel logic can be checked against the
+// oracle in a container without a GPU. Not part of the product: the product path
+// (python-raytracer_amd/rtx) never loads this library, and it has no HIP calls.
+#include "../../python-raytracer_amd/csrc/rtx_api.hip"
+
+#include <omp.h>
+
+namespace {
+void bind_view(const HostScene& H, SceneView& v) {
+    v.objs = H.objs.data();
+    v.tris = H.tris.data();
+    v.trins = H.trins.data();
+    v.mats = H.mats.data();
+    v.lights = H.lights.data();
+    v.n_objs = H.n_objs;
+    v.n_lights = H.n_lights;
+    std::memcpy(v.ambient, H.ambient, sizeof(v.ambient));
+}
+}  // namespace
+
+extern "C" int rtx_hostemu_render(const rtx_scene_desc* sd, const rtx_camera_desc* cd, int32_t row0, int32_t nrows,
+                                  float* fb, uint64_t* counters, int threads) {
+    HostScene H;
+    int rc = convert_scene(sd, H);
+    if (rc) return rc;
+    KParams k;
+    if ((rc = convert_camera(cd, k))) return rc;
+    if (row0 < 0 || nrows < 0 || row0 + nrows > cd->height) return fail(RTX_ERR_INVALID, "bad rows");
+    bind_view(H, k.S);
+    std::vector<float> times(cd->n_times);
+    for (int i = 0; i < cd->n_times; ++i) times[i] = (float)cd->times[i];
+    std::vector<float> noise;
+    const size_t nsamp = (size_t)cd->n_dof * cd->n_aa;
+    if (cd->jitter == RTX_JITTER_REPLAY) noise.assign(cd->noise, cd->noise + 3 * (size_t)cd->ncols * cd->height * nsamp);
+    k.xs = cd->xs; k.ys = cd->ys; k.dof_o = cd->dof_origins; k.aa_o = cd->aa_origins; k.times = times.data();
+    k.noise = noise.data();
+    k.fb = fb;
+    k.row0 = row0;
+    k.nrows = nrows;
+    const int64_t npix = (int64_t)nrows * k.ncols;
+    uint64_t tot[RTX_COUNTERS] = {};
+#pragma omp parallel num_threads(threads > 0 ? threads : 1)
+    {
+        uint64_t loc[RTX_COUNTERS] = {};
+#pragma omp for schedule(dynamic, 64)
+        for (int64_t p = 0; p < npix; ++p) {
+            Tally tl = {};
+            if (H.has_mesh) {
+                if (H.has_secondary) render_pixel<true, true, true>(k, p, tl);
+                else render_pixel<true, false, true>(k, p, tl);
+            } else {
+                if (H.has_secondary) render_pixel<false, true, true>(k, p, tl);
+                else render_pixel<false, false, true>(k, p, tl);
+            }
+            for (int q = 0; q < kMaxDepth; ++q) loc[q] += tl.cast[q];
+            loc[RTX_CNT_SHADOW] += tl.shadow;
+            loc[RTX_CNT_SHADE] += tl.shade;
+            loc[RTX_CNT_TRI] += tl.tri;
+        }
+#pragma omp critical
+        for (int q = 0; q < RTX_COUNTERS; ++q) tot[q] += loc[q];
+    }
+    if (counters)
+        for (int q = 0; q < RTX_COUNTERS; ++q) counters[q] = tot[q];
+    return RTX_OK;
+}
+
+extern "C" int rtx_hostemu_intersect(const rtx_scene_desc* sd, int64_t n, const float* ro, const float* rd, double time,
+                                     double* t_out, int32_t* obj_out, int32_t* mat_out, float* n_out, float* p_out) {
+    HostScene H;
+    int rc = convert_scene(sd, H);
+    if (rc) return rc;
+    SceneView v;
+    bind_view(H, v);
+    for (int64_t i = 0; i < n; ++i) {
+        const f3 o = mk(ro[i], ro[n + i], ro[2 * n + i]);
+        const f3 d = mk(rd[i], rd[n + i], rd[2 * n + i]);
+        Tally tl = {};
+        Hit h = H.has_mesh ? closest_hit<true, false>(v, o, d, (float)time, tl) : closest_hit<false, false>(v, o, d, (float)time, tl);
+        int32_t mat = -1;
+        f3 nn = mk(0, 0, 0), pp = mk(0, 0, 0);
+        if (h.obj >= 0) {
+            Surface sf = H.has_mesh ? resolve_hit<true>(v, h, o, d, (float)time) : resolve_hit<false>(v, h, o, d, (float)time);
+            mat = sf.mat; nn = sf.normal; pp = sf.position;
+        }
+        t_out[i] = h.t; obj_out[i] = h.obj; mat_out[i] = mat;
+        n_out[i] = nn.x; n_out[n + i] = nn.y; n_out[2 * n + i] = nn.z;
+        p_out[i] = pp.x; p_out[n + i] = pp.y; p_out[2 * n + i] = pp.z;
+    }
+    return RTX_OK;
+}
+
+extern "C" int rtx_hostemu_occluded(const rtx_scene_desc* sd, int64_t n, const float* ro, const float* rd,
+                                    const double* tmax, double time, uint8_t* occ) {
+    HostScene H;
+    int rc = convert_scene(sd, H);
+    if (rc) return rc;
+    SceneView v;
+    bind_view(H, v);
+    for (int64_t i = 0; i < n; ++i) {
+        const f3 o = mk(ro[i], ro[n + i], ro[2 * n + i]);
+        const f3 d = mk(rd[i], rd[n + i], rd[2 * n + i]);
+        Tally tl = {};
+        bool r = H.has_mesh ? occluded<true, false>(v, o, d, tmax[i], (float)time, tl)
+                            : occluded<false, false>(v, o, d, tmax[i], (float)time, tl);
+        occ[i] = r ? 1 : 0;
+    }
+    return RTX_OK;
+}
+
+extern "C" const char* rtx_hostemu_last_error(void) { return g_last_error.c_str(); }
+
+extern "C" int64_t rtx_hostemu_sizeof(int which) {
+    switch (which) {
+        case 0: return sizeof(rtx_object);
+        case 1: return sizeof(rtx_triangle);
+        case 2: return sizeof(rtx_material);
+        case 3: return sizeof(rtx_light);
+        case 4: return sizeof(rtx_scene_desc);
+        case 5: return sizeof(rtx_camera_desc);
+    }
+    return -1;
+}

@@ -1,0 +1,26 @@
+#!/bin/bash
+# One GPU session: smoke, GPU tests, bench, rocprofv3 kernel trace. Every GPU step has
+# its own time limit; the script stops at the first fault/abort/timeout (exit >= 2 from
+# pytest, or any non-zero from other steps).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${TAG:-s1}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {  # step NAME SECONDS CMD...
+  local name=$1 secs=$2; shift 2
+  echo "== $name" ; date
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "rc=$rc"; tail -5 "$OUT/$name.log"
+  return $rc
+}
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
+step pytest_gpu 600 python -m pytest tests -m gpu -q -rf -p no:cacheprovider
+rc=$?; [ $rc -le 1 ] || exit $rc
+step bench 300 python bench.py --steps 20 --warmup 5 --cpu-seconds 5 || exit 1
+for c in ${CONFIGS:-}; do
+  step bench_$c 300 python bench.py --config $c --steps 10 --warmup 3 --no-cpu-baseline || exit 1
+done
+step rocprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline || exit 1
+echo ALL_DONE
