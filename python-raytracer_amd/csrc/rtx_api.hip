@@ -47,11 +47,9 @@ struct KParams {
     const float* __restrict__ aa_o;    // [n_dof][n_aa][3]
     const float* __restrict__ times;   // [n_times] fp32
     const float* __restrict__ noise;   // replay jitter
-    float* __restrict__ fb;
-    unsigned long long* __restrict__ counters;
     float pos[4], u[4], v[4], dw[4];
     float focal, divisor, jscale, pad;
-    int32_t width, height, col0, ncols, row0, nrows;
+    int32_t width, height, col0, ncols;
     int32_t n_dof, n_aa, n_times, jitter;
     uint32_t seed_lo, seed_hi;
 };
@@ -78,10 +76,10 @@ __device__ __forceinline__ void flush_tally(const Tally& tl, unsigned long long*
 // scene.py:47-79 for pixel p of the output block (host/device: the tests-only host
 // emulation runs the same body).
 template <bool MESH, bool SEC, bool COUNT>
-RTX_HD void render_pixel(const KParams& P, int64_t p, Tally& tl) {
+RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int64_t p, Tally& tl) {
     const int rr = (int)(p / P.ncols);
     const int cc = (int)(p - (int64_t)rr * P.ncols);
-    const int j = P.height - 1 - (P.row0 + rr);  // reference row index (y grows upward)
+    const int j = P.height - 1 - (row0 + rr);  // reference row index (y grows upward)
     const float fx = P.xs[cc];
     const float fy = P.ys[j];
     // base_ray_direction = normalize(x * u + y * v - d * w)  (scene.py:54)
@@ -110,20 +108,28 @@ RTX_HD void render_pixel(const KParams& P, int64_t p, Tally& tl) {
         }
     }
     colour = divs(colour, P.divisor);  // scene.py:73
-    float* out = P.fb + 3 * p;
+    float* out = fb + 3 * p;
     out[0] = colour.x;
     out[1] = colour.y;
     out[2] = colour.z;
 }
 
+// The per-frame parameters live in device memory (uploaded by rtx_camera_set) and are
+// read with scalar loads; only the per-call output block is passed by value.
+struct Launch {
+    float* fb;
+    unsigned long long* counters;
+    int32_t row0, nrows;
+};
+
 template <bool MESH, bool SEC, bool COUNT>
-__global__ __launch_bounds__(256) void k_render(const KParams P) {
-    const int64_t npix = (int64_t)P.nrows * P.ncols;
+__global__ __launch_bounds__(256) void k_render(const KParams* __restrict__ Pp, const Launch L) {
+    const int64_t npix = (int64_t)L.nrows * Pp->ncols;
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool active = p < npix;
     Tally tl = {};
-    if (active) render_pixel<MESH, SEC, COUNT>(P, p, tl);
-    flush_tally<COUNT>(tl, P.counters, active);
+    if (active) render_pixel<MESH, SEC, COUNT>(*Pp, L.fb, L.row0, p, tl);
+    flush_tally<COUNT>(tl, L.counters, active);
 }
 
 template <bool MESH>
@@ -145,7 +151,7 @@ __global__ __launch_bounds__(256) void k_intersect(SceneView S, int64_t n, const
         pp = sf.position;
     }
     if (t_out) t_out[i] = h.t;
-    if (obj_out) obj_out[i] = h.obj;
+    if (obj_out) obj_out[i] = h.obj >= 0 ? h.oid : -1;
     if (mat_out) mat_out[i] = mat;
     if (n_out) { n_out[i] = nn.x; n_out[n + i] = nn.y; n_out[2 * n + i] = nn.z; }
     if (p_out) { p_out[i] = pp.x; p_out[n + i] = pp.y; p_out[2 * n + i] = pp.z; }
@@ -188,6 +194,7 @@ struct HostScene {
     std::vector<DLight> lights;
     bool has_mesh = false, has_secondary = false;
     int32_t n_objs = 0, n_lights = 0;
+    int32_t n_plane = 0, n_sphere = 0, n_box = 0, n_mesh = 0;
     float ambient[4] = {0, 0, 0, 0};
 };
 
@@ -305,6 +312,22 @@ int convert_scene(const rtx_scene_desc* desc, HostScene& H) {
                 return fail(RTX_ERR_INVALID, tag + "bad type");
         }
     }
+    // Group by type (planes, spheres, boxes, meshes), keeping scene order within a group;
+    // `oid` remembers the scene-order position for closest-hit ties.
+    std::vector<DObj> grouped;
+    grouped.reserve(H.objs.size());
+    const int32_t order[4] = {RTX_PLANE, RTX_SPHERE, RTX_BOX, RTX_MESH};
+    int32_t counts[4] = {0, 0, 0, 0};
+    for (int g = 0; g < 4; ++g)
+        for (int i = 0; i < desc->n_objects; ++i)
+            if (H.objs[i].type == order[g]) {
+                DObj d = H.objs[i];
+                d.oid = i;
+                grouped.push_back(d);
+                counts[g]++;
+            }
+    H.objs.swap(grouped);
+    H.n_plane = counts[0]; H.n_sphere = counts[1]; H.n_box = counts[2]; H.n_mesh = counts[3];
     H.n_objs = desc->n_objects;
     H.n_lights = desc->n_lights;
     set3(H.ambient, desc->ambient);
@@ -364,6 +387,7 @@ struct rtx_scene {
     float* d_aa = nullptr;
     float* d_times = nullptr;
     float* d_noise = nullptr;
+    KParams* d_kp = nullptr;
 };
 
 namespace {
@@ -378,7 +402,9 @@ int upload(void** dptr, const std::vector<T>& v) {
 
 void free_camera(rtx_scene* s) {
     for (float* p : {s->d_xs, s->d_ys, s->d_dof, s->d_aa, s->d_times, s->d_noise}) (void)hipFree(p);
+    (void)hipFree(s->d_kp);
     s->d_xs = s->d_ys = s->d_dof = s->d_aa = s->d_times = s->d_noise = nullptr;
+    s->d_kp = nullptr;
     s->cam_set = false;
 }
 
@@ -419,6 +445,7 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
     v.lights = (const DLight*)s->d_lights;
     v.n_objs = H.n_objs;
     v.n_lights = H.n_lights;
+    v.n_plane = H.n_plane; v.n_sphere = H.n_sphere; v.n_box = H.n_box; v.n_mesh = H.n_mesh;
     std::memcpy(v.ambient, H.ambient, sizeof(v.ambient));
     *out = s;
     return RTX_OK;
@@ -452,6 +479,8 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
         return rc;
     k.S = s->view;
     k.xs = s->d_xs; k.ys = s->d_ys; k.dof_o = s->d_dof; k.aa_o = s->d_aa; k.times = s->d_times; k.noise = s->d_noise;
+    RTX_HIP(hipMalloc((void**)&s->d_kp, sizeof(KParams)));
+    RTX_HIP(hipMemcpy(s->d_kp, &k, sizeof(KParams), hipMemcpyHostToDevice));
     s->kp = k;
     s->cam_set = true;
     return RTX_OK;
@@ -464,25 +493,26 @@ int rtx_render(rtx_scene* s, int32_t row0, int32_t nrows, float* fb_dev, uint64_
         return fail(RTX_ERR_INVALID, "rtx_render: row range outside the image");
     if (nrows == 0) return RTX_OK;
     if (!fb_dev) return fail(RTX_ERR_INVALID, "rtx_render: null framebuffer");
-    KParams k = s->kp;
-    k.fb = fb_dev;
-    k.row0 = row0;
-    k.nrows = nrows;
-    k.counters = reinterpret_cast<unsigned long long*>(counters_dev);
-    const int64_t npix = (int64_t)nrows * k.ncols;
+    Launch L;
+    L.fb = fb_dev;
+    L.row0 = row0;
+    L.nrows = nrows;
+    L.counters = reinterpret_cast<unsigned long long*>(counters_dev);
+    const int64_t npix = (int64_t)nrows * s->kp.ncols;
     const dim3 grid((unsigned)((npix + 255) / 256)), block(256);
     hipStream_t st = (hipStream_t)stream;
     const bool cnt = counters_dev != nullptr;
     const int sel = (s->has_mesh ? 4 : 0) | (s->has_secondary ? 2 : 0) | (cnt ? 1 : 0);
+    const KParams* kp = s->d_kp;
     switch (sel) {
-        case 0: hipLaunchKernelGGL((k_render<false, false, false>), grid, block, 0, st, k); break;
-        case 1: hipLaunchKernelGGL((k_render<false, false, true>), grid, block, 0, st, k); break;
-        case 2: hipLaunchKernelGGL((k_render<false, true, false>), grid, block, 0, st, k); break;
-        case 3: hipLaunchKernelGGL((k_render<false, true, true>), grid, block, 0, st, k); break;
-        case 4: hipLaunchKernelGGL((k_render<true, false, false>), grid, block, 0, st, k); break;
-        case 5: hipLaunchKernelGGL((k_render<true, false, true>), grid, block, 0, st, k); break;
-        case 6: hipLaunchKernelGGL((k_render<true, true, false>), grid, block, 0, st, k); break;
-        case 7: hipLaunchKernelGGL((k_render<true, true, true>), grid, block, 0, st, k); break;
+        case 0: hipLaunchKernelGGL((k_render<false, false, false>), grid, block, 0, st, kp, L); break;
+        case 1: hipLaunchKernelGGL((k_render<false, false, true>), grid, block, 0, st, kp, L); break;
+        case 2: hipLaunchKernelGGL((k_render<false, true, false>), grid, block, 0, st, kp, L); break;
+        case 3: hipLaunchKernelGGL((k_render<false, true, true>), grid, block, 0, st, kp, L); break;
+        case 4: hipLaunchKernelGGL((k_render<true, false, false>), grid, block, 0, st, kp, L); break;
+        case 5: hipLaunchKernelGGL((k_render<true, false, true>), grid, block, 0, st, kp, L); break;
+        case 6: hipLaunchKernelGGL((k_render<true, true, false>), grid, block, 0, st, kp, L); break;
+        case 7: hipLaunchKernelGGL((k_render<true, true, true>), grid, block, 0, st, kp, L); break;
     }
     RTX_HIP(hipGetLastError());
     return RTX_OK;

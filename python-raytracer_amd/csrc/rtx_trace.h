@@ -64,10 +64,12 @@ RTX_HD f3 clamp01(f3 c) { return f3{clamp01(c.x), clamp01(c.y), clamp01(c.z)}; }
 // ------------------------------------------------------------------ device scene records
 // Library-internal layouts (not ABI). Derived values are computed once on the host by
 // rtx_api.hip with the same fp32 operation order as the reference computes them per ray.
+// Objects are stored grouped by type (planes, spheres, boxes, meshes); `oid` is the
+// object's position in the scene list, which decides closest-hit ties.
 struct alignas(16) DObj {
     int32_t type, nmat, mat0, mat1;
     int32_t has_speed, tri_begin, tri_count, bv_type;
-    int32_t flat, pad0, pad1, pad2;
+    int32_t flat, oid, pad1, pad2;
     float a[4];       // sphere centre | plane point | box minpos
     float b[4];       // plane normal | box maxpos
     float c[4];       // plane width axis
@@ -113,12 +115,13 @@ enum : int32_t { LIGHT_POINT = 0, LIGHT_DIRECTIONAL = 1 };
 enum : int32_t { BV_AABB = 0, BV_SPHERE = 1 };
 
 struct SceneView {
-    const DObj* __restrict__ objs;
+    const DObj* __restrict__ objs;   // [planes | spheres | boxes | meshes]
     const DTri* __restrict__ tris;
     const DTriN* __restrict__ trins;
     const DMat* __restrict__ mats;
     const DLight* __restrict__ lights;
     int32_t n_objs, n_lights;
+    int32_t n_plane, n_sphere, n_box, n_mesh;
     float ambient[4];
 };
 
@@ -144,13 +147,21 @@ RTX_HD f3 moved(const DObj& o, const float* p, float time) {
 // Ray.getPoint(t) = origin + direction * t, t cast to fp32 (helperclasses.py:21-22)
 RTX_HD f3 get_point(f3 o, f3 d, double t) { return add(o, scale(d, (float)t)); }
 
-// Closest-hit record: t (fp64, as the reference compares it), object, sub-index
-// (box: entry slab label; mesh: face index).
+// Closest-hit record: t (fp64, as the reference compares it), object (index into the
+// type-grouped array), its scene-order id, and a sub-index (box: entry slab label; mesh:
+// face index).
 struct Hit {
     double t;
     int32_t obj;
+    int32_t oid;
     int32_t sub;
 };
+
+// min(intersections, key=time) keeps the FIRST minimum of the list, which is ordered by
+// object and then by hit within the object (scene.py:86-94). Each object contributes only
+// its own first minimum, so comparing (t, scene-order id) lexicographically selects the
+// same hit in any visiting order.
+RTX_HD bool closer(double t, int32_t oid, const Hit& h) { return t < h.t || (t == h.t && oid < h.oid); }
 
 // Sphere quadratic (simple_geometry.py:29-39); returns false when disc < 0.
 RTX_HD bool sphere_roots(f3 o, f3 d, f3 c, double r2, double& b, double& s, double& two_a) {
@@ -216,106 +227,118 @@ RTX_HD bool mesh_bv(const DObj& ob, f3 o, f3 d) {
 }
 
 // ------------------------------------------------------------------ closest hit
-// All objects in scene order; the first strict minimum wins (scene.py:86-94).
+template <bool COUNT>
+RTX_HD void mesh_closest(const SceneView& S, const DObj& ob, int oi, f3 o, f3 d, Hit& h, Tally& tl) {
+    // mesh.py:72-119: every face in order; the first strict minimum within the mesh wins.
+    if (!mesh_bv(ob, o, d)) return;
+    const int32_t f0 = ob.tri_begin, nf = ob.tri_count;
+    double best = INFINITY;
+    int32_t bf = -1;
+    for (int f = 0; f < nf; ++f) {
+        const DTri& T = S.tris[f0 + f];
+        tally_inc<COUNT>(tl, &Tally::tri);
+        f3 n = ld3(T.n);
+        float denom = dot(d, n);
+        if (fabs((double)denom) < 1e-4) continue;
+        f3 v0 = ld3(T.v0);
+        double t = (double)dot(sub(v0, o), n) / (double)denom;
+        if (t < 0.0) continue;
+        f3 p = get_point(o, d, t);
+        float b0 = dot(cross(ld3(T.e01), sub(p, v0)), n);
+        float b1 = dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n);
+        float b2 = dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n);
+        if (b0 >= 0.0f && b1 >= 0.0f && b2 >= 0.0f && t < best) { best = t; bf = f; }
+    }
+    if (bf >= 0 && closer(best, ob.oid, h)) { h.t = best; h.obj = oi; h.oid = ob.oid; h.sub = bf; }
+}
+
 template <bool MESH, bool COUNT>
 RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl) {
-    Hit h{INFINITY, -1, 0};
-    for (int oi = 0; oi < S.n_objs; ++oi) {
+    Hit h{INFINITY, -1, 0x7fffffff, 0};
+    int oi = 0;
+    for (int k = 0; k < S.n_plane; ++k, ++oi) {  // simple_geometry.py:105-120
         const DObj& ob = S.objs[oi];
-        const int32_t type = ob.type;
-        if (type == OBJ_SPHERE) {  // simple_geometry.py:20-46
-            double b, s, two_a;
-            if (sphere_roots(o, d, moved(ob, ob.a, time), ob.r2, b, s, two_a)) {
-                double t1 = (-b - s) / two_a;
-                if (t1 > 0.0) {
-                    if (t1 < h.t) { h.t = t1; h.obj = oi; h.sub = 0; }
-                } else {
-                    double t2 = (-b + s) / two_a;
-                    if (t2 > 0.0 && t2 < h.t) { h.t = t2; h.obj = oi; h.sub = 1; }
-                }
-            }
-        } else if (type == OBJ_PLANE) {  // simple_geometry.py:105-120
-            f3 n = ld3(ob.b);
-            float denom = dot(d, n);
-            if (fabs((double)denom) > 1e-4) {
-                double t = (double)dot(sub(moved(ob, ob.a, time), o), n) / (double)denom;
-                if (t >= 0.0 && t < h.t) { h.t = t; h.obj = oi; h.sub = 0; }
-            }
-        } else if (type == OBJ_BOX) {  // simple_geometry.py:188-249 (entry precedes exit)
-            double start, end;
-            int label;
-            if (box_slabs(o, d, moved(ob, ob.a, time), moved(ob, ob.b, time), start, label, end)) {
-                if (!(start > end || start < 0.0) && start < h.t) { h.t = start; h.obj = oi; h.sub = label; }
-            }
-        } else if (MESH && type == OBJ_MESH) {  // mesh.py:72-119
-            if (mesh_bv(ob, o, d)) {
-                const int32_t f0 = ob.tri_begin, nf = ob.tri_count;
-                for (int f = 0; f < nf; ++f) {
-                    const DTri& T = S.tris[f0 + f];
-                    tally_inc<COUNT>(tl, &Tally::tri);
-                    f3 n = ld3(T.n);
-                    float denom = dot(d, n);
-                    if (fabs((double)denom) < 1e-4) continue;
-                    f3 v0 = ld3(T.v0);
-                    double t = (double)dot(sub(v0, o), n) / (double)denom;
-                    if (t < 0.0) continue;
-                    f3 p = get_point(o, d, t);
-                    float b0 = dot(cross(ld3(T.e01), sub(p, v0)), n);
-                    float b1 = dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n);
-                    float b2 = dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n);
-                    if (b0 >= 0.0f && b1 >= 0.0f && b2 >= 0.0f && t < h.t) { h.t = t; h.obj = oi; h.sub = f; }
-                }
-            }
+        f3 n = ld3(ob.b);
+        float denom = dot(d, n);
+        if (fabs((double)denom) > 1e-4) {
+            double t = (double)dot(sub(moved(ob, ob.a, time), o), n) / (double)denom;
+            if (t >= 0.0 && closer(t, ob.oid, h)) { h.t = t; h.obj = oi; h.oid = ob.oid; h.sub = 0; }
         }
     }
+    for (int k = 0; k < S.n_sphere; ++k, ++oi) {  // simple_geometry.py:20-46
+        const DObj& ob = S.objs[oi];
+        double b, s, two_a;
+        if (sphere_roots(o, d, moved(ob, ob.a, time), ob.r2, b, s, two_a)) {
+            double t = (-b - s) / two_a;
+            int32_t root = 0;
+            if (!(t > 0.0)) { t = (-b + s) / two_a; root = 1; }
+            if (t > 0.0 && closer(t, ob.oid, h)) { h.t = t; h.obj = oi; h.oid = ob.oid; h.sub = root; }
+        }
+    }
+    for (int k = 0; k < S.n_box; ++k, ++oi) {  // simple_geometry.py:188-249 (entry precedes exit)
+        const DObj& ob = S.objs[oi];
+        double start, end;
+        int label;
+        if (box_slabs(o, d, moved(ob, ob.a, time), moved(ob, ob.b, time), start, label, end)) {
+            if (!(start > end || start < 0.0) && closer(start, ob.oid, h)) { h.t = start; h.obj = oi; h.oid = ob.oid; h.sub = label; }
+        }
+    }
+    if (MESH)
+        for (int k = 0; k < S.n_mesh; ++k, ++oi) mesh_closest<COUNT>(S, S.objs[oi], oi, o, d, h, tl);
     return h;
 }
 
 // ------------------------------------------------------------------ shadow any-hit
+// Any order gives the same answer; cheap objects first.
 template <bool MESH, bool COUNT>
 RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, Tally& tl) {
-    for (int oi = 0; oi < S.n_objs; ++oi) {
+    int oi = 0;
+    for (int k = 0; k < S.n_plane; ++k, ++oi) {  // simple_geometry.py:122-131
         const DObj& ob = S.objs[oi];
-        const int32_t type = ob.type;
-        if (type == OBJ_SPHERE) {  // simple_geometry.py:48-72 (shadow_epsilon 1e-3)
-            double b, s, two_a;
-            if (sphere_roots(o, d, moved(ob, ob.a, time), ob.r2, b, s, two_a)) {
-                double t = (-b - s) / two_a;
-                if (1e-3 < t && t < t_max) return true;
-                t = (-b + s) / two_a;
-                if (1e-3 < t && t < t_max) return true;
-            }
-        } else if (type == OBJ_PLANE) {  // simple_geometry.py:122-131
-            f3 n = ld3(ob.b);
-            float denom = dot(d, n);
-            if (fabs((double)denom) > 1e-4) {
-                double t = (double)dot(sub(moved(ob, ob.a, time), o), n) / (double)denom;
-                if (1e-4 < t && t < t_max) return true;
-            }
-        } else if (type == OBJ_BOX) {  // simple_geometry.py:251-294
-            double start, end;
-            int label;
-            if (box_slabs(o, d, moved(ob, ob.a, time), moved(ob, ob.b, time), start, label, end)) {
-                if (!(start > end) && 1e-4 < start && start < t_max) return true;
-            }
-        } else if (MESH && type == OBJ_MESH) {  // mesh.py:121-153 (no t_max test)
-            if (mesh_bv(ob, o, d)) {
-                const int32_t f0 = ob.tri_begin, nf = ob.tri_count;
-                for (int f = 0; f < nf; ++f) {
-                    const DTri& T = S.tris[f0 + f];
-                    tally_inc<COUNT>(tl, &Tally::tri);
-                    f3 n = ld3(T.nu);
-                    float denom = dot(d, n);
-                    if (fabs((double)denom) < 1e-4) continue;
-                    f3 v0 = ld3(T.v0);
-                    double t = (double)dot(sub(v0, o), n) / (double)denom;
-                    if (t < 1e-4) continue;
-                    f3 p = get_point(o, d, t);
-                    if (dot(cross(ld3(T.e01), sub(p, v0)), n) >= 0.0f &&
-                        dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n) >= 0.0f &&
-                        dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n) >= 0.0f)
-                        return true;
-                }
+        f3 n = ld3(ob.b);
+        float denom = dot(d, n);
+        if (fabs((double)denom) > 1e-4) {
+            double t = (double)dot(sub(moved(ob, ob.a, time), o), n) / (double)denom;
+            if (1e-4 < t && t < t_max) return true;
+        }
+    }
+    for (int k = 0; k < S.n_sphere; ++k, ++oi) {  // simple_geometry.py:48-72 (shadow_epsilon 1e-3)
+        const DObj& ob = S.objs[oi];
+        double b, s, two_a;
+        if (sphere_roots(o, d, moved(ob, ob.a, time), ob.r2, b, s, two_a)) {
+            double t = (-b - s) / two_a;
+            if (1e-3 < t && t < t_max) return true;
+            t = (-b + s) / two_a;
+            if (1e-3 < t && t < t_max) return true;
+        }
+    }
+    for (int k = 0; k < S.n_box; ++k, ++oi) {  // simple_geometry.py:251-294
+        const DObj& ob = S.objs[oi];
+        double start, end;
+        int label;
+        if (box_slabs(o, d, moved(ob, ob.a, time), moved(ob, ob.b, time), start, label, end)) {
+            if (!(start > end) && 1e-4 < start && start < t_max) return true;
+        }
+    }
+    if (MESH) {
+        for (int k = 0; k < S.n_mesh; ++k, ++oi) {  // mesh.py:121-153 (no t_max test)
+            const DObj& ob = S.objs[oi];
+            if (!mesh_bv(ob, o, d)) continue;
+            const int32_t f0 = ob.tri_begin, nf = ob.tri_count;
+            for (int f = 0; f < nf; ++f) {
+                const DTri& T = S.tris[f0 + f];
+                tally_inc<COUNT>(tl, &Tally::tri);
+                f3 n = ld3(T.nu);
+                float denom = dot(d, n);
+                if (fabs((double)denom) < 1e-4) continue;
+                f3 v0 = ld3(T.v0);
+                double t = (double)dot(sub(v0, o), n) / (double)denom;
+                if (t < 1e-4) continue;
+                f3 p = get_point(o, d, t);
+                if (dot(cross(ld3(T.e01), sub(p, v0)), n) >= 0.0f &&
+                    dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n) >= 0.0f &&
+                    dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n) >= 0.0f)
+                    return true;
             }
         }
     }

@@ -15,6 +15,7 @@ void bind_view(const HostScene& H, SceneView& v) {
     v.lights = H.lights.data();
     v.n_objs = H.n_objs;
     v.n_lights = H.n_lights;
+    v.n_plane = H.n_plane; v.n_sphere = H.n_sphere; v.n_box = H.n_box; v.n_mesh = H.n_mesh;
     std::memcpy(v.ambient, H.ambient, sizeof(v.ambient));
 }
 }  // namespace
@@ -35,9 +36,6 @@ extern "C" int rtx_hostemu_render(const rtx_scene_desc* sd, const rtx_camera_des
     if (cd->jitter == RTX_JITTER_REPLAY) noise.assign(cd->noise, cd->noise + 3 * (size_t)cd->ncols * cd->height * nsamp);
     k.xs = cd->xs; k.ys = cd->ys; k.dof_o = cd->dof_origins; k.aa_o = cd->aa_origins; k.times = times.data();
     k.noise = noise.data();
-    k.fb = fb;
-    k.row0 = row0;
-    k.nrows = nrows;
     const int64_t npix = (int64_t)nrows * k.ncols;
     uint64_t tot[RTX_COUNTERS] = {};
 #pragma omp parallel num_threads(threads > 0 ? threads : 1)
@@ -47,11 +45,11 @@ extern "C" int rtx_hostemu_render(const rtx_scene_desc* sd, const rtx_camera_des
         for (int64_t p = 0; p < npix; ++p) {
             Tally tl = {};
             if (H.has_mesh) {
-                if (H.has_secondary) render_pixel<true, true, true>(k, p, tl);
-                else render_pixel<true, false, true>(k, p, tl);
+                if (H.has_secondary) render_pixel<true, true, true>(k, fb, row0, p, tl);
+                else render_pixel<true, false, true>(k, fb, row0, p, tl);
             } else {
-                if (H.has_secondary) render_pixel<false, true, true>(k, p, tl);
-                else render_pixel<false, false, true>(k, p, tl);
+                if (H.has_secondary) render_pixel<false, true, true>(k, fb, row0, p, tl);
+                else render_pixel<false, false, true>(k, fb, row0, p, tl);
             }
             for (int q = 0; q < kMaxDepth; ++q) loc[q] += tl.cast[q];
             loc[RTX_CNT_SHADOW] += tl.shadow;
@@ -84,7 +82,7 @@ extern "C" int rtx_hostemu_intersect(const rtx_scene_desc* sd, int64_t n, const 
             Surface sf = H.has_mesh ? resolve_hit<true>(v, h, o, d, (float)time) : resolve_hit<false>(v, h, o, d, (float)time);
             mat = sf.mat; nn = sf.normal; pp = sf.position;
         }
-        t_out[i] = h.t; obj_out[i] = h.obj; mat_out[i] = mat;
+        t_out[i] = h.t; obj_out[i] = h.obj >= 0 ? h.oid : -1; mat_out[i] = mat;
         n_out[i] = nn.x; n_out[n + i] = nn.y; n_out[2 * n + i] = nn.z;
         p_out[i] = pp.x; p_out[n + i] = pp.y; p_out[2 * n + i] = pp.z;
     }

@@ -1,0 +1,24 @@
+"""Minimal render loop for rocprofv3 runs: N frames of a bench config on cuda:0."""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "python-raytracer_amd"))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+p = argparse.ArgumentParser()
+p.add_argument("--config", default="tsp1080")
+p.add_argument("--iters", type=int, default=10)
+a = p.parse_args()
+torch.cuda.set_device(0)
+sc = bench.make_scene(a.config)
+fb = torch.empty((sc.vc.height, sc.vc.width, 3), dtype=torch.float32, device="cuda")
+for _ in range(a.iters):
+    sc.render_device(out=fb)
+torch.cuda.synchronize()
+print("done", a.config, a.iters)
