@@ -41,12 +41,12 @@ int fail(int code, const std::string& msg) {
 struct KParams {
     SceneView S;
     // camera tables (device)
-    const float* __restrict__ xs;
-    const float* __restrict__ ys;
-    const float* __restrict__ dof_o;   // [n_dof][3]
-    const float* __restrict__ aa_o;    // [n_dof][n_aa][3]
-    const float* __restrict__ times;   // [n_times] fp32
-    const float* __restrict__ noise;   // replay jitter
+    cptr<float> xs;
+    cptr<float> ys;
+    cptr<float> dof_o;   // [n_dof][3]
+    cptr<float> aa_o;    // [n_dof][n_aa][3]
+    cptr<float> times;   // [n_times] fp32
+    cptr<float> noise;   // replay jitter
     float pos[4], u[4], v[4], dw[4];
     float focal, divisor, jscale, pad;
     int32_t width, height, col0, ncols;
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void k_intersect(SceneView S, int64_t n, const
         nn = sf.normal;
         pp = sf.position;
     }
-    if (t_out) t_out[i] = h.t;
+    if (t_out) t_out[i] = h.obj >= 0 ? exact_t(h) : (double)INFINITY;
     if (obj_out) obj_out[i] = h.obj >= 0 ? h.oid : -1;
     if (mat_out) mat_out[i] = mat;
     if (n_out) { n_out[i] = nn.x; n_out[n + i] = nn.y; n_out[2 * n + i] = nn.z; }
@@ -438,11 +438,11 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
     s->has_mesh = H.has_mesh;
     s->has_secondary = H.has_secondary;
     SceneView& v = s->view;
-    v.objs = (const DObj*)s->d_objs;
-    v.tris = (const DTri*)s->d_tris;
-    v.trins = (const DTriN*)s->d_trins;
-    v.mats = (const DMat*)s->d_mats;
-    v.lights = (const DLight*)s->d_lights;
+    v.objs = (cptr<DObj>)s->d_objs;
+    v.tris = (cptr<DTri>)s->d_tris;
+    v.trins = (cptr<DTriN>)s->d_trins;
+    v.mats = (cptr<DMat>)s->d_mats;
+    v.lights = (cptr<DLight>)s->d_lights;
     v.n_objs = H.n_objs;
     v.n_lights = H.n_lights;
     v.n_plane = H.n_plane; v.n_sphere = H.n_sphere; v.n_box = H.n_box; v.n_mesh = H.n_mesh;
@@ -478,7 +478,8 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     if (c->jitter == RTX_JITTER_REPLAY && (rc = up(&s->d_noise, c->noise, 3 * (size_t)c->ncols * c->height * nsamp)))
         return rc;
     k.S = s->view;
-    k.xs = s->d_xs; k.ys = s->d_ys; k.dof_o = s->d_dof; k.aa_o = s->d_aa; k.times = s->d_times; k.noise = s->d_noise;
+    k.xs = (cptr<float>)s->d_xs; k.ys = (cptr<float>)s->d_ys; k.dof_o = (cptr<float>)s->d_dof;
+    k.aa_o = (cptr<float>)s->d_aa; k.times = (cptr<float>)s->d_times; k.noise = (cptr<float>)s->d_noise;
     RTX_HIP(hipMalloc((void**)&s->d_kp, sizeof(KParams)));
     RTX_HIP(hipMemcpy(s->d_kp, &k, sizeof(KParams), hipMemcpyHostToDevice));
     s->kp = k;

@@ -12,6 +12,15 @@
 
 #define RTX_HD __host__ __device__ __forceinline__
 
+// Read-only scene and camera tables are addressed as the AMDGPU constant address space in
+// device code: wave-uniform reads of them become scalar (s_load) reads through the
+// constant cache. The host-emulation build (tests only) sees plain pointers.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RTX_CONST __attribute__((address_space(4)))
+#else
+#define RTX_CONST
+#endif
+
 namespace rtx {
 
 constexpr int kMaxDepth = 10;  // cast_ray(max_recursion=10) (scene.py:81)
@@ -22,6 +31,9 @@ struct f3 {
 };
 RTX_HD f3 mk(float x, float y, float z) { return f3{x, y, z}; }
 RTX_HD f3 ld3(const float* p) { return f3{p[0], p[1], p[2]}; }
+#if defined(__HIP_DEVICE_COMPILE__)
+RTX_HD f3 ld3(const float RTX_CONST* p) { return f3{p[0], p[1], p[2]}; }
+#endif
 RTX_HD f3 add(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
 RTX_HD f3 sub(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
 RTX_HD f3 mul(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
@@ -114,12 +126,15 @@ enum : int32_t { MAT_DIFFUSE = 0, MAT_MIRROR = 1, MAT_REFRACTIVE = 2 };
 enum : int32_t { LIGHT_POINT = 0, LIGHT_DIRECTIONAL = 1 };
 enum : int32_t { BV_AABB = 0, BV_SPHERE = 1 };
 
+template <class T>
+using cptr = const T RTX_CONST*;
+
 struct SceneView {
-    const DObj* __restrict__ objs;   // [planes | spheres | boxes | meshes]
-    const DTri* __restrict__ tris;
-    const DTriN* __restrict__ trins;
-    const DMat* __restrict__ mats;
-    const DLight* __restrict__ lights;
+    cptr<DObj> objs;   // [planes | spheres | boxes | meshes]
+    cptr<DTri> tris;
+    cptr<DTriN> trins;
+    cptr<DMat> mats;
+    cptr<DLight> lights;
     int32_t n_objs, n_lights;
     int32_t n_plane, n_sphere, n_box, n_mesh;
     float ambient[4];
@@ -147,21 +162,63 @@ RTX_HD f3 moved(const DObj& o, const float* p, float time) {
 // Ray.getPoint(t) = origin + direction * t, t cast to fp32 (helperclasses.py:21-22)
 RTX_HD f3 get_point(f3 o, f3 d, double t) { return add(o, scale(d, (float)t)); }
 
-// Closest-hit record: t (fp64, as the reference compares it), object (index into the
-// type-grouped array), its scene-order id, and a sub-index (box: entry slab label; mesh:
-// face index).
+// ------------------------------------------------------------------ exact fp32 proxies
+// Every `t` the reference compares is an fp64 value t64. We carry t32 = fl32(t64):
+//  * for plane/triangle hits t64 = fl64(num / den) of two floats, and fl32(fl64(q)) =
+//    fl32(q) (double rounding is innocuous when 53 >= 2*24 + 2), so t32 is one IEEE fp32
+//    division and getPoint(t64) = o + d * t32 exactly;
+//  * fl32 is monotone and equal t64 give equal t32, so t32a < t32b implies t64a < t64b
+//    and t32 > fl32(T) implies t64 > T. Only EQUAL proxies need the fp64 values.
+// 1e-4 and 1e-3 are not floats: |x| > 1e-4 for a float x  <=>  |x| >= kEps4Up.
+constexpr float kEps4Up = 0x1.a36e3p-14f;      // smallest float > 1e-4
+constexpr float kEps4Near = 1e-4f;             // fl32(1e-4) (< 1e-4)
+constexpr float kEps3Near = 1e-3f;             // fl32(1e-3)
+
+// Closest-hit record: t as its fp32 proxy plus what is needed to recover the exact fp64
+// value (t64 for spheres/boxes; num/den for planes/triangles), the object (index into
+// the type-grouped array), its scene-order id, and a sub-index (box: entry slab label;
+// mesh: face index).
 struct Hit {
-    double t;
+    float t32;
+    float num, den;    // q = num / den when quot != 0
+    int32_t quot;
+    double t64;        // exact value when quot == 0
     int32_t obj;
     int32_t oid;
     int32_t sub;
 };
 
+RTX_HD double exact_t(const Hit& h) { return h.quot ? (double)h.num / (double)h.den : h.t64; }
+
 // min(intersections, key=time) keeps the FIRST minimum of the list, which is ordered by
 // object and then by hit within the object (scene.py:86-94). Each object contributes only
 // its own first minimum, so comparing (t, scene-order id) lexicographically selects the
 // same hit in any visiting order.
-RTX_HD bool closer(double t, int32_t oid, const Hit& h) { return t < h.t || (t == h.t && oid < h.oid); }
+RTX_HD bool closer(const Hit& c, const Hit& h) {
+    if (c.t32 < h.t32) return true;
+    if (c.t32 > h.t32) return false;
+    const double a = exact_t(c), b = exact_t(h);   // equal proxies: decide in fp64
+    return a < b || (a == b && c.oid < h.oid);
+}
+
+// t64 > T for t64 = fl64(num / den), with T32 = fl32(T).
+RTX_HD bool quot_gt(float t32, float num, float den, double T, float T32) {
+    if (t32 != T32) return t32 > T32;
+    return (double)num / (double)den > T;
+}
+RTX_HD bool quot_lt(float t32, float num, float den, double T, float T32) {
+    if (t32 != T32) return t32 < T32;
+    return (double)num / (double)den < T;
+}
+// t64 >= 0 and t64 < 0 for t64 = fl64(num / den), den != 0, from t32 = fl32(num / den):
+// a quotient that underflows to +-0 in fp32 keeps its sign in fp64; NaN compares false.
+RTX_HD bool quot_signs_differ(float num, float den) { return num != 0.0f && ((num < 0.0f) != (den < 0.0f)); }
+RTX_HD bool quot_nonneg(float t32, float num, float den) {
+    return t32 > 0.0f || (t32 == 0.0f && !quot_signs_differ(num, den));
+}
+RTX_HD bool quot_neg(float t32, float num, float den) {
+    return t32 < 0.0f || (t32 == 0.0f && quot_signs_differ(num, den));
+}
 
 // Sphere quadratic (simple_geometry.py:29-39); returns false when disc < 0.
 RTX_HD bool sphere_roots(f3 o, f3 d, f3 c, double r2, double& b, double& s, double& two_a) {
@@ -174,6 +231,22 @@ RTX_HD bool sphere_roots(f3 o, f3 d, f3 c, double r2, double& b, double& s, doub
     s = sqrt(disc);
     two_a = 2.0 * a;
     return true;
+}
+
+// fp32 filter for the sign of the reference's fp64 discriminant (simple_geometry.py:29-34):
+// returns -1 (certainly < 0), +1 (certainly > 0) or 0 (undecided: use sphere_roots).
+// With h = dot(d, o - c) (b = 2h exactly), a = dot(d, d), q = dot(o - c, o - c), the
+// quarter discriminant h^2 - a (q - r^2) is evaluated in fp32; its error is below
+// 2^-21 (h^2 + a (q + r^2) + |D|), which also covers the reference's own fp64 rounding.
+RTX_HD int sphere_disc_sign(f3 o, f3 d, f3 c, float r2f) {
+    const f3 oc = sub(o, c);
+    const float a = dot(d, d), h = dot(d, oc), q = dot(oc, oc);
+    const float hh = h * h;
+    const float D = hh - a * (q - r2f);
+    const float E = 0x1p-21f * (hh + a * (q + r2f) + fabsf(D));
+    if (D < -E) return -1;
+    if (D > E) return 1;
+    return 0;  // also NaN/inf inputs: the exact path reproduces the reference
 }
 
 // AABB slabs (simple_geometry.py:196-226; bounding_volumes.py:61-91). Returns false if
@@ -232,80 +305,112 @@ RTX_HD void mesh_closest(const SceneView& S, const DObj& ob, int oi, f3 o, f3 d,
     // mesh.py:72-119: every face in order; the first strict minimum within the mesh wins.
     if (!mesh_bv(ob, o, d)) return;
     const int32_t f0 = ob.tri_begin, nf = ob.tri_count;
-    double best = INFINITY;
-    int32_t bf = -1;
+    Hit best;
+    best.t32 = INFINITY; best.num = 0.0f; best.den = 1.0f; best.quot = 1; best.sub = -1;
     for (int f = 0; f < nf; ++f) {
-        const DTri& T = S.tris[f0 + f];
+        const DTri T = S.tris[f0 + f];
         tally_inc<COUNT>(tl, &Tally::tri);
-        f3 n = ld3(T.n);
-        float denom = dot(d, n);
-        if (fabs((double)denom) < 1e-4) continue;
-        f3 v0 = ld3(T.v0);
-        double t = (double)dot(sub(v0, o), n) / (double)denom;
-        if (t < 0.0) continue;
-        f3 p = get_point(o, d, t);
-        float b0 = dot(cross(ld3(T.e01), sub(p, v0)), n);
-        float b1 = dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n);
-        float b2 = dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n);
-        if (b0 >= 0.0f && b1 >= 0.0f && b2 >= 0.0f && t < best) { best = t; bf = f; }
+        const f3 n = ld3(T.n);
+        const float denom = dot(d, n);
+        if (fabsf(denom) < kEps4Up) continue;                 // abs(denom) < epsilon
+        const f3 v0 = ld3(T.v0);
+        const float num = dot(sub(v0, o), n);
+        const float t32 = num / denom;
+        if (quot_neg(t32, num, denom)) continue;              // time < 0
+        const f3 p = add(o, scale(d, t32));                  // getPoint(time)
+        const float b0 = dot(cross(ld3(T.e01), sub(p, v0)), n);
+        const float b1 = dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n);
+        const float b2 = dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n);
+        if (b0 >= 0.0f && b1 >= 0.0f && b2 >= 0.0f) {
+            bool take = t32 < best.t32;
+            if (t32 == best.t32) take = (double)num / (double)denom < exact_t(best);
+            if (take) { best.t32 = t32; best.num = num; best.den = denom; best.sub = f; }
+        }
     }
-    if (bf >= 0 && closer(best, ob.oid, h)) { h.t = best; h.obj = oi; h.oid = ob.oid; h.sub = bf; }
+    if (best.sub >= 0) {
+        best.oid = ob.oid;
+        best.obj = oi;
+        best.t64 = 0.0;
+        if (closer(best, h)) h = best;
+    }
 }
 
 template <bool MESH, bool COUNT>
 RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl) {
-    Hit h{INFINITY, -1, 0x7fffffff, 0};
+    Hit h;
+    h.t32 = INFINITY; h.num = 0.0f; h.den = 1.0f; h.quot = 0; h.t64 = INFINITY;
+    h.obj = -1; h.oid = 0x7fffffff; h.sub = 0;
+    Hit c;
     int oi = 0;
     for (int k = 0; k < S.n_plane; ++k, ++oi) {  // simple_geometry.py:105-120
-        const DObj& ob = S.objs[oi];
-        f3 n = ld3(ob.b);
-        float denom = dot(d, n);
-        if (fabs((double)denom) > 1e-4) {
-            double t = (double)dot(sub(moved(ob, ob.a, time), o), n) / (double)denom;
-            if (t >= 0.0 && closer(t, ob.oid, h)) { h.t = t; h.obj = oi; h.oid = ob.oid; h.sub = 0; }
+        const DObj ob = S.objs[oi];
+        const f3 n = ld3(ob.b);
+        const float denom = dot(d, n);
+        if (fabsf(denom) >= kEps4Up) {                       // abs(denom) > epsilon
+            const float num = dot(sub(moved(ob, ob.a, time), o), n);
+            const float t32 = num / denom;
+            if (quot_nonneg(t32, num, denom)) {              // t >= 0
+                c.t32 = t32; c.num = num; c.den = denom; c.quot = 1; c.t64 = 0.0;
+                c.obj = oi; c.oid = ob.oid; c.sub = 0;
+                if (closer(c, h)) h = c;
+            }
         }
     }
     for (int k = 0; k < S.n_sphere; ++k, ++oi) {  // simple_geometry.py:20-46
-        const DObj& ob = S.objs[oi];
+        const DObj ob = S.objs[oi];
+        const f3 ctr = moved(ob, ob.a, time);
+        if (sphere_disc_sign(o, d, ctr, (float)ob.r2) < 0) continue;
         double b, s, two_a;
-        if (sphere_roots(o, d, moved(ob, ob.a, time), ob.r2, b, s, two_a)) {
+        if (sphere_roots(o, d, ctr, ob.r2, b, s, two_a)) {
             double t = (-b - s) / two_a;
             int32_t root = 0;
             if (!(t > 0.0)) { t = (-b + s) / two_a; root = 1; }
-            if (t > 0.0 && closer(t, ob.oid, h)) { h.t = t; h.obj = oi; h.oid = ob.oid; h.sub = root; }
+            if (t > 0.0) {
+                c.t32 = (float)t; c.quot = 0; c.t64 = t; c.num = 0.0f; c.den = 1.0f;
+                c.obj = oi; c.oid = ob.oid; c.sub = root;
+                if (closer(c, h)) h = c;
+            }
         }
     }
     for (int k = 0; k < S.n_box; ++k, ++oi) {  // simple_geometry.py:188-249 (entry precedes exit)
-        const DObj& ob = S.objs[oi];
+        const DObj ob = S.objs[oi];
         double start, end;
         int label;
         if (box_slabs(o, d, moved(ob, ob.a, time), moved(ob, ob.b, time), start, label, end)) {
-            if (!(start > end || start < 0.0) && closer(start, ob.oid, h)) { h.t = start; h.obj = oi; h.oid = ob.oid; h.sub = label; }
+            if (!(start > end || start < 0.0)) {
+                c.t32 = (float)start; c.quot = 0; c.t64 = start; c.num = 0.0f; c.den = 1.0f;
+                c.obj = oi; c.oid = ob.oid; c.sub = label;
+                if (closer(c, h)) h = c;
+            }
         }
     }
     if (MESH)
-        for (int k = 0; k < S.n_mesh; ++k, ++oi) mesh_closest<COUNT>(S, S.objs[oi], oi, o, d, h, tl);
+        for (int k = 0; k < S.n_mesh; ++k, ++oi) mesh_closest<COUNT>(S, (DObj)S.objs[oi], oi, o, d, h, tl);
     return h;
 }
 
 // ------------------------------------------------------------------ shadow any-hit
-// Any order gives the same answer; cheap objects first.
+// Any order gives the same answer; cheap objects first. T32max = fl32(t_max).
 template <bool MESH, bool COUNT>
 RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, Tally& tl) {
+    const float tmax32 = (float)t_max;
     int oi = 0;
     for (int k = 0; k < S.n_plane; ++k, ++oi) {  // simple_geometry.py:122-131
-        const DObj& ob = S.objs[oi];
-        f3 n = ld3(ob.b);
-        float denom = dot(d, n);
-        if (fabs((double)denom) > 1e-4) {
-            double t = (double)dot(sub(moved(ob, ob.a, time), o), n) / (double)denom;
-            if (1e-4 < t && t < t_max) return true;
+        const DObj ob = S.objs[oi];
+        const f3 n = ld3(ob.b);
+        const float denom = dot(d, n);
+        if (fabsf(denom) >= kEps4Up) {
+            const float num = dot(sub(moved(ob, ob.a, time), o), n);
+            const float t32 = num / denom;
+            if (quot_gt(t32, num, denom, 1e-4, kEps4Near) && quot_lt(t32, num, denom, t_max, tmax32)) return true;
         }
     }
     for (int k = 0; k < S.n_sphere; ++k, ++oi) {  // simple_geometry.py:48-72 (shadow_epsilon 1e-3)
-        const DObj& ob = S.objs[oi];
+        const DObj ob = S.objs[oi];
+        const f3 ctr = moved(ob, ob.a, time);
+        if (sphere_disc_sign(o, d, ctr, (float)ob.r2) < 0) continue;
         double b, s, two_a;
-        if (sphere_roots(o, d, moved(ob, ob.a, time), ob.r2, b, s, two_a)) {
+        if (sphere_roots(o, d, ctr, ob.r2, b, s, two_a)) {
             double t = (-b - s) / two_a;
             if (1e-3 < t && t < t_max) return true;
             t = (-b + s) / two_a;
@@ -313,7 +418,7 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
         }
     }
     for (int k = 0; k < S.n_box; ++k, ++oi) {  // simple_geometry.py:251-294
-        const DObj& ob = S.objs[oi];
+        const DObj ob = S.objs[oi];
         double start, end;
         int label;
         if (box_slabs(o, d, moved(ob, ob.a, time), moved(ob, ob.b, time), start, label, end)) {
@@ -322,19 +427,20 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
     }
     if (MESH) {
         for (int k = 0; k < S.n_mesh; ++k, ++oi) {  // mesh.py:121-153 (no t_max test)
-            const DObj& ob = S.objs[oi];
+            const DObj ob = S.objs[oi];
             if (!mesh_bv(ob, o, d)) continue;
             const int32_t f0 = ob.tri_begin, nf = ob.tri_count;
             for (int f = 0; f < nf; ++f) {
-                const DTri& T = S.tris[f0 + f];
+                const DTri T = S.tris[f0 + f];
                 tally_inc<COUNT>(tl, &Tally::tri);
-                f3 n = ld3(T.nu);
-                float denom = dot(d, n);
-                if (fabs((double)denom) < 1e-4) continue;
-                f3 v0 = ld3(T.v0);
-                double t = (double)dot(sub(v0, o), n) / (double)denom;
-                if (t < 1e-4) continue;
-                f3 p = get_point(o, d, t);
+                const f3 n = ld3(T.nu);
+                const float denom = dot(d, n);
+                if (fabsf(denom) < kEps4Up) continue;
+                const f3 v0 = ld3(T.v0);
+                const float num = dot(sub(v0, o), n);
+                const float t32 = num / denom;
+                if (quot_lt(t32, num, denom, 1e-4, kEps4Near)) continue;  // time < shadow_epsilon
+                const f3 p = add(o, scale(d, t32));
                 if (dot(cross(ld3(T.e01), sub(p, v0)), n) >= 0.0f &&
                     dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n) >= 0.0f &&
                     dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n) >= 0.0f)
@@ -383,8 +489,8 @@ struct Surface {
 template <bool MESH>
 RTX_HD Surface resolve_hit(const SceneView& S, const Hit& h, f3 o, f3 d, float time) {
     Surface sf;
-    const DObj& ob = S.objs[h.obj];
-    sf.position = get_point(o, d, h.t);
+    const DObj ob = S.objs[h.obj];
+    sf.position = add(o, scale(d, h.t32));  // getPoint(t): fl32(t64) == t32
     sf.mat = ob.mat0;
     const int32_t type = ob.type;
     if (type == OBJ_SPHERE) {
@@ -398,11 +504,11 @@ RTX_HD Surface resolve_hit(const SceneView& S, const Hit& h, f3 o, f3 d, float t
         float sgn = dl < 0.0f ? 1.0f : (dl > 0.0f ? -1.0f : 0.0f);
         sf.normal = f3{h.sub == 0 ? sgn : 0.0f, h.sub == 1 ? sgn : 0.0f, h.sub == 2 ? sgn : 0.0f};
     } else if (MESH) {
-        const DTri& T = S.tris[ob.tri_begin + h.sub];
+        const DTri T = S.tris[ob.tri_begin + h.sub];
         if (ob.flat)
             sf.normal = ld3(T.n);
         else
-            sf.normal = smooth_normal(T, S.trins[ob.tri_begin + h.sub], sf.position);
+            sf.normal = smooth_normal(T, (DTriN)S.trins[ob.tri_begin + h.sub], sf.position);
     }
     return sf;
 }
@@ -432,7 +538,7 @@ RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const 
     const f3 diffuse = ld3(m.diffuse);
     tally_inc<COUNT>(tl, &Tally::shade);
     for (int li = 0; li < S.n_lights; ++li) {
-        const DLight& L = S.lights[li];
+        const DLight L = S.lights[li];
         f3 sdir;
         double t_max;
         if (L.type == LIGHT_POINT) {
@@ -475,7 +581,7 @@ RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl) {
         Hit h = closest_hit<MESH, COUNT>(S, o, d, time, tl);
         if (h.obj < 0) break;  // miss -> black
         Surface sf = resolve_hit<MESH>(S, h, o, d, time);
-        const DMat& m = S.mats[sf.mat];
+        const DMat m = S.mats[sf.mat];
         if (SEC && m.type == MAT_MIRROR) {
             f3 rdir = reflect(d, sf.normal);
             f3 L = regular_lighting<MESH, COUNT>(S, d, sf.position, sf.normal, m, time, tl);
