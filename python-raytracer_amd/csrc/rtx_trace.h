@@ -25,6 +25,11 @@ namespace rtx {
 
 constexpr int kMaxDepth = 10;  // cast_ray(max_recursion=10) (scene.py:81)
 
+// Performance-experiment switch (tools/ablate.sh only; product builds leave it 0).
+#ifndef RTX_ABLATE
+#define RTX_ABLATE 0
+#endif
+
 // ------------------------------------------------------------------ fp32 vec3 (PyGLM)
 struct f3 {
     float x, y, z;
@@ -549,7 +554,8 @@ RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const 
             t_max = INFINITY;
         }
         tally_inc<COUNT>(tl, &Tally::shadow);
-        if (occluded<MESH, COUNT>(S, pos, sdir, t_max, time, tl)) continue;
+        if (RTX_ABLATE != 1 && occluded<MESH, COUNT>(S, pos, sdir, t_max, time, tl)) continue;
+        if (RTX_ABLATE == 3) { colour = add(colour, mul(ld3(L.cp), diffuse)); continue; }
         f3 light_dir = L.type == LIGHT_POINT ? normalize(sdir) : ld3(L.ndir);
         f3 lambert = scale(diffuse, pos_part(dot(normal, light_dir)));
         f3 half_vect = normalize(sub(light_dir, dir));
@@ -609,6 +615,7 @@ RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl) {
             in_shape = !in_shape;
             continue;
         }
+        if (RTX_ABLATE == 2) { tail = ld3(m.diffuse); break; }
         tail = clamp01(regular_lighting<MESH, COUNT>(S, d, sf.position, sf.normal, m, time, tl));
         break;
     }

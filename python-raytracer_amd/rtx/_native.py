@@ -13,6 +13,8 @@ import torch  # noqa: F401  (loads the process' HIP runtime before librtx.so)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_lib", "librtx.so")
+# Experiment builds (tools/ablate.sh) point this at another build of the same HIP source.
+LIB_PATH = os.environ.get("RTX_LIB_OVERRIDE", LIB_PATH)
 ABI_VERSION = 1
 
 RTX_OK, RTX_ERR_INVALID, RTX_ERR_HIP, RTX_ERR_UNSUPPORTED, RTX_ERR_STATE = 0, -1, -2, -3, -4

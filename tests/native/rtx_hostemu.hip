@@ -8,11 +8,11 @@
 
 namespace {
 void bind_view(const HostScene& H, SceneView& v) {
-    v.objs = H.objs.data();
-    v.tris = H.tris.data();
-    v.trins = H.trins.data();
-    v.mats = H.mats.data();
-    v.lights = H.lights.data();
+    v.objs = (cptr<DObj>)H.objs.data();
+    v.tris = (cptr<DTri>)H.tris.data();
+    v.trins = (cptr<DTriN>)H.trins.data();
+    v.mats = (cptr<DMat>)H.mats.data();
+    v.lights = (cptr<DLight>)H.lights.data();
     v.n_objs = H.n_objs;
     v.n_lights = H.n_lights;
     v.n_plane = H.n_plane; v.n_sphere = H.n_sphere; v.n_box = H.n_box; v.n_mesh = H.n_mesh;
@@ -34,8 +34,8 @@ extern "C" int rtx_hostemu_render(const rtx_scene_desc* sd, const rtx_camera_des
     std::vector<float> noise;
     const size_t nsamp = (size_t)cd->n_dof * cd->n_aa;
     if (cd->jitter == RTX_JITTER_REPLAY) noise.assign(cd->noise, cd->noise + 3 * (size_t)cd->ncols * cd->height * nsamp);
-    k.xs = cd->xs; k.ys = cd->ys; k.dof_o = cd->dof_origins; k.aa_o = cd->aa_origins; k.times = times.data();
-    k.noise = noise.data();
+    k.xs = (cptr<float>)cd->xs; k.ys = (cptr<float>)cd->ys; k.dof_o = (cptr<float>)cd->dof_origins;
+    k.aa_o = (cptr<float>)cd->aa_origins; k.times = (cptr<float>)times.data(); k.noise = (cptr<float>)noise.data();
     const int64_t npix = (int64_t)nrows * k.ncols;
     uint64_t tot[RTX_COUNTERS] = {};
 #pragma omp parallel num_threads(threads > 0 ? threads : 1)

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Build ablation variants of librtx.so (RTX_ABLATE=1: no shadow tests; 2: no lighting;
+# 3: no shading math after the shadow test) and time each on the bench configs.
+# Experiment only: results are not parity-correct for N != 0.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${TAG:-ablate}
+mkdir -p "$OUT" /tmp/rtx_ablate
+for n in ${VARIANTS:-0 1 2 3}; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -DRTX_ABLATE=$n \
+    ${EXTRA_FLAGS:-} -o /tmp/rtx_ablate/librtx_$n.so python-raytracer_amd/csrc/rtx_api.hip || exit 1
+done
+for n in ${VARIANTS:-0 1 2 3}; do
+  for c in ${CONFIGS:-tsp1080}; do
+    RTX_LIB_OVERRIDE=/tmp/rtx_ablate/librtx_$n.so timeout -k 10 120 python bench.py --config $c --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/v${n}_$c.log" 2>&1 || exit 1
+    echo "variant $n $c $(python3 -c "import json,sys; d=json.loads([l for l in open('$OUT/v${n}_$c.log') if l.startswith('{')][0]); print('frame_ms', d['frame_ms'])")"
+  done
+done
