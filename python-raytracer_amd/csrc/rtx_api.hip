@@ -122,11 +122,36 @@ struct Launch {
     int32_t row0, nrows;
 };
 
+#ifndef RTX_LB_WAVES
+#define RTX_LB_WAVES 1
+#endif
+#ifndef RTX_TILE
+#define RTX_TILE 0
+#endif
+
+// Pixel of this work-item. RTX_TILE=1 maps each 64-lane wave to an 8x8 pixel tile
+// (coherent rays per wave); 0 maps waves to 64 consecutive pixels of a row.
+__device__ __forceinline__ int64_t pixel_index(int32_t nrows, int32_t ncols) {
+    if (RTX_TILE == 0) return (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int tiles_x = (ncols + 7) >> 3;
+    const int64_t tile = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
+    const int64_t r = ty * 8 + (lane >> 3), c = tx * 8 + (lane & 7);
+    if (r >= nrows || c >= ncols) return -1;
+    return r * ncols + c;
+}
+
+__host__ __device__ inline int64_t launch_items(int32_t nrows, int32_t ncols) {
+    if (RTX_TILE == 0) return (int64_t)nrows * ncols;
+    return (int64_t)((ncols + 7) >> 3) * ((nrows + 7) >> 3) * 64;
+}
+
 template <bool MESH, bool SEC, bool COUNT>
-__global__ __launch_bounds__(256) void k_render(const KParams* __restrict__ Pp, const Launch L) {
+__global__ __launch_bounds__(256, RTX_LB_WAVES) void k_render(const KParams* __restrict__ Pp, const Launch L) {
     const int64_t npix = (int64_t)L.nrows * Pp->ncols;
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool active = p < npix;
+    const int64_t p = pixel_index(L.nrows, Pp->ncols);
+    const bool active = p >= 0 && p < npix;
     Tally tl = {};
     if (active) render_pixel<MESH, SEC, COUNT>(*Pp, L.fb, L.row0, p, tl);
     flush_tally<COUNT>(tl, L.counters, active);
@@ -499,8 +524,8 @@ int rtx_render(rtx_scene* s, int32_t row0, int32_t nrows, float* fb_dev, uint64_
     L.row0 = row0;
     L.nrows = nrows;
     L.counters = reinterpret_cast<unsigned long long*>(counters_dev);
-    const int64_t npix = (int64_t)nrows * s->kp.ncols;
-    const dim3 grid((unsigned)((npix + 255) / 256)), block(256);
+    const int64_t items = launch_items(nrows, s->kp.ncols);
+    const dim3 grid((unsigned)((items + 255) / 256)), block(256);
     hipStream_t st = (hipStream_t)stream;
     const bool cnt = counters_dev != nullptr;
     const int sel = (s->has_mesh ? 4 : 0) | (s->has_secondary ? 2 : 0) | (cnt ? 1 : 0);

@@ -6,9 +6,11 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${TAG:-ablate}
 mkdir -p "$OUT" /tmp/rtx_ablate
+# VARIANTS: names; FLAGS_<name> gives its hipcc -D flags (default: -DRTX_ABLATE=<name>)
 for n in ${VARIANTS:-0 1 2 3}; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -DRTX_ABLATE=$n \
-    ${EXTRA_FLAGS:-} -o /tmp/rtx_ablate/librtx_$n.so python-raytracer_amd/csrc/rtx_api.hip || exit 1
+  fl_var="FLAGS_$n"; fl="${!fl_var:--DRTX_ABLATE=$n}"
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared $fl \
+    -o /tmp/rtx_ablate/librtx_$n.so python-raytracer_amd/csrc/rtx_api.hip || exit 1
 done
 for n in ${VARIANTS:-0 1 2 3}; do
   for c in ${CONFIGS:-tsp1080}; do
