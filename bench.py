@@ -48,7 +48,20 @@ def parse():
     p.add_argument("--rowblock", action="store_true", help="also time row-block + RCCL gather of one frame")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--pmc-json", default=None,
+                   help="tools/pmc_summary.py output for this config (default profiles/pmc_<config>.json)")
     return p.parse_args()
+
+
+def pmc_traffic(path):
+    """HBM bytes per launch measured by rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE in
+    separate passes, gfx950 FETCH correction) — see tools/pmc_session.sh."""
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch"), path
+    except (OSError, ValueError):
+        return None, None
 
 
 def make_scene(cfg):
@@ -180,6 +193,10 @@ def main():
 
     if rank == 0:
         achieved = b_alg / (kern_ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic(a.pmc_json or os.path.join(REPO, "profiles", "pmc_%s.json" % a.config))
+        if traffic is not None:
+            traffic = int(round(traffic))
+            traffic_src = os.path.relpath(traffic_src, REPO)
         out = {
             "metric": METRIC if a.config == "tsp1080" else METRIC_OTHER % CONFIGS[a.config][3], "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms_per_step, 5), "higher_is_better": True, "scaling": "weak",
@@ -190,7 +207,8 @@ def main():
             "frame_ms": round(kern_ms, 5),
             "segments_per_frame": segments, "cast_rays_per_frame": cast_rays, "shadow_rays_per_frame": shadow_rays,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "traffic_unit": "bytes/launch (rocprofv3 PMC)", "traffic_source": traffic_src,
                          "model": "B_alg = 32 B x ray segments + 12 B x pixels per frame (SURVEY.md 8d) / kernel time",
                          "bytes_alg_per_frame": b_alg},
         }

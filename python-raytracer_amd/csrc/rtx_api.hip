@@ -48,7 +48,8 @@ struct KParams {
     cptr<float> times;   // [n_times] fp32
     cptr<float> noise;   // replay jitter
     float pos[4], u[4], v[4], dw[4];
-    float focal, divisor, jscale, pad;
+    float focal, divisor, jscale, inv_divisor;
+    int32_t div_pow2, pad0, pad1, pad2;
     int32_t width, height, col0, ncols;
     int32_t n_dof, n_aa, n_times, jitter;
     uint32_t seed_lo, seed_hi;
@@ -107,7 +108,10 @@ RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int64_t p, T
                 colour = add(colour, cast_ray<MESH, SEC, COUNT>(P.S, o, ddir, P.times[kt], tl));
         }
     }
-    colour = divs(colour, P.divisor);  // scene.py:73
+    // colour / (samples * dof_samples * len(motion_times)) (scene.py:73); for a power of
+    // two the exact reciprocal multiply gives the identical correctly rounded result.
+    if (P.div_pow2) colour = scale(colour, P.inv_divisor);
+    else colour = divs(colour, P.divisor);
     float* out = fb + 3 * p;
     out[0] = colour.x;
     out[1] = colour.y;
@@ -122,11 +126,14 @@ struct Launch {
     int32_t row0, nrows;
 };
 
+// Occupancy request (waves per SIMD) by kernel variant: mesh kernels without secondary
+// rays fit 128 VGPRs without scratch and gain from 4 waves/SIMD; the others spill if
+// forced below their natural allocation (measured, tools/ablate.sh).
 #ifndef RTX_LB_WAVES
-#define RTX_LB_WAVES 1
+#define RTX_LB_WAVES(MESH, SEC) ((MESH) && !(SEC) ? 4 : 1)
 #endif
 #ifndef RTX_TILE
-#define RTX_TILE 0
+#define RTX_TILE 1
 #endif
 
 // Pixel of this work-item. RTX_TILE=1 maps each 64-lane wave to an 8x8 pixel tile
@@ -148,7 +155,7 @@ __host__ __device__ inline int64_t launch_items(int32_t nrows, int32_t ncols) {
 }
 
 template <bool MESH, bool SEC, bool COUNT>
-__global__ __launch_bounds__(256, RTX_LB_WAVES) void k_render(const KParams* __restrict__ Pp, const Launch L) {
+__global__ __launch_bounds__(256, RTX_LB_WAVES(MESH, SEC)) void k_render(const KParams* __restrict__ Pp, const Launch L) {
     const int64_t npix = (int64_t)L.nrows * Pp->ncols;
     const int64_t p = pixel_index(L.nrows, Pp->ncols);
     const bool active = p >= 0 && p < npix;
@@ -384,6 +391,9 @@ int convert_camera(const rtx_camera_desc* c, KParams& k) {
     set3(k.dw, scale(ld3(c->w), (float)c->d));  // self.vc.d * self.vc.w
     k.focal = (float)c->focal_length;
     k.divisor = (float)(nsamp * c->n_times);     // samples * dof_samples * len(motion_times)
+    const int64_t nd = nsamp * c->n_times;
+    k.div_pow2 = (nd & (nd - 1)) == 0 ? 1 : 0;
+    k.inv_divisor = 1.0f / k.divisor;
     k.jscale = (float)c->jitter_scale;
     k.width = c->width; k.height = c->height; k.col0 = c->col0; k.ncols = c->ncols;
     k.n_dof = c->n_dof; k.n_aa = c->n_aa; k.n_times = c->n_times; k.jitter = c->jitter;

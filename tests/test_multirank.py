@@ -1,0 +1,78 @@
+"""World-size-2 gloo tests of the multi-rank frame path (row blocks + gather) on CPU,
+with the tests-only host build of the device source standing in for each rank's GPU."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, name, res, out_q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), "python-raytracer_amd"), here):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import hostemu
+    from common import product_scene
+    from rtx.distributed import render_frame
+    sc = product_scene(name, res)
+
+    def rows(row0, nrows):
+        img, _ = hostemu.render(sc, threads=2)   # full frame on the host, then this rank's block
+        fb = np.ascontiguousarray(np.transpose(img, (1, 0, 2))[::-1]).astype(np.float32)
+        return torch.from_numpy(fb[row0:row0 + nrows].copy())
+
+    for dtype in (torch.float32, torch.uint8):
+        frame = render_frame(sc, rank, world, render_rows=rows, dtype=dtype)
+        if rank == 0:
+            out_q.put((str(dtype), frame.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,res", [(2, (40, 23)), (3, (17, 10))])
+def test_gather_row_blocks(world, res):
+    from common import oracle_render
+    from oracle import oracle as O
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, "MirrorRefraction", res, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = oracle_render("MirrorRefraction", res)
+    fb_ref = np.transpose(ref, (1, 0, 2))[::-1].astype(np.float32)
+    assert np.array_equal(got["torch.float32"], fb_ref)
+    assert np.array_equal(got["torch.uint8"], O.to_png_array(ref))
+
+
+def test_glue_reassembles_strips(tmp_path):
+    """rtx.glue over render(k, N) strips == full render (provided/glue.py semantics)."""
+    import hostemu
+    from common import product_scene
+    from oracle import oracle as O
+    from rtx.glue import glue
+    sc = product_scene("TwoSpheresPlane", (37, 20))
+    for k in range(4):
+        img, _ = hostemu.render(sc, k, 4)
+        np.save(tmp_path / ("%d.npy" % k), img)
+    full, _ = hostemu.render(sc)
+    assert np.array_equal(glue(str(tmp_path)), O.to_png_array(full))

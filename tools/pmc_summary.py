@@ -1,0 +1,32 @@
+"""Summarise a tools/pmc_session.sh run: per-dispatch averages of every counter for the
+render kernel, and HBM traffic per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 bytes
+(FETCH_SIZE/WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reads half the bytes of a wide
+stream — MI355X_MICROARCH.md §HBM — so it is doubled).
+
+usage: python tools/pmc_summary.py gpurun_out/<tag> <config> > profiles/rNN/pmc_<config>.json
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+d, cfg = sys.argv[1], sys.argv[2]
+acc = {}
+kname = None
+for f in sorted(glob.glob(os.path.join(d, "p*", "*counter_collection.csv"))):
+    for r in csv.DictReader(open(f)):
+        if "k_render" not in r["Kernel_Name"]:
+            continue
+        kname = r["Kernel_Name"]
+        acc.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+avg = {k: sum(v) / len(v) for k, v in acc.items()}
+out = {"config": cfg, "kernel": kname, "dispatches": max(len(v) for v in acc.values()) if acc else 0,
+       "counters_per_dispatch": avg}
+if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+    out["hbm_bytes_per_launch"] = (2 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024
+    out["hbm_bytes_note"] = "(2*FETCH_SIZE + WRITE_SIZE) KiB; FETCH doubled per MI355X_MICROARCH.md gfx950 note"
+if "SQ_WAVES" in avg and "SQ_INSTS_VALU" in avg:
+    out["valu_insts_per_wave"] = avg["SQ_INSTS_VALU"] / avg["SQ_WAVES"]
+    out["salu_insts_per_wave"] = avg.get("SQ_INSTS_SALU", 0) / avg["SQ_WAVES"]
+print(json.dumps(out, indent=1))
