@@ -76,10 +76,9 @@ __device__ __forceinline__ void flush_tally(const Tally& tl, unsigned long long*
 
 // scene.py:47-79 for pixel p of the output block (host/device: the tests-only host
 // emulation runs the same body).
-template <bool MESH, bool SEC, bool COUNT>
-RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int64_t p, Tally& tl) {
-    const int rr = (int)(p / P.ncols);
-    const int cc = (int)(p - (int64_t)rr * P.ncols);
+template <bool MESH, bool SEC, bool COUNT, bool JIT>
+RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, int32_t cc, Tally& tl) {
+    const int64_t p = (int64_t)rr * P.ncols + cc;
     const int j = P.height - 1 - (row0 + rr);  // reference row index (y grows upward)
     const float fx = P.xs[cc];
     const float fy = P.ys[j];
@@ -91,7 +90,7 @@ RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int64_t p, T
         const f3 ddir = normalize(sub(focal, ld3(P.dof_o + 3 * kd)));  // scene.py:58
         for (int ka = 0; ka < P.n_aa; ++ka) {
             f3 o = ld3(P.aa_o + 3 * (kd * P.n_aa + ka));
-            if (P.jitter != RTX_JITTER_OFF) {  // scene.py:63-65
+            if (JIT) {  // scene.py:63-65
                 f3 rnd;
                 if (P.jitter == RTX_JITTER_REPLAY) {
                     const int64_t idx = (((int64_t)cc * P.height + j) * P.n_dof + kd) * P.n_aa + ka;
@@ -136,17 +135,24 @@ struct Launch {
 #define RTX_TILE 1
 #endif
 
-// Pixel of this work-item. RTX_TILE=1 maps each 64-lane wave to an 8x8 pixel tile
-// (coherent rays per wave); 0 maps waves to 64 consecutive pixels of a row.
-__device__ __forceinline__ int64_t pixel_index(int32_t nrows, int32_t ncols) {
-    if (RTX_TILE == 0) return (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int tiles_x = (ncols + 7) >> 3;
-    const int64_t tile = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+// Output pixel (row, column within the block) of this work-item. RTX_TILE=1 maps each
+// 64-lane wave to an 8x8 pixel tile (coherent rays per wave); 0 maps waves to 64
+// consecutive pixels of a row. The wave's tile is wave-uniform, so its coordinates are
+// scalar 32-bit arithmetic.
+struct PixelRC {
+    int32_t r, c;
+};
+__device__ __forceinline__ PixelRC pixel_rc(int32_t ncols) {
     const int lane = threadIdx.x & 63;
-    const int64_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
-    const int64_t r = ty * 8 + (lane >> 3), c = tx * 8 + (lane & 7);
-    if (r >= nrows || c >= ncols) return -1;
-    return r * ncols + c;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+    if (RTX_TILE == 0) {
+        const int64_t p = (int64_t)wave * 64 + lane;
+        const int32_t r = (int32_t)(p / ncols);
+        return PixelRC{r, (int32_t)(p - (int64_t)r * ncols)};
+    }
+    const int tiles_x = (ncols + 7) >> 3;
+    const int ty = wave / tiles_x, tx = wave - ty * tiles_x;
+    return PixelRC{ty * 8 + (lane >> 3), tx * 8 + (lane & 7)};
 }
 
 __host__ __device__ inline int64_t launch_items(int32_t nrows, int32_t ncols) {
@@ -154,13 +160,13 @@ __host__ __device__ inline int64_t launch_items(int32_t nrows, int32_t ncols) {
     return (int64_t)((ncols + 7) >> 3) * ((nrows + 7) >> 3) * 64;
 }
 
-template <bool MESH, bool SEC, bool COUNT>
+template <bool MESH, bool SEC, bool COUNT, bool JIT>
 __global__ __launch_bounds__(256, RTX_LB_WAVES(MESH, SEC)) void k_render(const KParams* __restrict__ Pp, const Launch L) {
-    const int64_t npix = (int64_t)L.nrows * Pp->ncols;
-    const int64_t p = pixel_index(L.nrows, Pp->ncols);
-    const bool active = p >= 0 && p < npix;
+    const int32_t ncols = Pp->ncols;
+    const PixelRC px = pixel_rc(ncols);
+    const bool active = px.r < L.nrows && px.c < ncols;
     Tally tl = {};
-    if (active) render_pixel<MESH, SEC, COUNT>(*Pp, L.fb, L.row0, p, tl);
+    if (active) render_pixel<MESH, SEC, COUNT, JIT>(*Pp, L.fb, L.row0, px.r, px.c, tl);
     flush_tally<COUNT>(tl, L.counters, active);
 }
 
@@ -538,18 +544,30 @@ int rtx_render(rtx_scene* s, int32_t row0, int32_t nrows, float* fb_dev, uint64_
     const dim3 grid((unsigned)((items + 255) / 256)), block(256);
     hipStream_t st = (hipStream_t)stream;
     const bool cnt = counters_dev != nullptr;
-    const int sel = (s->has_mesh ? 4 : 0) | (s->has_secondary ? 2 : 0) | (cnt ? 1 : 0);
+    const bool jit = s->kp.jitter != RTX_JITTER_OFF;
+    const int sel = (s->has_mesh ? 8 : 0) | (s->has_secondary ? 4 : 0) | (cnt ? 2 : 0) | (jit ? 1 : 0);
     const KParams* kp = s->d_kp;
+#define RTX_LAUNCH(M, S, C, J) \
+    hipLaunchKernelGGL((k_render<M, S, C, J>), grid, block, 0, st, kp, L)
     switch (sel) {
-        case 0: hipLaunchKernelGGL((k_render<false, false, false>), grid, block, 0, st, kp, L); break;
-        case 1: hipLaunchKernelGGL((k_render<false, false, true>), grid, block, 0, st, kp, L); break;
-        case 2: hipLaunchKernelGGL((k_render<false, true, false>), grid, block, 0, st, kp, L); break;
-        case 3: hipLaunchKernelGGL((k_render<false, true, true>), grid, block, 0, st, kp, L); break;
-        case 4: hipLaunchKernelGGL((k_render<true, false, false>), grid, block, 0, st, kp, L); break;
-        case 5: hipLaunchKernelGGL((k_render<true, false, true>), grid, block, 0, st, kp, L); break;
-        case 6: hipLaunchKernelGGL((k_render<true, true, false>), grid, block, 0, st, kp, L); break;
-        case 7: hipLaunchKernelGGL((k_render<true, true, true>), grid, block, 0, st, kp, L); break;
+        case 0: RTX_LAUNCH(false, false, false, false); break;
+        case 1: RTX_LAUNCH(false, false, false, true); break;
+        case 2: RTX_LAUNCH(false, false, true, false); break;
+        case 3: RTX_LAUNCH(false, false, true, true); break;
+        case 4: RTX_LAUNCH(false, true, false, false); break;
+        case 5: RTX_LAUNCH(false, true, false, true); break;
+        case 6: RTX_LAUNCH(false, true, true, false); break;
+        case 7: RTX_LAUNCH(false, true, true, true); break;
+        case 8: RTX_LAUNCH(true, false, false, false); break;
+        case 9: RTX_LAUNCH(true, false, false, true); break;
+        case 10: RTX_LAUNCH(true, false, true, false); break;
+        case 11: RTX_LAUNCH(true, false, true, true); break;
+        case 12: RTX_LAUNCH(true, true, false, false); break;
+        case 13: RTX_LAUNCH(true, true, false, true); break;
+        case 14: RTX_LAUNCH(true, true, true, false); break;
+        case 15: RTX_LAUNCH(true, true, true, true); break;
     }
+#undef RTX_LAUNCH
     RTX_HIP(hipGetLastError());
     return RTX_OK;
 }
