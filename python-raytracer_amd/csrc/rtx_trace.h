@@ -56,7 +56,11 @@ RTX_HD f3 cross(f3 a, f3 b) {
 }
 // glm::normalize = v * inversesqrt(dot(v, v)), inversesqrt(x) = 1 / sqrt(x)
 RTX_HD f3 normalize(f3 v) {
+#if RTX_ABLATE == 6
+    float inv = __builtin_amdgcn_rsqf(dot(v, v));  // cost probe only
+#else
     float inv = 1.0f / sqrtf(dot(v, v));
+#endif
     return scale(v, inv);
 }
 RTX_HD bool is_zero(f3 v) { return v.x == 0.0f && v.y == 0.0f && v.z == 0.0f; }
@@ -227,6 +231,16 @@ RTX_HD bool quot_neg(float t32, float num, float den) {
 
 // Sphere quadratic (simple_geometry.py:29-39); returns false when disc < 0.
 RTX_HD bool sphere_roots(f3 o, f3 d, f3 c, double r2, double& b, double& s, double& two_a) {
+    if (RTX_ABLATE == 4) {  // cost probe only: fp32 quadratic (not parity-correct)
+        float a = dot(d, d);
+        f3 oc = sub(o, c);
+        float bf = 2.0f * dot(d, oc);
+        float cf = dot(oc, oc) - (float)r2;
+        float disc = bf * bf - 4.0f * a * cf;
+        if (disc < 0.0f) return false;
+        b = bf; s = sqrtf(disc); two_a = 2.0f * a;
+        return true;
+    }
     double a = (double)dot(d, d);
     f3 oc = sub(o, c);
     b = 2.0 * (double)dot(d, oc);
@@ -523,6 +537,7 @@ RTX_HD Surface resolve_hit(const SceneView& S, const Hit& h, f3 o, f3 d, float t
 // exponentiation; the fp32 cast that follows makes it equal to libm pow except when the
 // exact value lies within a few fp64 ulps of an fp32 rounding boundary.
 RTX_HD double spec_pow(double x, const DMat& m) {
+    if (RTX_ABLATE == 5) return (double)__builtin_powf((float)x, (float)m.hardness);  // cost probe only
     if (m.hard_is_int) {
         int n = m.hard_int;
         double r = 1.0, b = x;
