@@ -56,7 +56,7 @@ RTX_HD f3 cross(f3 a, f3 b) {
 }
 // glm::normalize = v * inversesqrt(dot(v, v)), inversesqrt(x) = 1 / sqrt(x)
 RTX_HD f3 normalize(f3 v) {
-#if RTX_ABLATE == 6
+#if RTX_ABLATE == 6 && defined(__HIP_DEVICE_COMPILE__)
     float inv = __builtin_amdgcn_rsqf(dot(v, v));  // cost probe only
 #else
     float inv = 1.0f / sqrtf(dot(v, v));
