@@ -233,6 +233,7 @@ struct HostScene {
     bool has_mesh = false, has_secondary = false;
     int32_t n_objs = 0, n_lights = 0;
     int32_t n_plane = 0, n_sphere = 0, n_box = 0, n_mesh = 0;
+    int32_t pow_bits = 0;
     float ambient[4] = {0, 0, 0, 0};
 };
 
@@ -266,6 +267,8 @@ int convert_scene(const rtx_scene_desc* desc, HostScene& H) {
         d.hardness = m.hardness;
         d.hard_is_int = (m.hardness >= 0.0 && m.hardness <= 4096.0 && std::floor(m.hardness) == m.hardness) ? 1 : 0;
         d.hard_int = d.hard_is_int ? (int32_t)m.hardness : 0;
+        for (int b = 0; b < 31; ++b)
+            if ((d.hard_int >> b) && H.pow_bits < b + 1) H.pow_bits = b + 1;
     }
     for (int i = 0; i < desc->n_lights; ++i) {
         const rtx_light& l = desc->lights[i];
@@ -487,6 +490,7 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
     v.n_objs = H.n_objs;
     v.n_lights = H.n_lights;
     v.n_plane = H.n_plane; v.n_sphere = H.n_sphere; v.n_box = H.n_box; v.n_mesh = H.n_mesh;
+    v.pow_bits = H.pow_bits;
     std::memcpy(v.ambient, H.ambient, sizeof(v.ambient));
     *out = s;
     return RTX_OK;

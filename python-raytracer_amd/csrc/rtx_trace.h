@@ -146,6 +146,7 @@ struct SceneView {
     cptr<DLight> lights;
     int32_t n_objs, n_lights;
     int32_t n_plane, n_sphere, n_box, n_mesh;
+    int32_t pow_bits, pad0, pad1, pad2;   // bit length of the largest integer hardness
     float ambient[4];
 };
 
@@ -471,6 +472,16 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
 }
 
 // ------------------------------------------------------------------ hit record
+// math.floor(a - b) of two floats, where the reference subtracts in fp64 (exactly). The
+// fp32 difference d = fl32(a - b) lies in [k, k + 1] when floor(a - b) = k (k and k + 1
+// are floats below 2^23), so floorf(d) is exact unless d is an integer: then use fp64.
+RTX_HD int32_t floor_diff(float a, float b) {
+    const float d = a - b;
+    const float f = floorf(d);
+    if (fabsf(d) < 0x1p23f && d != f) return (int32_t)f;
+    return (int32_t)(int64_t)floor((double)a - (double)b);
+}
+
 // Plane.get_material (simple_geometry.py:133-148): checker by floor of the projected
 // coordinates, Python modulo.
 RTX_HD int32_t plane_material(const DObj& ob, f3 point, float time) {
@@ -480,9 +491,7 @@ RTX_HD int32_t plane_material(const DObj& ob, f3 point, float time) {
     point = sub(point, scale(n, dot(sub(point, position), n)));
     float x = dot(sub(point, position), ld3(ob.c));
     float z = dot(sub(point, position), ld3(ob.e));
-    double dx = floor((double)position.x - (double)x);
-    double dz = floor((double)position.z - (double)z);
-    int64_t s = (int64_t)dx + (int64_t)dz;
+    const int32_t s = floor_diff(position.x, x) + floor_diff(position.z, z);
     return (s & 1) ? ob.mat1 : ob.mat0;  // (dx + dz) % 2 with Python modulo
 }
 
@@ -535,16 +544,19 @@ RTX_HD Surface resolve_hit(const SceneView& S, const Hit& h, f3 o, f3 d, float t
 // ------------------------------------------------------------------ shading
 // `x ** hardness` (CPython float_pow -> pow) in fp64. Integer exponents use binary
 // exponentiation; the fp32 cast that follows makes it equal to libm pow except when the
-// exact value lies within a few fp64 ulps of an fp32 rounding boundary.
-RTX_HD double spec_pow(double x, const DMat& m) {
+// exact value lies within a few fp64 ulps of an fp32 rounding boundary. The loop runs a
+// scene-uniform number of steps (bits of the largest integer hardness) with selects, so
+// lanes shading different materials do not diverge; each lane performs exactly the
+// multiplications of `while (n) { if (n & 1) r *= b; b *= b; n >>= 1; }`.
+RTX_HD double spec_pow(double x, const DMat& m, int pow_bits) {
     if (RTX_ABLATE == 5) return (double)__builtin_powf((float)x, (float)m.hardness);  // cost probe only
     if (m.hard_is_int) {
-        int n = m.hard_int;
+        const int n = m.hard_int;
         double r = 1.0, b = x;
-        while (n > 0) {
-            if (n & 1) r *= b;
-            b *= b;
-            n >>= 1;
+        for (int k = 0; k < pow_bits; ++k) {
+            const double rb = r * b;
+            r = ((n >> k) & 1) ? rb : r;
+            b = b * b;
         }
         return r;
     }
@@ -576,7 +588,7 @@ RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const 
         f3 half_vect = normalize(sub(light_dir, dir));
         float nh = dot(normal, half_vect);
         double base = nh > 0.0f ? (double)nh : 0.0;
-        f3 specular = scale(ld3(m.specular), (float)spec_pow(base, m));
+        f3 specular = scale(ld3(m.specular), (float)spec_pow(base, m, S.pow_bits));
         colour = add(colour, mul(ld3(L.cp), add(lambert, specular)));
     }
     colour = add(colour, mul(ld3(S.ambient), diffuse));

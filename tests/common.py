@@ -53,3 +53,18 @@ def assert_parity(img, ref, what=""):
     s = compare(img, ref)
     assert s["frac_diff"] <= MAX_FRAC_DIFF and s["mean_abs"] <= MAX_MEAN_ABS, "%s parity: %s" % (what, s)
     return s
+
+
+def oracle_render_dict(data, subimage=0, tasks=1, noise=None, tallies=False):
+    import os
+    base = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets")
+    return O.OracleScene(data, base).render(subimage, tasks, noise=noise, tallies=tallies)
+
+
+def product_scene_dict(data):
+    import copy
+    import os
+    import rtx
+    d = copy.deepcopy(data)
+    d["__base_dir__"] = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets")
+    return rtx.load_scene(d, verbose=False)

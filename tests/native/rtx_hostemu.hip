@@ -16,6 +16,7 @@ void bind_view(const HostScene& H, SceneView& v) {
     v.n_objs = H.n_objs;
     v.n_lights = H.n_lights;
     v.n_plane = H.n_plane; v.n_sphere = H.n_sphere; v.n_box = H.n_box; v.n_mesh = H.n_mesh;
+    v.pow_bits = H.pow_bits;
     std::memcpy(v.ambient, H.ambient, sizeof(v.ambient));
 }
 }  // namespace

@@ -138,3 +138,20 @@ def test_full_size_dof_4k_properties():
     b = torch.cat([sc.render_device(row0=1000, nrows=32), sc.render_device(row0=1032, nrows=32)])
     assert torch.equal(a, b)
     assert float(a.min()) >= 0.0 and float(a.max()) <= 1.0
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_random_scenes_match_oracle(seed):
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import random_scene
+    d = random_scene(seed, res=(64, 48), mesh=(seed % 3 == 0))
+    img = product_scene_dict(d).render()
+    ref = oracle_render_dict(d)
+    assert_parity(img, ref, "seed %d" % seed)
+
+
+def test_ties_follow_scene_order():
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import tie_scene
+    d = tie_scene((80, 60))
+    assert compare(product_scene_dict(d).render(), oracle_render_dict(d))["frac_diff"] == 0.0

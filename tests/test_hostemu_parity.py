@@ -76,3 +76,26 @@ def test_hostemu_geometry_kat(name):
         assert np.array_equal(got["position"][hit], pp[hit])
         for tmax in (1.0, np.inf):
             assert np.array_equal(hostemu.occluded(sc, o, d, tmax, time), osc.shadow(time, o, d, tmax).astype(bool))
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_hostemu_random_scenes(seed):
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import random_scene
+    d = random_scene(seed, mesh=(seed % 3 == 0))
+    img, cnt = hostemu.render(product_scene_dict(d))
+    ref, tl = oracle_render_dict(d, tallies=True)
+    s = assert_parity(img, ref, "seed %d" % seed)
+    assert s["frac_diff"] == 0.0, s
+    assert list(cnt[:10]) == tl[:10] and cnt[10] == tl[11]
+
+
+def test_hostemu_ties_follow_scene_order():
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import tie_scene
+    d = tie_scene()
+    img, _ = hostemu.render(product_scene_dict(d))
+    ref = oracle_render_dict(d)
+    assert assert_parity(img, ref)["frac_diff"] == 0.0
+    # the red/blue coincident spheres: s1 (blue) is first in scene order
+    assert (ref[..., 2] > ref[..., 0]).any()
