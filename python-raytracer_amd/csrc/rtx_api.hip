@@ -267,6 +267,13 @@ int convert_scene(const rtx_scene_desc* desc, HostScene& H) {
         d.hardness = m.hardness;
         d.hard_is_int = (m.hardness >= 0.0 && m.hardness <= 4096.0 && std::floor(m.hardness) == m.hardness) ? 1 : 0;
         d.hard_int = d.hard_is_int ? (int32_t)m.hardness : 0;
+        // specular lobe provably zero: +0 specular (so +0 * pow(...) = +0 for the finite,
+        // non-negative pow) and +0-or-positive diffuse (so lambert >= +0 and lambert + 0 == lambert)
+        auto pos_zero = [](float v) { return v == 0.0f && !std::signbit(v); };
+        auto nonneg = [](float v) { return v > 0.0f || (v == 0.0f && !std::signbit(v)); };
+        d.spec_zero = pos_zero(m.specular[0]) && pos_zero(m.specular[1]) && pos_zero(m.specular[2]) &&
+                      nonneg(m.diffuse[0]) && nonneg(m.diffuse[1]) && nonneg(m.diffuse[2]) &&
+                      m.hardness >= 0.0 && m.hardness <= 1e6;  // pow(base <= 1 + eps, h) stays finite
         for (int b = 0; b < 31; ++b)
             if ((d.hard_int >> b) && H.pow_bits < b + 1) H.pow_bits = b + 1;
     }

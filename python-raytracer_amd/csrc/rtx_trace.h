@@ -118,7 +118,7 @@ struct alignas(16) DMat {
     float specular[4];
     float tint, omt;               // f32(tint), f32(1 - tint)       (scene.py:104,108)
     float eta_in, eta_out;         // f32(refr_index), f32(1 / refr_index) (scene.py:191,194)
-    int32_t type, hard_int, hard_is_int, pad;
+    int32_t type, hard_int, hard_is_int, spec_zero;
     double hardness;
 };
 
@@ -554,6 +554,9 @@ RTX_HD double spec_pow(double x, const DMat& m, int pow_bits) {
         const int n = m.hard_int;
         double r = 1.0, b = x;
         for (int k = 0; k < pow_bits; ++k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+            if (!__any(n >> k)) break;  // wave-uniform exit once no lane has bits left
+#endif
             const double rb = r * b;
             r = ((n >> k) & 1) ? rb : r;
             b = b * b;
@@ -585,11 +588,16 @@ RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const 
         if (RTX_ABLATE == 3) { colour = add(colour, mul(ld3(L.cp), diffuse)); continue; }
         f3 light_dir = L.type == LIGHT_POINT ? normalize(sdir) : ld3(L.ndir);
         f3 lambert = scale(diffuse, pos_part(dot(normal, light_dir)));
-        f3 half_vect = normalize(sub(light_dir, dir));
-        float nh = dot(normal, half_vect);
-        double base = nh > 0.0f ? (double)nh : 0.0;
-        f3 specular = scale(ld3(m.specular), (float)spec_pow(base, m, S.pow_bits));
-        colour = add(colour, mul(ld3(L.cp), add(lambert, specular)));
+        f3 ls = lambert;
+        if (!m.spec_zero) {
+            f3 half_vect = normalize(sub(light_dir, dir));
+            float nh = dot(normal, half_vect);
+            double base = nh > 0.0f ? (double)nh : 0.0;
+            f3 specular = scale(ld3(m.specular), (float)spec_pow(base, m, S.pow_bits));
+            ls = add(lambert, specular);
+        }
+        // spec_zero: specular == +0 and diffuse >= +0, so lambert + specular == lambert exactly
+        colour = add(colour, mul(ld3(L.cp), ls));
     }
     colour = add(colour, mul(ld3(S.ambient), diffuse));
     return colour;
