@@ -188,8 +188,8 @@ __global__ __launch_bounds__(256) void k_intersect(SceneView S, int64_t n, const
         nn = sf.normal;
         pp = sf.position;
     }
-    if (t_out) t_out[i] = h.obj >= 0 ? exact_t(h) : (double)INFINITY;
-    if (obj_out) obj_out[i] = h.obj >= 0 ? h.oid : -1;
+    if (t_out) t_out[i] = h.obj >= 0 ? hit_t64(S, h.obj, h.sub, o, d, time) : (double)INFINITY;
+    if (obj_out) obj_out[i] = h.obj >= 0 ? S.objs[h.obj].oid : -1;
     if (mat_out) mat_out[i] = mat;
     if (n_out) { n_out[i] = nn.x; n_out[n + i] = nn.y; n_out[2 * n + i] = nn.z; }
     if (p_out) { p_out[i] = pp.x; p_out[n + i] = pp.y; p_out[2 * n + i] = pp.z; }

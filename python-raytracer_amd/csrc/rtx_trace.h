@@ -184,32 +184,24 @@ constexpr float kEps4Up = 0x1.a36e3p-14f;      // smallest float > 1e-4
 constexpr float kEps4Near = 1e-4f;             // fl32(1e-4) (< 1e-4)
 constexpr float kEps3Near = 1e-3f;             // fl32(1e-3)
 
-// Closest-hit record: t as its fp32 proxy plus what is needed to recover the exact fp64
-// value (t64 for spheres/boxes; num/den for planes/triangles), the object (index into
-// the type-grouped array), its scene-order id, and a sub-index (box: entry slab label;
-// mesh: face index).
+// Wave-uniform predicates: true if the predicate holds in ANY / ALL active lanes (one
+// ballot on the device); the host emulation runs a single lane.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RTX_ANY(p) (__any((int)(p)) != 0)
+#define RTX_ALL(p) (__all((int)(p)) != 0)
+#else
+#define RTX_ANY(p) ((bool)(p))
+#define RTX_ALL(p) ((bool)(p))
+#endif
+
+// Closest-hit record: t as its fp32 proxy, the object (index into the type-grouped
+// array, -1 = none) and a sub-index (sphere: root; box: entry slab label; mesh: face).
+// The exact fp64 t is recomputed from (obj, sub) when two proxies tie.
 struct Hit {
     float t32;
-    float num, den;    // q = num / den when quot != 0
-    int32_t quot;
-    double t64;        // exact value when quot == 0
     int32_t obj;
-    int32_t oid;
     int32_t sub;
 };
-
-RTX_HD double exact_t(const Hit& h) { return h.quot ? (double)h.num / (double)h.den : h.t64; }
-
-// min(intersections, key=time) keeps the FIRST minimum of the list, which is ordered by
-// object and then by hit within the object (scene.py:86-94). Each object contributes only
-// its own first minimum, so comparing (t, scene-order id) lexicographically selects the
-// same hit in any visiting order.
-RTX_HD bool closer(const Hit& c, const Hit& h) {
-    if (c.t32 < h.t32) return true;
-    if (c.t32 > h.t32) return false;
-    const double a = exact_t(c), b = exact_t(h);   // equal proxies: decide in fp64
-    return a < b || (a == b && c.oid < h.oid);
-}
 
 // t64 > T for t64 = fl64(num / den), with T32 = fl32(T).
 RTX_HD bool quot_gt(float t32, float num, float den, double T, float T32) {
@@ -319,156 +311,191 @@ RTX_HD bool mesh_bv(const DObj& ob, f3 o, f3 d) {
     return (-b + s) / two_a > 0.0;
 }
 
-// ------------------------------------------------------------------ closest hit
-template <bool COUNT>
-RTX_HD void mesh_closest(const SceneView& S, const DObj& ob, int oi, f3 o, f3 d, Hit& h, Tally& tl) {
-    // mesh.py:72-119: every face in order; the first strict minimum within the mesh wins.
-    if (!mesh_bv(ob, o, d)) return;
-    const int32_t f0 = ob.tri_begin, nf = ob.tri_count;
-    Hit best;
-    best.t32 = INFINITY; best.num = 0.0f; best.den = 1.0f; best.quot = 1; best.sub = -1;
-    for (int f = 0; f < nf; ++f) {
-        const DTri T = S.tris[f0 + f];
-        tally_inc<COUNT>(tl, &Tally::tri);
-        const f3 n = ld3(T.n);
-        const float denom = dot(d, n);
-        if (fabsf(denom) < kEps4Up) continue;                 // abs(denom) < epsilon
-        const f3 v0 = ld3(T.v0);
-        const float num = dot(sub(v0, o), n);
-        const float t32 = num / denom;
-        if (quot_neg(t32, num, denom)) continue;              // time < 0
-        const f3 p = add(o, scale(d, t32));                  // getPoint(time)
-        const float b0 = dot(cross(ld3(T.e01), sub(p, v0)), n);
-        const float b1 = dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n);
-        const float b2 = dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n);
-        if (b0 >= 0.0f && b1 >= 0.0f && b2 >= 0.0f) {
-            bool take = t32 < best.t32;
-            if (t32 == best.t32) take = (double)num / (double)denom < exact_t(best);
-            if (take) { best.t32 = t32; best.num = num; best.den = denom; best.sub = f; }
-        }
+// Exact fp64 t of a candidate, recomputed from the object exactly as during its test
+// (used only when two fp32 proxies tie).
+RTX_HD double hit_t64(const SceneView& S, int32_t obj, int32_t sb, f3 o, f3 d, float time) {
+    const DObj ob = S.objs[obj];
+    if (ob.type == OBJ_PLANE) {
+        const f3 n = ld3(ob.b);
+        return (double)dot(sub(moved(ob, ob.a, time), o), n) / (double)dot(d, n);
     }
-    if (best.sub >= 0) {
-        best.oid = ob.oid;
-        best.obj = oi;
-        best.t64 = 0.0;
-        if (closer(best, h)) h = best;
+    if (ob.type == OBJ_SPHERE) {
+        double b = 0.0, s = 0.0, two_a = 1.0;
+        sphere_roots(o, d, moved(ob, ob.a, time), ob.r2, b, s, two_a);
+        return sb == 0 ? (-b - s) / two_a : (-b + s) / two_a;
     }
+    if (ob.type == OBJ_BOX) {
+        double start = 0.0, end = 0.0;
+        int label = 0;
+        box_slabs(o, d, moved(ob, ob.a, time), moved(ob, ob.b, time), start, label, end);
+        return start;
+    }
+    const DTri T = S.tris[ob.tri_begin + sb];
+    const f3 n = ld3(T.n);
+    return (double)dot(sub(ld3(T.v0), o), n) / (double)dot(d, n);
 }
 
+// min(intersections, key=time) keeps the FIRST minimum of the list, which is ordered by
+// object and then by hit within the object (scene.py:86-94). Candidates are offered in
+// any object order but in hit order within an object; a candidate replaces the record
+// iff its t is smaller, or equal with a smaller scene-order id. Proxies decide unless
+// they are equal; then the exact fp64 values (and the ids) do.
+RTX_HD void offer(const SceneView& S, Hit& h, bool valid, float t32, int32_t obj, int32_t sb, f3 o, f3 d,
+                  float time) {
+    bool take = valid && t32 < h.t32;
+    const bool tie = valid && t32 == h.t32;
+    if (tie) {
+        const double a = hit_t64(S, obj, sb, o, d, time);
+        if (h.obj < 0) {
+            take = a < INFINITY;
+        } else {
+            const double b = hit_t64(S, h.obj, h.sub, o, d, time);
+            take = a < b || (a == b && S.objs[obj].oid < S.objs[h.obj].oid);
+        }
+    }
+    h.t32 = take ? t32 : h.t32;
+    h.obj = take ? obj : h.obj;
+    h.sub = take ? sb : h.sub;
+}
+
+// ------------------------------------------------------------------ closest hit
 template <bool MESH, bool COUNT>
 RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl) {
-    Hit h;
-    h.t32 = INFINITY; h.num = 0.0f; h.den = 1.0f; h.quot = 0; h.t64 = INFINITY;
-    h.obj = -1; h.oid = 0x7fffffff; h.sub = 0;
-    Hit c;
+    Hit h{INFINITY, -1, 0};
     int oi = 0;
     for (int k = 0; k < S.n_plane; ++k, ++oi) {  // simple_geometry.py:105-120
         const DObj ob = S.objs[oi];
         const f3 n = ld3(ob.b);
         const float denom = dot(d, n);
-        if (fabsf(denom) >= kEps4Up) {                       // abs(denom) > epsilon
-            const float num = dot(sub(moved(ob, ob.a, time), o), n);
-            const float t32 = num / denom;
-            if (quot_nonneg(t32, num, denom)) {              // t >= 0
-                c.t32 = t32; c.num = num; c.den = denom; c.quot = 1; c.t64 = 0.0;
-                c.obj = oi; c.oid = ob.oid; c.sub = 0;
-                if (closer(c, h)) h = c;
-            }
-        }
+        const float num = dot(sub(moved(ob, ob.a, time), o), n);
+        const float t32 = num / denom;
+        // abs(denom) > epsilon and t >= 0
+        const bool valid = fabsf(denom) >= kEps4Up && quot_nonneg(t32, num, denom);
+        offer(S, h, valid, t32, oi, 0, o, d, time);
     }
     for (int k = 0; k < S.n_sphere; ++k, ++oi) {  // simple_geometry.py:20-46
         const DObj ob = S.objs[oi];
         const f3 ctr = moved(ob, ob.a, time);
-        if (sphere_disc_sign(o, d, ctr, (float)ob.r2) < 0) continue;
-        double b, s, two_a;
-        if (sphere_roots(o, d, ctr, ob.r2, b, s, two_a)) {
-            double t = (-b - s) / two_a;
-            int32_t root = 0;
-            if (!(t > 0.0)) { t = (-b + s) / two_a; root = 1; }
-            if (t > 0.0) {
-                c.t32 = (float)t; c.quot = 0; c.t64 = t; c.num = 0.0f; c.den = 1.0f;
-                c.obj = oi; c.oid = ob.oid; c.sub = root;
-                if (closer(c, h)) h = c;
+        bool valid = false;
+        float t32 = INFINITY;
+        int32_t root = 0;
+        if (sphere_disc_sign(o, d, ctr, (float)ob.r2) >= 0) {  // fp64 only where a hit is possible
+            double b, s, two_a;
+            if (sphere_roots(o, d, ctr, ob.r2, b, s, two_a)) {
+                double t = (-b - s) / two_a;
+                if (!(t > 0.0)) { t = (-b + s) / two_a; root = 1; }
+                valid = t > 0.0;
+                t32 = (float)t;
             }
         }
+        offer(S, h, valid, t32, oi, root, o, d, time);
     }
     for (int k = 0; k < S.n_box; ++k, ++oi) {  // simple_geometry.py:188-249 (entry precedes exit)
         const DObj ob = S.objs[oi];
-        double start, end;
-        int label;
-        if (box_slabs(o, d, moved(ob, ob.a, time), moved(ob, ob.b, time), start, label, end)) {
-            if (!(start > end || start < 0.0)) {
-                c.t32 = (float)start; c.quot = 0; c.t64 = start; c.num = 0.0f; c.den = 1.0f;
-                c.obj = oi; c.oid = ob.oid; c.sub = label;
-                if (closer(c, h)) h = c;
-            }
-        }
-    }
-    if (MESH)
-        for (int k = 0; k < S.n_mesh; ++k, ++oi) mesh_closest<COUNT>(S, (DObj)S.objs[oi], oi, o, d, h, tl);
-    return h;
-}
-
-// ------------------------------------------------------------------ shadow any-hit
-// Any order gives the same answer; cheap objects first. T32max = fl32(t_max).
-template <bool MESH, bool COUNT>
-RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, Tally& tl) {
-    const float tmax32 = (float)t_max;
-    int oi = 0;
-    for (int k = 0; k < S.n_plane; ++k, ++oi) {  // simple_geometry.py:122-131
-        const DObj ob = S.objs[oi];
-        const f3 n = ld3(ob.b);
-        const float denom = dot(d, n);
-        if (fabsf(denom) >= kEps4Up) {
-            const float num = dot(sub(moved(ob, ob.a, time), o), n);
-            const float t32 = num / denom;
-            if (quot_gt(t32, num, denom, 1e-4, kEps4Near) && quot_lt(t32, num, denom, t_max, tmax32)) return true;
-        }
-    }
-    for (int k = 0; k < S.n_sphere; ++k, ++oi) {  // simple_geometry.py:48-72 (shadow_epsilon 1e-3)
-        const DObj ob = S.objs[oi];
-        const f3 ctr = moved(ob, ob.a, time);
-        if (sphere_disc_sign(o, d, ctr, (float)ob.r2) < 0) continue;
-        double b, s, two_a;
-        if (sphere_roots(o, d, ctr, ob.r2, b, s, two_a)) {
-            double t = (-b - s) / two_a;
-            if (1e-3 < t && t < t_max) return true;
-            t = (-b + s) / two_a;
-            if (1e-3 < t && t < t_max) return true;
-        }
-    }
-    for (int k = 0; k < S.n_box; ++k, ++oi) {  // simple_geometry.py:251-294
-        const DObj ob = S.objs[oi];
-        double start, end;
-        int label;
-        if (box_slabs(o, d, moved(ob, ob.a, time), moved(ob, ob.b, time), start, label, end)) {
-            if (!(start > end) && 1e-4 < start && start < t_max) return true;
-        }
+        double start = 0.0, end = 0.0;
+        int label = 0;
+        bool valid = box_slabs(o, d, moved(ob, ob.a, time), moved(ob, ob.b, time), start, label, end);
+        valid = valid && !(start > end || start < 0.0);
+        offer(S, h, valid, (float)start, oi, label, o, d, time);
     }
     if (MESH) {
-        for (int k = 0; k < S.n_mesh; ++k, ++oi) {  // mesh.py:121-153 (no t_max test)
+        for (int k = 0; k < S.n_mesh; ++k, ++oi) {  // mesh.py:72-119, faces in order
             const DObj ob = S.objs[oi];
             if (!mesh_bv(ob, o, d)) continue;
             const int32_t f0 = ob.tri_begin, nf = ob.tri_count;
             for (int f = 0; f < nf; ++f) {
                 const DTri T = S.tris[f0 + f];
                 tally_inc<COUNT>(tl, &Tally::tri);
-                const f3 n = ld3(T.nu);
+                const f3 n = ld3(T.n);
                 const float denom = dot(d, n);
-                if (fabsf(denom) < kEps4Up) continue;
                 const f3 v0 = ld3(T.v0);
                 const float num = dot(sub(v0, o), n);
                 const float t32 = num / denom;
-                if (quot_lt(t32, num, denom, 1e-4, kEps4Near)) continue;  // time < shadow_epsilon
-                const f3 p = add(o, scale(d, t32));
-                if (dot(cross(ld3(T.e01), sub(p, v0)), n) >= 0.0f &&
-                    dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n) >= 0.0f &&
-                    dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n) >= 0.0f)
-                    return true;
+                // abs(denom) < epsilon -> skip; time < 0 -> skip
+                bool valid = !(fabsf(denom) < kEps4Up) && !quot_neg(t32, num, denom);
+                const f3 p = add(o, scale(d, t32));  // getPoint(time)
+                const float b0 = dot(cross(ld3(T.e01), sub(p, v0)), n);
+                const float b1 = dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n);
+                const float b2 = dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n);
+                valid = valid && b0 >= 0.0f && b1 >= 0.0f && b2 >= 0.0f;
+                offer(S, h, valid, t32, oi, f, o, d, time);
             }
         }
     }
-    return false;
+    return h;
+}
+
+// ------------------------------------------------------------------ shadow any-hit
+// Any order gives the same answer; cheap objects first, and the wave leaves as soon as
+// every active lane is occluded.
+template <bool MESH, bool COUNT>
+RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, Tally& tl) {
+    const float tmax32 = (float)t_max;
+    bool occ = false;
+    int oi = 0;
+    for (int k = 0; k < S.n_plane; ++k, ++oi) {  // simple_geometry.py:122-131
+        const DObj ob = S.objs[oi];
+        const f3 n = ld3(ob.b);
+        const float denom = dot(d, n);
+        const float num = dot(sub(moved(ob, ob.a, time), o), n);
+        const float t32 = num / denom;
+        const bool hit = fabsf(denom) >= kEps4Up && quot_gt(t32, num, denom, 1e-4, kEps4Near) &&
+                         quot_lt(t32, num, denom, t_max, tmax32);
+        occ = occ || hit;
+    }
+    if (RTX_ALL(occ)) return true;
+    for (int k = 0; k < S.n_sphere; ++k, ++oi) {  // simple_geometry.py:48-72 (shadow_epsilon 1e-3)
+        const DObj ob = S.objs[oi];
+        const f3 ctr = moved(ob, ob.a, time);
+        if (!occ && sphere_disc_sign(o, d, ctr, (float)ob.r2) >= 0) {
+            double b, s, two_a;
+            if (sphere_roots(o, d, ctr, ob.r2, b, s, two_a)) {
+                const double t1 = (-b - s) / two_a;
+                bool hit = 1e-3 < t1 && t1 < t_max;
+                if (!hit) {
+                    const double t2 = (-b + s) / two_a;
+                    hit = 1e-3 < t2 && t2 < t_max;
+                }
+                occ = hit;
+            }
+        }
+    }
+    if (RTX_ALL(occ)) return true;
+    for (int k = 0; k < S.n_box; ++k, ++oi) {  // simple_geometry.py:251-294
+        const DObj ob = S.objs[oi];
+        if (!occ) {
+            double start, end;
+            int label;
+            if (box_slabs(o, d, moved(ob, ob.a, time), moved(ob, ob.b, time), start, label, end))
+                occ = !(start > end) && 1e-4 < start && start < t_max;
+        }
+    }
+    if (MESH) {
+        for (int k = 0; k < S.n_mesh; ++k, ++oi) {  // mesh.py:121-153 (no t_max test)
+            const DObj ob = S.objs[oi];
+            if (RTX_ALL(occ)) break;
+            if (occ || !mesh_bv(ob, o, d)) continue;
+            const int32_t f0 = ob.tri_begin, nf = ob.tri_count;
+            for (int f = 0; f < nf; ++f) {
+                if (RTX_ALL(occ)) break;
+                const DTri T = S.tris[f0 + f];
+                tally_inc<COUNT>(tl, &Tally::tri);
+                const f3 n = ld3(T.nu);
+                const float denom = dot(d, n);
+                const f3 v0 = ld3(T.v0);
+                const float num = dot(sub(v0, o), n);
+                const float t32 = num / denom;
+                // abs(denom) < epsilon -> skip; time < shadow_epsilon -> skip
+                bool hit = !(fabsf(denom) < kEps4Up) && !quot_lt(t32, num, denom, 1e-4, kEps4Near);
+                const f3 p = add(o, scale(d, t32));
+                hit = hit && dot(cross(ld3(T.e01), sub(p, v0)), n) >= 0.0f &&
+                      dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n) >= 0.0f &&
+                      dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n) >= 0.0f;
+                occ = occ || hit;
+            }
+        }
+    }
+    return occ;
 }
 
 // ------------------------------------------------------------------ hit record

@@ -89,7 +89,8 @@ extern "C" int rtx_hostemu_intersect(const rtx_scene_desc* sd, int64_t n, const 
             Surface sf = H.has_mesh ? resolve_hit<true>(v, h, o, d, (float)time) : resolve_hit<false>(v, h, o, d, (float)time);
             mat = sf.mat; nn = sf.normal; pp = sf.position;
         }
-        t_out[i] = h.obj >= 0 ? exact_t(h) : (double)INFINITY; obj_out[i] = h.obj >= 0 ? h.oid : -1; mat_out[i] = mat;
+        t_out[i] = h.obj >= 0 ? hit_t64(v, h.obj, h.sub, o, d, (float)time) : (double)INFINITY;
+        obj_out[i] = h.obj >= 0 ? v.objs[h.obj].oid : -1; mat_out[i] = mat;
         n_out[i] = nn.x; n_out[n + i] = nn.y; n_out[2 * n + i] = nn.z;
         p_out[i] = pp.x; p_out[n + i] = pp.y; p_out[2 * n + i] = pp.z;
     }
