@@ -312,8 +312,8 @@ RTX_HD bool mesh_bv(const DObj& ob, f3 o, f3 d) {
 }
 
 // Exact fp64 t of a candidate, recomputed from the object exactly as during its test
-// (used only when two fp32 proxies tie).
-RTX_HD double hit_t64(const SceneView& S, int32_t obj, int32_t sb, f3 o, f3 d, float time) {
+// (used only when two fp32 proxies tie; out of line to keep the hot loop's registers low).
+__host__ __device__ __attribute__((noinline)) inline double hit_t64(const SceneView& S, int32_t obj, int32_t sb, f3 o, f3 d, float time) {
     const DObj ob = S.objs[obj];
     if (ob.type == OBJ_PLANE) {
         const f3 n = ld3(ob.b);
@@ -569,6 +569,11 @@ RTX_HD Surface resolve_hit(const SceneView& S, const Hit& h, f3 o, f3 d, float t
 }
 
 // ------------------------------------------------------------------ shading
+// General fp64 pow for non-integer exponents, kept out of line: the inlined libm path
+// would raise the kernel's register allocation (occupancy) for a case the reference
+// scenes never use.
+__host__ __device__ __attribute__((noinline)) inline double pow_general(double x, double y) { return pow(x, y); }
+
 // `x ** hardness` (CPython float_pow -> pow) in fp64. Integer exponents use binary
 // exponentiation; the fp32 cast that follows makes it equal to libm pow except when the
 // exact value lies within a few fp64 ulps of an fp32 rounding boundary. The loop runs a
@@ -590,7 +595,7 @@ RTX_HD double spec_pow(double x, const DMat& m, int pow_bits) {
         }
         return r;
     }
-    return pow(x, m.hardness);
+    return pow_general(x, m.hardness);
 }
 
 // _compute_regular_lighting (scene.py:140-187)
