@@ -77,7 +77,8 @@ __device__ __forceinline__ void flush_tally(const Tally& tl, unsigned long long*
 // scene.py:47-79 for pixel p of the output block (host/device: the tests-only host
 // emulation runs the same body).
 template <bool MESH, bool SEC, bool COUNT, bool JIT>
-RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, int32_t cc, Tally& tl) {
+RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, int32_t cc, Tally& tl,
+                         const FrameStack& fs) {
     const int64_t p = (int64_t)rr * P.ncols + cc;
     const int j = P.height - 1 - (row0 + rr);  // reference row index (y grows upward)
     const float fx = P.xs[cc];
@@ -104,7 +105,7 @@ RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, 
                 o = add(o, scale(normalize(rnd), P.jscale));
             }
             for (int kt = 0; kt < P.n_times; ++kt)
-                colour = add(colour, cast_ray<MESH, SEC, COUNT>(P.S, o, ddir, P.times[kt], tl));
+                colour = add(colour, cast_ray<MESH, SEC, COUNT>(P.S, o, ddir, P.times[kt], tl, fs));
         }
     }
     // colour / (samples * dof_samples * len(motion_times)) (scene.py:73); for a power of
@@ -166,7 +167,10 @@ __global__ __launch_bounds__(256, RTX_LB_WAVES(MESH, SEC)) void k_render(const K
     const PixelRC px = pixel_rc(ncols);
     const bool active = px.r < L.nrows && px.c < ncols;
     Tally tl = {};
-    if (active) render_pixel<MESH, SEC, COUNT, JIT>(*Pp, L.fb, L.row0, px.r, px.c, tl);
+    // secondary-ray frames: [frame][word][thread] in LDS (40 KB per 256-thread block)
+    __shared__ float frames[SEC ? kMaxDepth * 4 * 256 : 1];
+    const FrameStack fs{frames + threadIdx.x, 256};
+    if (active) render_pixel<MESH, SEC, COUNT, JIT>(*Pp, L.fb, L.row0, px.r, px.c, tl, fs);
     flush_tally<COUNT>(tl, L.counters, active);
 }
 

@@ -637,62 +637,75 @@ RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const 
 
 // ------------------------------------------------------------------ cast_ray, iteratively
 // scene.py:81-116 + _compute_refraction (:189-209). Secondary rays form a chain (one
-// reflect or refract child per level), so the recursion becomes a loop that records
-// (lighting, tint, 1 - tint) per mirror/refractive level and unwinds bottom-up with the
-// per-level clamp. Frames live in registers: only constant indices touch the arrays.
+// reflect or refract child per level), so the recursion becomes a loop that records one
+// frame (lighting RGB, material) per mirror/refractive level and unwinds bottom-up with
+// the per-level clamp: colour = clamp(L * tint + child * (1 - tint)). Frames live in a
+// caller-provided store: LDS on the device ([frame][word][thread], conflict-free), a
+// local array in the host emulation.
+struct FrameStack {
+    float* base;
+    int stride;
+    RTX_HD void put(int k, f3 L, int32_t mat) const {
+        float* p = base + k * 4 * stride;
+        p[0] = L.x;
+        p[stride] = L.y;
+        p[2 * stride] = L.z;
+        p[3 * stride] = __builtin_bit_cast(float, mat);
+    }
+    RTX_HD f3 get(int k, int32_t& mat) const {
+        const float* p = base + k * 4 * stride;
+        mat = __builtin_bit_cast(int32_t, p[3 * stride]);
+        return f3{p[0], p[stride], p[2 * stride]};
+    }
+};
+
 template <bool MESH, bool SEC, bool COUNT>
-RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl) {
-    constexpr int NF = SEC ? kMaxDepth : 1;
-    float fr_r[NF], fr_g[NF], fr_b[NF], fr_t[NF], fr_o[NF];
-#pragma unroll
-    for (int k = 0; k < NF; ++k) { fr_r[k] = fr_g[k] = fr_b[k] = fr_t[k] = fr_o[k] = 0.0f; }
+RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const FrameStack& fs) {
     int nfr = 0;
     f3 tail = mk(0.0f, 0.0f, 0.0f);
     bool in_shape = false;
     for (int level = 0; level < (SEC ? kMaxDepth : 1); ++level) {
         if (COUNT) tl.cast[level]++;
-        Hit h = closest_hit<MESH, COUNT>(S, o, d, time, tl);
+        const Hit h = closest_hit<MESH, COUNT>(S, o, d, time, tl);
         if (h.obj < 0) break;  // miss -> black
-        Surface sf = resolve_hit<MESH>(S, h, o, d, time);
+        const Surface sf = resolve_hit<MESH>(S, h, o, d, time);
         const DMat m = S.mats[sf.mat];
-        if (SEC && m.type == MAT_MIRROR) {
-            f3 rdir = reflect(d, sf.normal);
-            f3 L = regular_lighting<MESH, COUNT>(S, d, sf.position, sf.normal, m, time, tl);
-#pragma unroll
-            for (int k = 0; k < NF; ++k)
-                if (k == nfr) { fr_r[k] = L.x; fr_g[k] = L.y; fr_b[k] = L.z; fr_t[k] = m.tint; fr_o[k] = m.omt; }
-            ++nfr;
-            o = add(sf.position, scale(rdir, 0.01f));
-            d = rdir;
-            in_shape = false;
-            continue;
+        f3 n = sf.normal;
+        bool chain = false, tir = false;
+        f3 next_o = o, next_d = d;
+        if (SEC && m.type == MAT_MIRROR) {  // reflect; child with in_shape = False
+            const f3 rdir = reflect(d, n);
+            next_o = add(sf.position, scale(rdir, 0.01f));
+            next_d = rdir;
+            chain = true;
+        } else if (SEC && m.type == MAT_REFRACTIVE) {  // the negated normal also shades
+            const float eta = in_shape ? m.eta_in : m.eta_out;
+            if (in_shape) n = neg(n);
+            const f3 rdir = refract(d, n, eta);
+            tir = is_zero(rdir);  // total internal reflection -> black child
+            next_o = add(sf.position, scale(rdir, 0.0001f));
+            next_d = rdir;
+            chain = true;
         }
-        if (SEC && m.type == MAT_REFRACTIVE) {
-            float eta = in_shape ? m.eta_in : m.eta_out;
-            f3 n = in_shape ? neg(sf.normal) : sf.normal;
-            f3 rdir = refract(d, n, eta);
-            f3 L = regular_lighting<MESH, COUNT>(S, d, sf.position, n, m, time, tl);
-#pragma unroll
-            for (int k = 0; k < NF; ++k)
-                if (k == nfr) { fr_r[k] = L.x; fr_g[k] = L.y; fr_b[k] = L.z; fr_t[k] = m.tint; fr_o[k] = m.omt; }
-            ++nfr;
-            if (is_zero(rdir)) break;  // total internal reflection -> black child
-            o = add(sf.position, scale(rdir, 0.0001f));
-            d = rdir;
-            in_shape = !in_shape;
-            continue;
+        if (RTX_ABLATE == 2 && !chain) { tail = ld3(m.diffuse); break; }
+        const f3 L = regular_lighting<MESH, COUNT>(S, d, sf.position, n, m, time, tl);
+        if (!SEC || !chain) {
+            tail = clamp01(L);
+            break;
         }
-        if (RTX_ABLATE == 2) { tail = ld3(m.diffuse); break; }
-        tail = clamp01(regular_lighting<MESH, COUNT>(S, d, sf.position, sf.normal, m, time, tl));
-        break;
+        fs.put(nfr, L, sf.mat);
+        ++nfr;
+        if (tir) break;
+        in_shape = m.type == MAT_REFRACTIVE ? !in_shape : false;
+        o = next_o;
+        d = next_d;
     }
     if (SEC) {
-#pragma unroll
-        for (int k = NF - 1; k >= 0; --k) {
-            if (k < nfr) {
-                f3 c = add(scale(mk(fr_r[k], fr_g[k], fr_b[k]), fr_t[k]), scale(tail, fr_o[k]));
-                tail = clamp01(c);
-            }
+        for (int k = nfr - 1; k >= 0; --k) {
+            int32_t mi;
+            const f3 L = fs.get(k, mi);
+            const DMat m = S.mats[mi];
+            tail = clamp01(add(scale(L, m.tint), scale(tail, m.omt)));
         }
     }
     return tail;

@@ -45,18 +45,20 @@ extern "C" int rtx_hostemu_render(const rtx_scene_desc* sd, const rtx_camera_des
 #pragma omp for schedule(dynamic, 64)
         for (int64_t p = 0; p < npix; ++p) {
             Tally tl = {};
+            float frames[kMaxDepth * 4];
+            const FrameStack fs{frames, 1};
             const int32_t rr = (int32_t)(p / k.ncols), cc = (int32_t)(p % k.ncols);
             const bool jit = k.jitter != RTX_JITTER_OFF;
             if (H.has_mesh) {
-                if (H.has_secondary) jit ? render_pixel<true, true, true, true>(k, fb, row0, rr, cc, tl)
-                                         : render_pixel<true, true, true, false>(k, fb, row0, rr, cc, tl);
-                else jit ? render_pixel<true, false, true, true>(k, fb, row0, rr, cc, tl)
-                         : render_pixel<true, false, true, false>(k, fb, row0, rr, cc, tl);
+                if (H.has_secondary) jit ? render_pixel<true, true, true, true>(k, fb, row0, rr, cc, tl, fs)
+                                         : render_pixel<true, true, true, false>(k, fb, row0, rr, cc, tl, fs);
+                else jit ? render_pixel<true, false, true, true>(k, fb, row0, rr, cc, tl, fs)
+                         : render_pixel<true, false, true, false>(k, fb, row0, rr, cc, tl, fs);
             } else {
-                if (H.has_secondary) jit ? render_pixel<false, true, true, true>(k, fb, row0, rr, cc, tl)
-                                         : render_pixel<false, true, true, false>(k, fb, row0, rr, cc, tl);
-                else jit ? render_pixel<false, false, true, true>(k, fb, row0, rr, cc, tl)
-                         : render_pixel<false, false, true, false>(k, fb, row0, rr, cc, tl);
+                if (H.has_secondary) jit ? render_pixel<false, true, true, true>(k, fb, row0, rr, cc, tl, fs)
+                                         : render_pixel<false, true, true, false>(k, fb, row0, rr, cc, tl, fs);
+                else jit ? render_pixel<false, false, true, true>(k, fb, row0, rr, cc, tl, fs)
+                         : render_pixel<false, false, true, false>(k, fb, row0, rr, cc, tl, fs);
             }
             for (int q = 0; q < kMaxDepth; ++q) loc[q] += tl.cast[q];
             loc[RTX_CNT_SHADOW] += tl.shadow;
