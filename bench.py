@@ -48,6 +48,7 @@ def parse():
     p.add_argument("--rowblock", action="store_true", help="also time row-block + RCCL gather of one frame")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--force-dist", action="store_true", help="initialise torch.distributed even for one rank (tests)")
     p.add_argument("--pmc-json", default=None,
                    help="tools/pmc_summary.py output for this config (default profiles/pmc_<config>.json)")
     return p.parse_args()
@@ -121,7 +122,8 @@ def main():
         if world == 1 and a.gpus > 1:
             sys.exit("--gpus %d needs torch.distributed.run with %d processes" % (a.gpus, a.gpus))
     torch.cuda.set_device(local)
-    if world > 1:
+    use_dist = world > 1 or a.force_dist
+    if use_dist:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import rtx  # noqa: F401
     from rtx.scene import split_rows
@@ -148,7 +150,7 @@ def main():
     # HIP events on the launch stream bracket the whole timed region (events between
     # launches would insert ~10 us gaps on ROCm); kernel time = elapsed / steps.
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -157,12 +159,12 @@ def main():
         sc.render_device(out=fb, stream=stream)
     e1.record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     t1 = time.perf_counter()
     wall = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
     kern = torch.tensor([e0.elapsed_time(e1) / a.steps], dtype=torch.float64, device="cuda")
-    if world > 1:
+    if use_dist:
         dist.all_reduce(wall, op=dist.ReduceOp.MAX)
         dist.all_reduce(kern, op=dist.ReduceOp.MAX)
     wall_s = float(wall.item())
@@ -172,7 +174,7 @@ def main():
     value = samples_per_step * a.steps / wall_s / 1e6
 
     rowblock = None
-    if a.rowblock and world > 1:
+    if a.rowblock and use_dist:
         from rtx.distributed import render_frame
         for _ in range(3):
             render_frame(sc, rank, world, dtype=torch.uint8)
@@ -217,7 +219,7 @@ def main():
         if world == 1 and not a.no_cpu_baseline and a.cpu_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(a.config, a.cpu_seconds)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 
