@@ -11,6 +11,7 @@
 //   k_to_rgb8     (v * 255.0) truncated to uint8 (main.py:327)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -232,6 +233,8 @@ struct HostScene {
     std::vector<DObj> objs;
     std::vector<DTri> tris;
     std::vector<DTriN> trins;
+    std::vector<DLeaf> leaves;
+    std::vector<int32_t> tri_orig;
     std::vector<DMat> mats;
     std::vector<DLight> lights;
     bool has_mesh = false, has_secondary = false;
@@ -380,6 +383,69 @@ int convert_scene(const rtx_scene_desc* desc, HostScene& H) {
             }
     H.objs.swap(grouped);
     H.n_plane = counts[0]; H.n_sphere = counts[1]; H.n_box = counts[2]; H.n_mesh = counts[3];
+    // Mesh face clusters: reorder each mesh's faces into spatially coherent leaves of <= 8
+    // faces (median splits on face centroids) and record each face's OBJ order index.
+    H.tri_orig.assign(desc->n_triangles, 0);
+    for (DObj& d : H.objs) {
+        if (d.type != RTX_MESH) continue;
+        const int32_t b0 = d.tri_begin, n = d.tri_count;
+        std::vector<int32_t> idx(n);
+        for (int32_t i = 0; i < n; ++i) idx[i] = i;
+        auto centroid = [&](int32_t i, int ax) {
+            const DTri& t = H.tris[b0 + i];
+            return (double)t.v0[ax] + (double)t.v1[ax] + (double)t.v2[ax];
+        };
+        const int32_t leaf0 = (int32_t)H.leaves.size();
+        std::vector<std::pair<int32_t, int32_t>> stack{{0, n}};
+        std::vector<std::pair<int32_t, int32_t>> ranges;
+        while (!stack.empty()) {
+            auto [a, e] = stack.back();
+            stack.pop_back();
+            if (e - a <= 8) { ranges.push_back({a, e}); continue; }
+            double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            for (int32_t k = a; k < e; ++k)
+                for (int ax = 0; ax < 3; ++ax) {
+                    const double c = centroid(idx[k], ax);
+                    lo[ax] = std::min(lo[ax], c);
+                    hi[ax] = std::max(hi[ax], c);
+                }
+            int ax = 0;
+            for (int q = 1; q < 3; ++q)
+                if (hi[q] - lo[q] > hi[ax] - lo[ax]) ax = q;
+            const int32_t mid = (a + e) / 2;
+            std::nth_element(idx.begin() + a, idx.begin() + mid, idx.begin() + e,
+                             [&](int32_t x, int32_t y) { return centroid(x, ax) < centroid(y, ax); });
+            stack.push_back({mid, e});
+            stack.push_back({a, mid});
+        }
+        std::vector<DTri> tris(n);
+        std::vector<DTriN> trins(n);
+        float cmax = 0.0f;
+        for (auto [a, e] : ranges) {
+            DLeaf L;
+            L.first = a;
+            L.count = e - a;
+            for (int ax = 0; ax < 3; ++ax) { L.lo[ax] = INFINITY; L.hi[ax] = -INFINITY; }
+            for (int32_t k = a; k < e; ++k) {
+                const DTri& t = H.tris[b0 + idx[k]];
+                tris[k] = t;
+                trins[k] = H.trins[b0 + idx[k]];
+                H.tri_orig[b0 + k] = idx[k];
+                for (const float* v : {t.v0, t.v1, t.v2})
+                    for (int ax = 0; ax < 3; ++ax) {
+                        L.lo[ax] = std::min(L.lo[ax], v[ax]);
+                        L.hi[ax] = std::max(L.hi[ax], v[ax]);
+                        cmax = std::max(cmax, std::fabs(v[ax]));
+                    }
+            }
+            H.leaves.push_back(L);
+        }
+        std::copy(tris.begin(), tris.end(), H.tris.begin() + b0);
+        std::copy(trins.begin(), trins.end(), H.trins.begin() + b0);
+        d.leaf_begin = leaf0;
+        d.leaf_count = (int32_t)H.leaves.size() - leaf0;
+        d.cmax = cmax;
+    }
     H.n_objs = desc->n_objects;
     H.n_lights = desc->n_lights;
     set3(H.ambient, desc->ambient);
@@ -433,6 +499,8 @@ struct rtx_scene {
     void* d_trins = nullptr;
     void* d_mats = nullptr;
     void* d_lights = nullptr;
+    void* d_leaves = nullptr;
+    void* d_tri_orig = nullptr;
     // camera
     bool cam_set = false;
     KParams kp{};
@@ -465,7 +533,8 @@ void free_camera(rtx_scene* s) {
 
 void free_scene(rtx_scene* s) {
     free_camera(s);
-    for (void* p : {s->d_objs, s->d_tris, s->d_trins, s->d_mats, s->d_lights}) (void)hipFree(p);
+    for (void* p : {s->d_objs, s->d_tris, s->d_trins, s->d_mats, s->d_lights, s->d_leaves, s->d_tri_orig})
+        (void)hipFree(p);
     delete s;
 }
 
@@ -486,7 +555,8 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
     rtx_scene* s = new rtx_scene();
     if (hipGetDevice(&s->device) != hipSuccess) { delete s; return fail(RTX_ERR_HIP, "hipGetDevice failed"); }
     if ((rc = upload(&s->d_objs, H.objs)) || (rc = upload(&s->d_tris, H.tris)) || (rc = upload(&s->d_trins, H.trins)) ||
-        (rc = upload(&s->d_mats, H.mats)) || (rc = upload(&s->d_lights, H.lights))) {
+        (rc = upload(&s->d_mats, H.mats)) || (rc = upload(&s->d_lights, H.lights)) ||
+        (rc = upload(&s->d_leaves, H.leaves)) || (rc = upload(&s->d_tri_orig, H.tri_orig))) {
         free_scene(s);
         return rc;
     }
@@ -498,6 +568,8 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
     v.trins = (cptr<DTriN>)s->d_trins;
     v.mats = (cptr<DMat>)s->d_mats;
     v.lights = (cptr<DLight>)s->d_lights;
+    v.leaves = (cptr<DLeaf>)s->d_leaves;
+    v.tri_orig = (cptr<int32_t>)s->d_tri_orig;
     v.n_objs = H.n_objs;
     v.n_lights = H.n_lights;
     v.n_plane = H.n_plane; v.n_sphere = H.n_sphere; v.n_box = H.n_box; v.n_mesh = H.n_mesh;

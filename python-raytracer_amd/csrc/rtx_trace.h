@@ -90,7 +90,8 @@ RTX_HD f3 clamp01(f3 c) { return f3{clamp01(c.x), clamp01(c.y), clamp01(c.z)}; }
 struct alignas(16) DObj {
     int32_t type, nmat, mat0, mat1;
     int32_t has_speed, tri_begin, tri_count, bv_type;
-    int32_t flat, oid, pad1, pad2;
+    int32_t flat, oid, leaf_begin, leaf_count;   // mesh: face clusters (DLeaf range)
+    float cmax, pad3, pad4, pad5;                // mesh: max |vertex coordinate|
     float a[4];       // sphere centre | plane point | box minpos
     float b[4];       // plane normal | box maxpos
     float c[4];       // plane width axis
@@ -111,6 +112,16 @@ struct alignas(16) DTri {
 
 struct alignas(16) DTriN {
     float n0[4], n1[4], n2[4];     // smooth vertex normals (mesh.py:53-70)
+};
+
+// A cluster of <= 8 spatially sorted faces of one mesh with the bounds of their vertices.
+// Used only to skip faces conservatively (see leaf_maybe_hit); faces keep their original
+// index for tie breaks (tri_orig).
+struct alignas(16) DLeaf {
+    float lo[3];
+    int32_t first;                 // into the mesh's (cluster-ordered) faces
+    float hi[3];
+    int32_t count;
 };
 
 struct alignas(16) DMat {
@@ -144,6 +155,8 @@ struct SceneView {
     cptr<DTriN> trins;
     cptr<DMat> mats;
     cptr<DLight> lights;
+    cptr<DLeaf> leaves;
+    cptr<int32_t> tri_orig;          // original face index (within its mesh) of each stored face
     int32_t n_objs, n_lights;
     int32_t n_plane, n_sphere, n_box, n_mesh;
     int32_t pow_bits, pad0, pad1, pad2;   // bit length of the largest integer hardness
@@ -311,6 +324,31 @@ RTX_HD bool mesh_bv(const DObj& ob, f3 o, f3 d) {
     return (-b + s) / two_a > 0.0;
 }
 
+// Conservative ray/cluster test. A face whose exact test passes has its computed point
+// o + d*t32 inside the triangle up to fp32 rounding, i.e. within ~2^-22 (|o| + cmax) of
+// the cluster box; the box is padded by 2^-16 (|o|_max + cmax) per ray, far above every
+// rounding term, so a cluster is skipped only if none of its faces can pass.
+struct RayInv {
+    f3 inv;
+    float pad_rel;
+};
+RTX_HD RayInv ray_inv(f3 o, f3 d) {
+    auto safe = [](float v) { return fabsf(v) < 1e-30f ? copysignf(1e-30f, v) : v; };
+    RayInv r;
+    r.inv = f3{1.0f / safe(d.x), 1.0f / safe(d.y), 1.0f / safe(d.z)};
+    r.pad_rel = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
+    return r;
+}
+RTX_HD bool leaf_maybe_hit(const DLeaf& L, f3 o, const RayInv& ri, float cmax) {
+    const float pad = 0x1p-16f * (ri.pad_rel + cmax);
+    const float tx1 = (L.lo[0] - pad - o.x) * ri.inv.x, tx2 = (L.hi[0] + pad - o.x) * ri.inv.x;
+    const float ty1 = (L.lo[1] - pad - o.y) * ri.inv.y, ty2 = (L.hi[1] + pad - o.y) * ri.inv.y;
+    const float tz1 = (L.lo[2] - pad - o.z) * ri.inv.z, tz2 = (L.hi[2] + pad - o.z) * ri.inv.z;
+    const float tn = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+    const float tf = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+    return tf >= tn && tf >= 0.0f;
+}
+
 // Exact fp64 t of a candidate, recomputed from the object exactly as during its test
 // (used only when two fp32 proxies tie; out of line to keep the hot loop's registers low).
 __host__ __device__ __attribute__((noinline)) inline double hit_t64(const SceneView& S, int32_t obj, int32_t sb, f3 o, f3 d, float time) {
@@ -350,7 +388,11 @@ RTX_HD void offer(const SceneView& S, Hit& h, bool valid, float t32, int32_t obj
             take = a < INFINITY;
         } else {
             const double b = hit_t64(S, h.obj, h.sub, o, d, time);
-            take = a < b || (a == b && S.objs[obj].oid < S.objs[h.obj].oid);
+            // equal t: earlier object, then (same mesh) earlier face in OBJ order
+            const DObj oa = S.objs[obj], ob = S.objs[h.obj];
+            const int32_t fa = oa.type == OBJ_MESH ? S.tri_orig[oa.tri_begin + sb] : 0;
+            const int32_t fb = ob.type == OBJ_MESH ? S.tri_orig[ob.tri_begin + h.sub] : 0;
+            take = a < b || (a == b && (oa.oid < ob.oid || (oa.oid == ob.oid && fa < fb)));
         }
     }
     h.t32 = take ? t32 : h.t32;
@@ -401,24 +443,29 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl) {
     if (MESH) {
         for (int k = 0; k < S.n_mesh; ++k, ++oi) {  // mesh.py:72-119, faces in order
             const DObj ob = S.objs[oi];
-            if (!mesh_bv(ob, o, d)) continue;
-            const int32_t f0 = ob.tri_begin, nf = ob.tri_count;
-            for (int f = 0; f < nf; ++f) {
-                const DTri T = S.tris[f0 + f];
-                tally_inc<COUNT>(tl, &Tally::tri);
-                const f3 n = ld3(T.n);
-                const float denom = dot(d, n);
-                const f3 v0 = ld3(T.v0);
-                const float num = dot(sub(v0, o), n);
-                const float t32 = num / denom;
-                // abs(denom) < epsilon -> skip; time < 0 -> skip
-                bool valid = !(fabsf(denom) < kEps4Up) && !quot_neg(t32, num, denom);
-                const f3 p = add(o, scale(d, t32));  // getPoint(time)
-                const float b0 = dot(cross(ld3(T.e01), sub(p, v0)), n);
-                const float b1 = dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n);
-                const float b2 = dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n);
-                valid = valid && b0 >= 0.0f && b1 >= 0.0f && b2 >= 0.0f;
-                offer(S, h, valid, t32, oi, f, o, d, time);
+            if (!mesh_bv(ob, o, d)) continue;  // the reference's bounding volume, quirks included
+            const RayInv ri = ray_inv(o, d);
+            for (int li = 0; li < ob.leaf_count; ++li) {
+                const DLeaf L = S.leaves[ob.leaf_begin + li];
+                const bool maybe = leaf_maybe_hit(L, o, ri, ob.cmax);
+                if (!RTX_ANY(maybe)) continue;
+                for (int f = L.first; f < L.first + L.count; ++f) {
+                    const DTri T = S.tris[ob.tri_begin + f];
+                    tally_inc<COUNT>(tl, &Tally::tri);
+                    const f3 n = ld3(T.n);
+                    const float denom = dot(d, n);
+                    const f3 v0 = ld3(T.v0);
+                    const float num = dot(sub(v0, o), n);
+                    const float t32 = num / denom;
+                    // abs(denom) < epsilon -> skip; time < 0 -> skip
+                    bool valid = maybe && !(fabsf(denom) < kEps4Up) && !quot_neg(t32, num, denom);
+                    const f3 p = add(o, scale(d, t32));  // getPoint(time)
+                    const float b0 = dot(cross(ld3(T.e01), sub(p, v0)), n);
+                    const float b1 = dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n);
+                    const float b2 = dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n);
+                    valid = valid && b0 >= 0.0f && b1 >= 0.0f && b2 >= 0.0f;
+                    offer(S, h, valid, t32, oi, f, o, d, time);
+                }
             }
         }
     }
@@ -474,11 +521,15 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
         for (int k = 0; k < S.n_mesh; ++k, ++oi) {  // mesh.py:121-153 (no t_max test)
             const DObj ob = S.objs[oi];
             if (RTX_ALL(occ)) break;
-            if (occ || !mesh_bv(ob, o, d)) continue;
-            const int32_t f0 = ob.tri_begin, nf = ob.tri_count;
-            for (int f = 0; f < nf; ++f) {
-                if (RTX_ALL(occ)) break;
-                const DTri T = S.tris[f0 + f];
+            const bool live = !occ && mesh_bv(ob, o, d);
+            if (!RTX_ANY(live)) continue;
+            const RayInv ri = ray_inv(o, d);
+            for (int li = 0; li < ob.leaf_count; ++li) {
+              const DLeaf L = S.leaves[ob.leaf_begin + li];
+              const bool maybe = live && !occ && leaf_maybe_hit(L, o, ri, ob.cmax);
+              if (!RTX_ANY(maybe)) continue;
+              for (int f = L.first; f < L.first + L.count; ++f) {
+                const DTri T = S.tris[ob.tri_begin + f];
                 tally_inc<COUNT>(tl, &Tally::tri);
                 const f3 n = ld3(T.nu);
                 const float denom = dot(d, n);
@@ -491,7 +542,8 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
                 hit = hit && dot(cross(ld3(T.e01), sub(p, v0)), n) >= 0.0f &&
                       dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n) >= 0.0f &&
                       dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n) >= 0.0f;
-                occ = occ || hit;
+                occ = occ || (maybe && hit);
+              }
             }
         }
     }

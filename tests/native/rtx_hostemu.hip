@@ -13,6 +13,8 @@ void bind_view(const HostScene& H, SceneView& v) {
     v.trins = (cptr<DTriN>)H.trins.data();
     v.mats = (cptr<DMat>)H.mats.data();
     v.lights = (cptr<DLight>)H.lights.data();
+    v.leaves = (cptr<DLeaf>)H.leaves.data();
+    v.tri_orig = (cptr<int32_t>)H.tri_orig.data();
     v.n_objs = H.n_objs;
     v.n_lights = H.n_lights;
     v.n_plane = H.n_plane; v.n_sphere = H.n_sphere; v.n_box = H.n_box; v.n_mesh = H.n_mesh;
