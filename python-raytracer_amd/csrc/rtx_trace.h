@@ -416,6 +416,7 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl) {
         offer(S, h, valid, t32, oi, 0, o, d, time);
     }
     for (int k = 0; k < S.n_sphere; ++k, ++oi) {  // simple_geometry.py:20-46
+        if (RTX_ABLATE == 7) continue;  // cost probe: no spheres in the primary test
         const DObj ob = S.objs[oi];
         const f3 ctr = moved(ob, ob.a, time);
         bool valid = false;
@@ -718,6 +719,7 @@ RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const 
     bool in_shape = false;
     for (int level = 0; level < (SEC ? kMaxDepth : 1); ++level) {
         if (COUNT) tl.cast[level]++;
+        if (RTX_ABLATE == 8) { tail = d; break; }  // cost probe: camera + store only
         const Hit h = closest_hit<MESH, COUNT>(S, o, d, time, tl);
         if (h.obj < 0) break;  // miss -> black
         const Surface sf = resolve_hit<MESH>(S, h, o, d, time);
@@ -739,7 +741,7 @@ RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const 
             next_d = rdir;
             chain = true;
         }
-        if (RTX_ABLATE == 2 && !chain) { tail = ld3(m.diffuse); break; }
+        if ((RTX_ABLATE == 2 || RTX_ABLATE == 7) && !chain) { tail = ld3(m.diffuse); break; }
         const f3 L = regular_lighting<MESH, COUNT>(S, d, sf.position, n, m, time, tl);
         if (!SEC || !chain) {
             tail = clamp01(L);
