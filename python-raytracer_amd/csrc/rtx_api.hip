@@ -136,6 +136,11 @@ struct Launch {
 #ifndef RTX_TILE
 #define RTX_TILE 1
 #endif
+// Pixels per lane: each wave renders RTX_PPL 8x8 tiles in sequence (amortises the
+// per-wave setup chain: parameters, tables, scene records).
+#ifndef RTX_PPL
+#define RTX_PPL 1
+#endif
 
 // Output pixel (row, column within the block) of this work-item. RTX_TILE=1 maps each
 // 64-lane wave to an 8x8 pixel tile (coherent rays per wave); 0 maps waves to 64
@@ -144,9 +149,10 @@ struct Launch {
 struct PixelRC {
     int32_t r, c;
 };
-__device__ __forceinline__ PixelRC pixel_rc(int32_t ncols) {
+__device__ __forceinline__ PixelRC pixel_rc(int32_t ncols, int sub) {
     const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+    const int wave = __builtin_amdgcn_readfirstlane(
+        (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RTX_PPL + sub));
     if (RTX_TILE == 0) {
         const int64_t p = (int64_t)wave * 64 + lane;
         const int32_t r = (int32_t)(p / ncols);
@@ -158,21 +164,26 @@ __device__ __forceinline__ PixelRC pixel_rc(int32_t ncols) {
 }
 
 __host__ __device__ inline int64_t launch_items(int32_t nrows, int32_t ncols) {
-    if (RTX_TILE == 0) return (int64_t)nrows * ncols;
-    return (int64_t)((ncols + 7) >> 3) * ((nrows + 7) >> 3) * 64;
+    const int64_t waves = RTX_TILE == 0 ? ((int64_t)nrows * ncols + 63) / 64
+                                        : (int64_t)((ncols + 7) >> 3) * ((nrows + 7) >> 3);
+    return (waves + RTX_PPL - 1) / RTX_PPL * 64;
 }
 
 template <bool MESH, bool SEC, bool COUNT, bool JIT>
 __global__ __launch_bounds__(256, RTX_LB_WAVES(MESH, SEC)) void k_render(const KParams* __restrict__ Pp, const Launch L) {
     const int32_t ncols = Pp->ncols;
-    const PixelRC px = pixel_rc(ncols);
-    const bool active = px.r < L.nrows && px.c < ncols;
     Tally tl = {};
     // secondary-ray frames: [frame][word][thread] in LDS (40 KB per 256-thread block)
     __shared__ float frames[SEC ? kMaxDepth * 4 * 256 : 1];
     const FrameStack fs{frames + threadIdx.x, 256};
-    if (active) render_pixel<MESH, SEC, COUNT, JIT>(*Pp, L.fb, L.row0, px.r, px.c, tl, fs);
-    flush_tally<COUNT>(tl, L.counters, active);
+    bool any_active = false;
+    for (int sub = 0; sub < RTX_PPL; ++sub) {
+        const PixelRC px = pixel_rc(ncols, sub);
+        const bool active = px.r < L.nrows && px.c < ncols;
+        any_active = any_active || active;
+        if (active) render_pixel<MESH, SEC, COUNT, JIT>(*Pp, L.fb, L.row0, px.r, px.c, tl, fs);
+    }
+    flush_tally<COUNT>(tl, L.counters, any_active);
 }
 
 template <bool MESH>
