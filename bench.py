@@ -36,7 +36,13 @@ CONFIGS = {
     "tm1080": ("TorusMesh", (1920, 1080), (1, None), "TorusMesh 1920x1080 1spp (128-triangle mesh)"),
     "mr1080": ("MirrorRefraction", (1920, 1080), (1, None), "MirrorRefraction 1920x1080 1spp (reflect/refract chains)"),
     "dof4k": ("DepthOfField", (3840, 2160), (2, 32), "DepthOfField 3840x2160 AA2 x DOF32 = 64spp, jittered"),
+    "ns1": ("NovelScene1", (2048, 1024), None, "NovelScene1 2048x1024 AA32 jittered (CSG hierarchies + textures)"),
+    "ns2": ("NovelScene2", (1024, 512), None,
+            "NovelScene2 1024x512 AA2 x DOF15 x 16 motion times, jittered (CSG hierarchies + textures)"),
 }
+# CPU-baseline sub-sampling for the configs whose full frame takes minutes on one core:
+# the first of N column strips (np.array_split(arange(W), N)[0]) per repeat.
+CPU_STRIPS = {"tm1080": 16, "dof4k": 16, "ns1": 32, "ns2": 128}
 
 
 def parse():
@@ -86,21 +92,20 @@ def cpu_baseline(cfg, budget_s):
     osc = O.OracleScene(d, base)
     W, H = res
     rows = H
-    if cfg in ("tm1080", "dof4k"):
-        rows = max(1, H // 16)  # deterministic sub-sample for the slow configs
     nsamp = 0
     frames = 0
     t0 = time.perf_counter()
     noise = None
     while True:
-        if cfg in ("tm1080", "dof4k"):
-            # a 1/16-height strip of the frame: columns subset via tasks=16, subimage 0
-            ncol = len(np.array_split(np.arange(W), 16)[0])
+        if cfg in CPU_STRIPS:
+            # the first of N column strips (tasks=N, subimage 0)
+            ns = CPU_STRIPS[cfg]
+            ncol = len(np.array_split(np.arange(W), ns)[0])
             if osc.jitter:
                 noise = np.random.RandomState(0).rand(ncol * H * osc.spp_rays * 3)
-            osc.render(0, 16, noise=noise)
+            osc.render(0, ns, noise=noise)
             nsamp += ncol * H * osc.n_samples
-            sample = "columns 0..%d of %dx%d (1/16 of the frame) per repeat" % (ncol - 1, W, H)
+            sample = "columns 0..%d of %dx%d (1/%d of the frame) per repeat" % (ncol - 1, W, H, ns)
         else:
             osc.render()
             nsamp += W * rows * osc.n_samples

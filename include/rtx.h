@@ -7,9 +7,11 @@
  * ctypes binding of that interface binds:
  *
  *   rtx_scene_create   <- scene_parser.load_scene's object construction
- *                         (provided/scene_parser.py:104-163, geometry ctors in
- *                         provided/geometry/simple_geometry.py:15-18,87-103,180-186 and
- *                         provided/geometry/mesh.py:17-70): scene objects -> HBM
+ *                         (provided/scene_parser.py:104-294, geometry ctors in
+ *                         provided/geometry/simple_geometry.py:15-18,87-103,180-186,
+ *                         provided/geometry/mesh.py:17-70 and
+ *                         provided/geometry/hierarchy.py:12-40, textures
+ *                         scene_parser.py:222-247): scene objects -> HBM
  *   rtx_camera_set     <- ViewportCamera + the per-frame setup of Scene.render
  *                         (provided/helperclasses.py:69-108, provided/scene.py:36-45)
  *   rtx_render         <- Scene.render's pixel/sample loops + cast_ray + shading
@@ -43,7 +45,7 @@
 extern "C" {
 #endif
 
-#define RTX_ABI_VERSION 1
+#define RTX_ABI_VERSION 2
 
 typedef enum rtx_status {
     RTX_OK = 0,
@@ -53,14 +55,22 @@ typedef enum rtx_status {
     RTX_ERR_STATE = -4        /* e.g. rtx_render before rtx_camera_set */
 } rtx_status;
 
-typedef enum rtx_object_type { RTX_SPHERE = 0, RTX_PLANE = 1, RTX_BOX = 2, RTX_MESH = 3 } rtx_object_type;
+typedef enum rtx_object_type { RTX_SPHERE = 0, RTX_PLANE = 1, RTX_BOX = 2, RTX_MESH = 3, RTX_NODE = 4 } rtx_object_type;
+typedef enum rtx_hierarchy_type {
+    RTX_UNION = 0, RTX_INTERSECTION = 1, RTX_DIFFERENCE = 2, RTX_HIER_OTHER = 3  /* other: no hits */
+} rtx_hierarchy_type;
 typedef enum rtx_material_type { RTX_MAT_DIFFUSE = 0, RTX_MAT_MIRROR = 1, RTX_MAT_REFRACTIVE = 2 } rtx_material_type;
 typedef enum rtx_light_type { RTX_LIGHT_POINT = 0, RTX_LIGHT_DIRECTIONAL = 1 } rtx_light_type;
 typedef enum rtx_bv_type { RTX_BV_AABB = 0, RTX_BV_SPHERE = 1 } rtx_bv_type;
 typedef enum rtx_jitter_mode { RTX_JITTER_OFF = 0, RTX_JITTER_PHILOX = 1, RTX_JITTER_REPLAY = 2 } rtx_jitter_mode;
 
-/* One geometry object, in scene (JSON) order: the order is the closest-hit tie break
- * (min() keeps the first minimum, provided/scene.py:94). */
+/* One geometry record. Top-level objects (parent == -1) are in scene (JSON) order, which
+ * is the closest-hit tie break (min() keeps the first minimum, provided/scene.py:94).
+ * Hierarchy nodes (RTX_NODE, provided/geometry/hierarchy.py) are followed by their
+ * subtree in preorder: every record after a node whose parent is that node is one of
+ * its children, in child order. Child records carry what the parser gives them:
+ * materials after Hierarchy.set_fallback_material (hierarchy.py:21-28), speeds after
+ * traverse_children's `speed + child speed` (scene_parser.py:268-271). */
 typedef struct rtx_object {
     int32_t type;          /* rtx_object_type */
     int32_t n_mats;        /* associated materials (Plane: 1 = plain, >=2 = checker) */
@@ -77,7 +87,19 @@ typedef struct rtx_object {
     float bv_a[3];         /* mesh BV: AABB min | sphere centre */
     float bv_b[3];         /* mesh BV: AABB max */
     double bv_radius;      /* mesh BV: sphere radius (Python float) */
+    int32_t parent;        /* -1: top-level; else index of the enclosing RTX_NODE record */
+    int32_t hierarchy_type;/* node: rtx_hierarchy_type */
+    float trs[9];          /* node: position, rotation (degrees), scale (Hierarchy.make_matrices) */
+    int32_t texture;       /* plane / box: index into rtx_scene_desc.textures, -1 = none */
+    double texture_scale;  /* plane: texture_scale (scene_parser.py:226, default 1.0) */
 } rtx_object;
+
+/* A texture as Image.getpixel sees it (scene_parser.py:224, simple_geometry.py:168):
+ * rgb[3 * (j * width + i) + c] = getpixel((i, j))[c]. */
+typedef struct rtx_texture {
+    int32_t width, height;
+    const uint8_t* rgb;
+} rtx_texture;
 
 /* One mesh face after Mesh.__init__'s (v + translate) * scale transform (mesh.py:24),
  * with the per-vertex smooth normals of _compute_normals (mesh.py:53-70; ignored
@@ -113,6 +135,8 @@ typedef struct rtx_scene_desc {
     int32_t n_triangles;
     const rtx_triangle* triangles;
     float ambient[3];
+    int32_t n_textures;
+    const rtx_texture* textures;
 } rtx_scene_desc;
 
 /* Per-frame camera state. Tables are the reference's scalar sequences, evaluated on the

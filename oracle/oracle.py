@@ -45,6 +45,11 @@ class _SceneIn(C.Structure):
         ("obj_scalar", _d), ("obj_flat", _i),
         ("mesh_vert_off", _i), ("mesh_nverts", _i), ("mesh_face_off", _i), ("mesh_nfaces", _i),
         ("verts", _d), ("faces", _i),
+        ("obj_parent", _i), ("obj_child_off", _i), ("obj_nchild", _i), ("child_idx", _i),
+        ("node_htype", _i), ("node_trs", _d),
+        ("obj_tex", _i), ("obj_tex_scale", _d),
+        ("n_tex", C.c_int), ("tex_w", _i), ("tex_h", _i), ("tex_off", C.POINTER(C.c_longlong)),
+        ("tex_data", C.POINTER(C.c_ubyte)),
     ]
 
 
@@ -93,6 +98,111 @@ def _read_obj(path):
 
 def _vec(v):
     return [float(v[0]), float(v[1]), float(v[2])]
+
+_TYPES = {"sphere": 0, "plane": 1, "box": 2, "mesh": 3, "node": 4}
+_HTYPES = {"union": 0, "intersection": 1, "difference": 2}
+
+
+def _f32vec(v):
+    return [float(x) for x in np.asarray(v, np.float64).astype(np.float32)]
+
+
+def _load_texture(path):
+    """Image.open(texture) + getpixel((i, j))[0:3] (simple_geometry.py:168-169): RGB8 [h, w, 3]."""
+    from PIL import Image
+    im = Image.open(path)
+    if im.mode not in ("RGB", "RGBA", "RGBX", "CMYK", "RGBa", "YCbCr", "LAB", "HSV"):
+        raise TypeError("texture %s: getpixel of mode %s is not indexable as RGB" % (path, im.mode))
+    return np.ascontiguousarray(np.asarray(im)[:, :, :3], dtype=np.uint8)
+
+
+def _parse_objects(data, ids, base_dir):
+    """scene_parser.py:144-161 + parse_geometry/add_basic_shape/traverse_children
+    (:166-285) + Hierarchy.set_fallback_material (hierarchy.py:21-28), restated on plain
+    dicts. Returns geometry records in preorder (top-level objects have parent -1)."""
+    import copy
+
+    def mats_of(g):
+        return [k for i in g.get("materials", []) for k, mid in enumerate(ids) if mid == i]
+
+    def basic(g, speed):
+        t = g["type"]
+        g["name"]  # noqa: B018
+        if t not in ("sphere", "plane", "box", "mesh"):
+            return None
+        if t == "sphere":
+            g["radius"]  # noqa: B018
+        return {"kind": t, "json": g, "pos": _f32vec(g.get("position", [0, 0, 0])), "mats": mats_of(g),
+                "speed": speed, "children": []}
+
+    def node(g, speed, children_speed):
+        return {"kind": "node", "json": {}, "mats": mats_of(g), "speed": speed,
+                "htype": g.get("hierarchy_type", "union"),
+                "trs": _f32vec(g.get("position", [0, 0, 0])) + _f32vec(g.get("rotation", [0, 0, 0]))
+                + _f32vec(g.get("scale", [1, 1, 1])),
+                "children": traverse(g["children"], children_speed)}
+
+    def traverse(children, speed):
+        out = []
+        for g in children:
+            g["name"]  # noqa: B018
+            gt = g["type"]
+            g.get("position", [0, 0, 0])
+            cs = None if speed is None else _f32vec(np.float32(speed) + np.float32(g.get("speed", [0, 0, 0])))
+            leaf = basic(g, cs)
+            if leaf is not None:
+                out.append(leaf)
+            elif gt == "node":
+                out.append(node(g, cs, speed))   # grandchildren get the ROOT's speed again (:283)
+        return out
+
+    objects, root_names, roots = [], [], []
+    for g in data["objects"]:
+        sp = g.get("speed")
+        sp = None if sp is None else _f32vec(sp)
+        leaf = basic(g, sp)
+        if leaf is not None:
+            objects.append(leaf)
+        elif g["type"] == "node":
+            ref = g.get("ref", "")
+            if ref == "":
+                root_names.append(g["name"])
+                n = node(g, sp, sp)
+                roots.append(n)
+                objects.append(n)
+            elif ref in root_names:
+                n = copy.deepcopy(roots[root_names.index(ref)])
+                n["mats"] = mats_of(g)
+                n["trs"] = (_f32vec(g.get("position", [0, 0, 0])) + _f32vec(g.get("rotation", [0, 0, 0]))
+                            + _f32vec(g.get("scale", [1, 1, 1])))
+                objects.append(n)
+    # set_fallback_material(obj.materials) for every top-level hierarchy, after parsing
+    def fallback(n, mats):
+        if not mats:
+            return
+        for c in n["children"]:
+            if c["kind"] == "node":
+                fallback(c, mats)
+            else:
+                c["mats"] = c["mats"] + mats
+    for o in objects:
+        if o["kind"] == "node":
+            fallback(o, list(o["mats"]))
+    records = []
+
+    def flatten(o, parent):
+        idx = len(records)
+        rec = dict(o)
+        rec["parent"] = parent
+        records.append(rec)
+        rec["child_ids"] = [flatten(c, idx) for c in o["children"]]
+        return idx
+    for o in objects:
+        flatten(o, -1)
+    for r in records:
+        if r["kind"] != "node" and not r["mats"]:
+            raise IndexError("object has no material (the reference raises IndexError when it is hit)")
+    return records
 
 
 class OracleScene:
@@ -155,39 +265,29 @@ class OracleScene:
         s.mat_diffuse, s.mat_specular, s.mat_hardness = self._ad(md), self._ad(msp), self._ad(mh)
         s.mat_type, s.mat_tint, s.mat_refr = self._ai(mty), self._ad(mti), self._ad(mr)
 
+        records = _parse_objects(data, ids, base_dir)
         ot, on, om, ohs, osp, oa, ob, oc, obm, osc, ofl = ([] for _ in range(11))
         mvo, mnv, mfo, mnf = [], [], [], []
+        opar, coff, nch, cidx, hty, trs, otex, otsc = [], [], [], [], [], [], [], []
         allv, allf = [np.zeros((0, 3))], [np.zeros((0, 3), np.int32)]
+        textures, tex_index = [], {}
         nv_total = nf_total = 0
-        for g in data["objects"]:
-            gt = g["type"]
-            g["name"]  # noqa: B018
-            if gt not in ("sphere", "plane", "box", "mesh"):
-                if gt == "node":
-                    raise NotImplementedError("oracle: hierarchy nodes are not restated yet")
-                continue
-            mats = [k for i in g.get("materials", []) for k, mid in enumerate(ids) if mid == i]
-            if not mats:
-                raise IndexError("object %r has no material (reference raises IndexError)" % g["name"])
-            pos = _vec(g.get("position", [0, 0, 0]))
-            sp = g.get("speed")
-            a, b, c, bm, sc, fl_, vo, nv, fo, nf = pos, [0.0] * 3, [0.0] * 3, 0, 0.0, 0, 0, 0, 0, 0
-            if gt == "sphere":
-                code, sc = 0, float(g["radius"])
-            elif gt == "plane":
-                code, b = 1, _vec(g["normal"])
-                if "texture" in g:
-                    raise NotImplementedError("oracle: textures are not restated yet")
-            elif gt == "box":
-                code = 2
-                if "texture" in g:
-                    raise NotImplementedError("oracle: textures are not restated yet")
+        for r in records:
+            mats = r["mats"]
+            code = _TYPES[r["kind"]]
+            a, b, c, bm, sc, fl_, vo, nv, fo, nf = r.get("pos", [0.0] * 3), [0.0] * 3, [0.0] * 3, 0, 0.0, 0, 0, 0, 0, 0
+            tex, tsc = -1, 1.0
+            g = r.get("json", {})
+            if r["kind"] == "sphere":
+                sc = float(g["radius"])
+            elif r["kind"] == "plane":
+                b = _vec(g["normal"])
+            elif r["kind"] == "box":
                 if "size" in g:
                     b = _vec(g["size"])
                 else:
                     bm, c, b = 1, _vec(g["min"]), _vec(g["max"])
-            else:
-                code = 3
+            elif r["kind"] == "mesh":
                 path = g["filepath"]
                 if base_dir is not None and not os.path.exists(path):
                     path = os.path.join(base_dir, path)
@@ -196,10 +296,24 @@ class OracleScene:
                 vo, nv, fo, nf = nv_total, len(V), nf_total, len(F)
                 allv.append(V); allf.append(F)
                 nv_total += nv; nf_total += nf
+            if r["kind"] in ("plane", "box") and "texture" in g:
+                path = g["texture"]
+                if base_dir is not None and not os.path.exists(path):
+                    path = os.path.join(base_dir, path)
+                if path not in tex_index:
+                    tex_index[path] = len(textures)
+                    textures.append(_load_texture(path))
+                tex = tex_index[path]
+                if r["kind"] == "plane":
+                    tsc = float(g.get("texture_scale", 1.0))
+            sp = r.get("speed")
             ot.append(code); on.append(len(mats)); om += (mats + [0, 0, 0, 0])[:4]
-            ohs.append(0 if sp is None else 1); osp += [0.0] * 3 if sp is None else _vec(sp)
+            ohs.append(0 if sp is None else 1); osp += [0.0] * 3 if sp is None else [float(x) for x in sp]
             oa += a; ob += b; oc += c; obm.append(bm); osc.append(sc); ofl.append(fl_)
             mvo.append(vo); mnv.append(nv); mfo.append(fo); mnf.append(nf)
+            opar.append(r["parent"]); coff.append(len(cidx)); nch.append(len(r["child_ids"])); cidx += r["child_ids"]
+            hty.append(_HTYPES.get(r.get("htype"), 3)); trs += r.get("trs", [0.0] * 9)
+            otex.append(tex); otsc.append(tsc)
         s.n_objs = len(ot)
         s.obj_type, s.obj_nmat, s.obj_mat, s.obj_has_speed = self._ai(ot), self._ai(on), self._ai(om), self._ai(ohs)
         s.obj_speed, s.obj_a, s.obj_b, s.obj_c = self._ad(osp), self._ad(oa), self._ad(ob), self._ad(oc)
@@ -208,6 +322,20 @@ class OracleScene:
         s.mesh_face_off, s.mesh_nfaces = self._ai(mfo), self._ai(mnf)
         s.verts = self._ad(np.concatenate(allv).ravel())
         s.faces = self._ai(np.concatenate(allf).ravel())
+        s.obj_parent, s.obj_child_off, s.obj_nchild, s.child_idx = self._ai(opar), self._ai(coff), self._ai(nch), self._ai(cidx)
+        s.node_htype, s.node_trs = self._ai(hty), self._ad(trs)
+        s.obj_tex, s.obj_tex_scale = self._ai(otex), self._ad(otsc)
+        s.n_tex = len(textures)
+        s.tex_w = self._ai([t.shape[1] for t in textures])
+        s.tex_h = self._ai([t.shape[0] for t in textures])
+        offs = np.cumsum([0] + [t.size for t in textures])[:-1]
+        a = np.ascontiguousarray(np.asarray(offs, np.int64))
+        self._keep.append(a)
+        s.tex_off = a.ctypes.data_as(C.POINTER(C.c_longlong))
+        td = np.ascontiguousarray(np.concatenate([t.ravel() for t in textures]) if textures else np.zeros(1, np.uint8))
+        self._keep.append(td)
+        s.tex_data = td.ctypes.data_as(C.POINTER(C.c_ubyte))
+        self.records = records
         self.s = s
         self.width, self.height = s.width, s.height
         self.n_samples = s.samples * s.dof_samples * (s.motion_samples + s.motion_final)
@@ -246,6 +374,8 @@ class OracleScene:
         tl = (C.c_longlong * 13)()
         rc = lib().oracle_render(C.byref(self.s), subimage, tasks, out.ctypes.data_as(_d),
                                  None if nz is None else nz.ctypes.data_as(_d), tl)
+        if rc == -3:
+            raise IndexError("oracle_render: the reference raises here (texture index / missing material)")
         if rc != 0:
             raise RuntimeError("oracle_render failed: %d" % rc)
         if tallies:

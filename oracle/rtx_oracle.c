@@ -69,6 +69,152 @@ static inline vec3 vrefract(vec3 I, vec3 N, float eta) {
 /* Python min(a, b) / max(a, b): the first argument unless the second compares strictly */
 static inline double pymin(double a, double b) { return (b < a) ? b : a; }
 static inline double pymax(double a, double b) { return (b > a) ? b : a; }
+/* CPython float_rem: x % m with the sign of m */
+static inline double pymod(double x, double m) {
+    double mod = fmod(x, m);
+    if (mod != 0.0) {
+        if ((m < 0) != (mod < 0)) mod += m;
+    } else {
+        mod = copysign(0.0, m);
+    }
+    return mod;
+}
+
+/* ----------------------------------------------------------------- GLM mat4 (float)
+ * Restated from GLM 0.9.9's generic (non-SIMD) code, which PyGLM wraps: m[column][row],
+ * every vec4 operation componentwise in fp32, left to right. */
+typedef struct { float m[4][4]; } mat4_t;
+
+static mat4_t mat_identity(void) {
+    mat4_t r;
+    memset(&r, 0, sizeof(r));
+    for (int k = 0; k < 4; k++) r.m[k][k] = 1.0f;
+    return r;
+}
+/* glm::translate: Result[3] = m[0] * v[0] + m[1] * v[1] + m[2] * v[2] + m[3] */
+static mat4_t mat_translate(mat4_t m, vec3 v) {
+    mat4_t r = m;
+    for (int k = 0; k < 4; k++) r.m[3][k] = ((m.m[0][k] * v.x + m.m[1][k] * v.y) + m.m[2][k] * v.z) + m.m[3][k];
+    return r;
+}
+/* glm::rotate(m, angle, v) */
+static mat4_t mat_rotate(mat4_t m, float angle, vec3 v) {
+    const float c = cosf(angle), s = sinf(angle);
+    vec3 axis = vnormalize(v);
+    vec3 temp = vscale(axis, 1.0f - c);
+    float R[3][3];
+    R[0][0] = c + temp.x * axis.x;
+    R[0][1] = temp.x * axis.y + s * axis.z;
+    R[0][2] = temp.x * axis.z - s * axis.y;
+    R[1][0] = temp.y * axis.x - s * axis.z;
+    R[1][1] = c + temp.y * axis.y;
+    R[1][2] = temp.y * axis.z + s * axis.x;
+    R[2][0] = temp.z * axis.x + s * axis.y;
+    R[2][1] = temp.z * axis.y - s * axis.x;
+    R[2][2] = c + temp.z * axis.z;
+    mat4_t r;
+    for (int col = 0; col < 3; col++)
+        for (int k = 0; k < 4; k++)
+            r.m[col][k] = (m.m[0][k] * R[col][0] + m.m[1][k] * R[col][1]) + m.m[2][k] * R[col][2];
+    for (int k = 0; k < 4; k++) r.m[3][k] = m.m[3][k];
+    return r;
+}
+/* glm::scale: Result[i] = m[i] * v[i] (i < 3), Result[3] = m[3] */
+static mat4_t mat_scale(mat4_t m, vec3 v) {
+    mat4_t r = m;
+    const float s[3] = {v.x, v.y, v.z};
+    for (int col = 0; col < 3; col++)
+        for (int k = 0; k < 4; k++) r.m[col][k] = m.m[col][k] * s[col];
+    return r;
+}
+/* glm::inverse (compute_inverse<4, 4>, cofactors) */
+static mat4_t mat_inverse(mat4_t M) {
+    float (*m)[4] = M.m;
+    float Coef00 = m[2][2] * m[3][3] - m[3][2] * m[2][3];
+    float Coef02 = m[1][2] * m[3][3] - m[3][2] * m[1][3];
+    float Coef03 = m[1][2] * m[2][3] - m[2][2] * m[1][3];
+    float Coef04 = m[2][1] * m[3][3] - m[3][1] * m[2][3];
+    float Coef06 = m[1][1] * m[3][3] - m[3][1] * m[1][3];
+    float Coef07 = m[1][1] * m[2][3] - m[2][1] * m[1][3];
+    float Coef08 = m[2][1] * m[3][2] - m[3][1] * m[2][2];
+    float Coef10 = m[1][1] * m[3][2] - m[3][1] * m[1][2];
+    float Coef11 = m[1][1] * m[2][2] - m[2][1] * m[1][2];
+    float Coef12 = m[2][0] * m[3][3] - m[3][0] * m[2][3];
+    float Coef14 = m[1][0] * m[3][3] - m[3][0] * m[1][3];
+    float Coef15 = m[1][0] * m[2][3] - m[2][0] * m[1][3];
+    float Coef16 = m[2][0] * m[3][2] - m[3][0] * m[2][2];
+    float Coef18 = m[1][0] * m[3][2] - m[3][0] * m[1][2];
+    float Coef19 = m[1][0] * m[2][2] - m[2][0] * m[1][2];
+    float Coef20 = m[2][0] * m[3][1] - m[3][0] * m[2][1];
+    float Coef22 = m[1][0] * m[3][1] - m[3][0] * m[1][1];
+    float Coef23 = m[1][0] * m[2][1] - m[2][0] * m[1][1];
+    const float Fac0[4] = {Coef00, Coef00, Coef02, Coef03};
+    const float Fac1[4] = {Coef04, Coef04, Coef06, Coef07};
+    const float Fac2[4] = {Coef08, Coef08, Coef10, Coef11};
+    const float Fac3[4] = {Coef12, Coef12, Coef14, Coef15};
+    const float Fac4[4] = {Coef16, Coef16, Coef18, Coef19};
+    const float Fac5[4] = {Coef20, Coef20, Coef22, Coef23};
+    const float Vec0[4] = {m[1][0], m[0][0], m[0][0], m[0][0]};
+    const float Vec1[4] = {m[1][1], m[0][1], m[0][1], m[0][1]};
+    const float Vec2[4] = {m[1][2], m[0][2], m[0][2], m[0][2]};
+    const float Vec3[4] = {m[1][3], m[0][3], m[0][3], m[0][3]};
+    const float SignA[4] = {+1, -1, +1, -1}, SignB[4] = {-1, +1, -1, +1};
+    mat4_t inv;
+    for (int k = 0; k < 4; k++) {
+        inv.m[0][k] = ((Vec1[k] * Fac0[k] - Vec2[k] * Fac1[k]) + Vec3[k] * Fac2[k]) * SignA[k];
+        inv.m[1][k] = ((Vec0[k] * Fac0[k] - Vec2[k] * Fac3[k]) + Vec3[k] * Fac4[k]) * SignB[k];
+        inv.m[2][k] = ((Vec0[k] * Fac1[k] - Vec1[k] * Fac3[k]) + Vec3[k] * Fac5[k]) * SignA[k];
+        inv.m[3][k] = ((Vec0[k] * Fac2[k] - Vec1[k] * Fac4[k]) + Vec2[k] * Fac5[k]) * SignB[k];
+    }
+    const float Row0[4] = {inv.m[0][0], inv.m[1][0], inv.m[2][0], inv.m[3][0]};
+    float Dot0[4];
+    for (int k = 0; k < 4; k++) Dot0[k] = m[0][k] * Row0[k];
+    const float Dot1 = (Dot0[0] + Dot0[1]) + (Dot0[2] + Dot0[3]);
+    const float OneOverDeterminant = 1.0f / Dot1;
+    for (int c = 0; c < 4; c++)
+        for (int k = 0; k < 4; k++) inv.m[c][k] = inv.m[c][k] * OneOverDeterminant;
+    return inv;
+}
+static mat4_t mat_transpose(mat4_t m) {
+    mat4_t r;
+    for (int c = 0; c < 4; c++)
+        for (int k = 0; k < 4; k++) r.m[c][k] = m.m[k][c];
+    return r;
+}
+/* mat4 * vec4: (m[0] * v.x + m[1] * v.y) + (m[2] * v.z + m[3] * v.w) */
+static void mat_vec4(const mat4_t* M, const float v[4], float out[4]) {
+    for (int k = 0; k < 4; k++)
+        out[k] = (M->m[0][k] * v[0] + M->m[1][k] * v[1]) + (M->m[2][k] * v[2] + M->m[3][k] * v[3]);
+}
+/* glm.vec3(M * glm.vec4(p, w)) */
+static vec3 mat_xform(const mat4_t* M, vec3 p, float w) {
+    const float v[4] = {p.x, p.y, p.z, w};
+    float o[4];
+    mat_vec4(M, v, o);
+    return V3(o[0], o[1], o[2]);
+}
+/* glm.normalize(glm.transpose(Minv) * glm.vec4(n, 0)).xyz (hierarchy.py:76): the vec4
+ * dot is (x*x + y*y) + (z*z + w*w), and w is kept in the length */
+static vec3 normal_xform(const mat4_t* MinvT, vec3 n) {
+    const float v[4] = {n.x, n.y, n.z, 0.0f};
+    float o[4];
+    mat_vec4(MinvT, v, o);
+    const float d = (o[0] * o[0] + o[1] * o[1]) + (o[2] * o[2] + o[3] * o[3]);
+    const float inv = 1.0f / sqrtf(d);
+    return V3(o[0] * inv, o[1] * inv, o[2] * inv);
+}
+/* Hierarchy.make_matrices (hierarchy.py:30-40); glm.radians of a Python float is fp64 */
+static void make_matrices(vec3 t, vec3 r, vec3 s, mat4_t* M, mat4_t* Minv) {
+    const double k = 0.017453292519943295;
+    mat4_t m = mat_identity();
+    m = mat_translate(m, t);
+    m = mat_rotate(m, (float)((double)r.x * k), V3(1, 0, 0));
+    m = mat_rotate(m, (float)((double)r.y * k), V3(0, 1, 0));
+    m = mat_rotate(m, (float)((double)r.z * k), V3(0, 0, 1));
+    m = mat_scale(m, s);
+    *M = m;
+    *Minv = mat_inverse(m);
+}
 
 /* ----------------------------------------------------------------- input description */
 /* Filled by oracle/oracle.py from a scene JSON dictionary (JSON numbers as doubles). */
@@ -111,10 +257,27 @@ typedef struct {
     const int* mesh_nfaces;
     const double* verts;       /* [3 * total verts] raw OBJ values */
     const int* faces;          /* [3 * total faces] 0-based */
+    /* hierarchy (scene_parser.py:166-209, :261-285): every geometry record, top-level or
+     * child, in one array; obj_parent = -1 marks the scene's top-level objects (in order) */
+    const int* obj_parent;
+    const int* obj_child_off;  /* children of a node: child_idx[off .. off + nchild) */
+    const int* obj_nchild;
+    const int* child_idx;
+    const int* node_htype;     /* 0 union, 1 intersection, 2 difference, 3 other */
+    const double* node_trs;    /* [9n] position, rotation (degrees), scale */
+    /* textures (scene_parser.py:222-247): RGB8 texels, getpixel((i, j)) = data[3 (j w + i)] */
+    const int* obj_tex;        /* texture index or -1 */
+    const double* obj_tex_scale;
+    int n_tex;
+    const int* tex_w;
+    const int* tex_h;
+    const long long* tex_off;  /* byte offset into tex_data */
+    const unsigned char* tex_data;
 } oracle_scene_in;
 
 /* ----------------------------------------------------------------- scene objects */
-enum { T_SPHERE = 0, T_PLANE = 1, T_BOX = 2, T_MESH = 3 };
+enum { T_SPHERE = 0, T_PLANE = 1, T_BOX = 2, T_MESH = 3, T_NODE = 4 };
+enum { H_UNION = 0, H_INTER = 1, H_DIFF = 2, H_OTHER = 3 };
 enum { M_DIFFUSE = 0, M_MIRROR = 1, M_REFRACTIVE = 2 };
 enum { L_POINT = 0, L_DIRECTIONAL = 1 };
 
@@ -149,6 +312,13 @@ typedef struct {
     int bv_is_aabb;
     vec3 bv_min, bv_max, bv_center;
     double bv_radius;
+    /* Hierarchy (hierarchy.py:11-40) */
+    int htype, nchild;
+    const int* children;
+    mat4_t M, Minv, MinvT;
+    /* texture (scene_parser.py:222-247) */
+    int tex;
+    double tex_scale;
 } object_t;
 
 typedef struct {
@@ -163,7 +333,10 @@ typedef struct {
     vec3 ambient;
     int n_lights; light_t* lights;
     int n_mats; material_t* mats;
-    int n_objs; object_t* objs;
+    int n_objs; object_t* objs;     /* every geometry record (children included) */
+    int n_roots; int* roots;        /* Scene.objects: the top-level records, in order */
+    int n_tex; const int* tex_w; const int* tex_h; const long long* tex_off; const unsigned char* tex_data;
+    int error;                      /* an exception the reference would raise (IndexError) */
     double current_time;
     /* tallies (Appendix C of SURVEY.md) */
     long long cast_depth[11];
@@ -485,12 +658,16 @@ static int mesh_shadow(const scene_t* sc, int oi, const ray_t* ray, double t_max
 }
 
 /* ----------------------------------------------------------------- dispatch */
+static void node_intersect(const scene_t* sc, int oi, const ray_t* ray, hitlist_t* out);
+static int node_shadow(const scene_t* sc, int oi, const ray_t* ray, double t_max);
+
 static void obj_intersect(const scene_t* sc, int oi, const ray_t* ray, hitlist_t* out) {
     switch (sc->objs[oi].type) {
         case T_SPHERE: sphere_intersect(sc, oi, ray, out); break;
         case T_PLANE: plane_intersect(sc, oi, ray, out); break;
         case T_BOX: box_intersect(sc, oi, ray, out); break;
         case T_MESH: mesh_intersect(sc, oi, ray, out); break;
+        case T_NODE: node_intersect(sc, oi, ray, out); break;
     }
 }
 
@@ -500,8 +677,198 @@ static int obj_shadow(const scene_t* sc, int oi, const ray_t* ray, double t_max)
         case T_PLANE: return plane_shadow(sc, oi, ray, t_max);
         case T_BOX: return box_shadow(sc, oi, ray, t_max);
         case T_MESH: return mesh_shadow(sc, oi, ray, t_max);
+        case T_NODE: return node_shadow(sc, oi, ray, t_max);
     }
     return 0;
+}
+
+/* Geometry.is_inside: Sphere (simple_geometry.py:74-80), AABB (:296-307), Hierarchy
+ * (hierarchy.py:111-129); Plane and Mesh keep Geometry's False (geometry/__init__.py:53-54) */
+static int obj_is_inside(const scene_t* sc, int oi, vec3 point) {
+    const object_t* o = &sc->objs[oi];
+    switch (o->type) {
+        case T_SPHERE: {
+            vec3 center = moved(sc, o, o->center);
+            return (double)vlength(vsub(point, center)) < o->radius;
+        }
+        case T_BOX: {
+            vec3 mn = moved(sc, o, o->minpos), mx = moved(sc, o, o->maxpos);
+            return (mn.x < point.x && point.x < mx.x) && (mn.y < point.y && point.y < mx.y) &&
+                   (mn.z < point.z && point.z < mx.z);
+        }
+        case T_NODE: {
+            vec3 q = mat_xform(&o->Minv, point, 1.0f);
+            if (o->htype == H_UNION) {
+                for (int c = 0; c < o->nchild; c++)
+                    if (obj_is_inside(sc, o->children[c], q)) return 1;
+                return 0;
+            }
+            if (o->htype == H_INTER) {
+                for (int c = 0; c < o->nchild; c++)
+                    if (!obj_is_inside(sc, o->children[c], q)) return 0;
+                return 1;
+            }
+            if (o->htype == H_DIFF) {
+                if (o->nchild < 2) { ((scene_t*)sc)->error = 1; return 0; }
+                int c1 = obj_is_inside(sc, o->children[0], q);
+                int c2 = obj_is_inside(sc, o->children[1], q);
+                return c1 && !c2;
+            }
+            return 0;
+        }
+    }
+    return 0;
+}
+
+/* Geometry.get_material (geometry/__init__.py:56-57), Plane (simple_geometry.py:133-148),
+ * Hierarchy (hierarchy.py:131-138); -1 = None */
+static int obj_get_material(const scene_t* sc, int oi, vec3 point) {
+    const object_t* o = &sc->objs[oi];
+    if (o->type == T_PLANE) return plane_material(sc, o, point);
+    if (o->type != T_NODE) {
+        if (o->nmat < 1) { ((scene_t*)sc)->error = 1; return 0; }
+        return o->mat[0];
+    }
+    vec3 q = mat_xform(&o->Minv, point, 1.0f);
+    for (int c = 0; c < o->nchild; c++)
+        if (obj_is_inside(sc, o->children[c], q)) return obj_get_material(sc, o->children[c], q);
+    return -1;
+}
+
+static void hl_free(hitlist_t* h) { free(h->v); h->v = NULL; h->n = h->cap = 0; }
+
+/* Hierarchy.intersect (hierarchy.py:42-78) */
+static void node_intersect(const scene_t* sc, int oi, const ray_t* ray, hitlist_t* out) {
+    const object_t* o = &sc->objs[oi];
+    ray_t m_ray;
+    m_ray.origin = mat_xform(&o->Minv, ray->origin, 1.0f);
+    m_ray.direction = mat_xform(&o->Minv, ray->direction, 0.0f);
+    hitlist_t hl = {0, 0, 0};
+    if (o->htype == H_UNION) {
+        for (int c = 0; c < o->nchild; c++) obj_intersect(sc, o->children[c], &m_ray, &hl);
+    } else if (o->htype == H_INTER) {
+        for (int c = 0; c < o->nchild; c++) {
+            hitlist_t ch = {0, 0, 0};
+            obj_intersect(sc, o->children[c], &m_ray, &ch);
+            for (int k = 0; k < ch.n; k++) {
+                int keep = 1;
+                for (int c2 = 0; c2 < o->nchild; c2++)
+                    if (c2 != c && !obj_is_inside(sc, o->children[c2], ch.v[k].position)) keep = 0;
+                if (keep) hl_push(&hl, ch.v[k]);
+            }
+            hl_free(&ch);
+        }
+    } else if (o->htype == H_DIFF) {
+        if (o->nchild < 2) { ((scene_t*)sc)->error = 1; return; }
+        hitlist_t c1 = {0, 0, 0}, c2 = {0, 0, 0};
+        obj_intersect(sc, o->children[0], &m_ray, &c1);
+        obj_intersect(sc, o->children[1], &m_ray, &c2);
+        for (int k = 0; k < c1.n; k++)
+            if (!obj_is_inside(sc, o->children[1], c1.v[k].position)) hl_push(&hl, c1.v[k]);
+        for (int k = 0; k < c2.n; k++) {
+            isect_t it = c2.v[k];
+            if (obj_is_inside(sc, o->children[0], it.position)) {
+                it.mat = obj_get_material(sc, o->children[0], it.position);
+                it.normal = vneg(it.normal);
+                hl_push(&hl, it);
+            }
+        }
+        hl_free(&c1);
+        hl_free(&c2);
+    }
+    for (int k = 0; k < hl.n; k++) {
+        isect_t it = hl.v[k];
+        if (it.mat < 0) {
+            if (o->nmat < 1) { ((scene_t*)sc)->error = 1; it.mat = 0; }
+            else it.mat = o->mat[0];
+        }
+        it.position = mat_xform(&o->M, it.position, 1.0f);
+        it.normal = normal_xform(&o->MinvT, it.normal);
+        hl_push(out, it);
+    }
+    hl_free(&hl);
+}
+
+/* Hierarchy.shadow_intersect (hierarchy.py:80-109) */
+static int node_shadow(const scene_t* sc, int oi, const ray_t* ray, double t_max) {
+    const object_t* o = &sc->objs[oi];
+    ray_t m_ray;
+    m_ray.origin = mat_xform(&o->Minv, ray->origin, 1.0f);
+    m_ray.direction = mat_xform(&o->Minv, ray->direction, 0.0f);
+    if (o->htype == H_UNION) {
+        for (int c = 0; c < o->nchild; c++)
+            if (obj_shadow(sc, o->children[c], &m_ray, t_max)) return 1;
+        return 0;
+    }
+    if (o->htype == H_INTER) {
+        for (int c = 0; c < o->nchild; c++)
+            if (!obj_shadow(sc, o->children[c], &m_ray, t_max)) return 0;
+        return 1;
+    }
+    if (o->htype == H_DIFF) {
+        if (o->nchild < 2) { ((scene_t*)sc)->error = 1; return 0; }
+        hitlist_t c1 = {0, 0, 0}, c2 = {0, 0, 0};
+        obj_intersect(sc, o->children[0], &m_ray, &c1);
+        obj_intersect(sc, o->children[1], &m_ray, &c2);
+        int hit = 0;
+        for (int k = 0; k < c1.n && !hit; k++)
+            if (c1.v[k].time > SHADOW_EPS && !obj_is_inside(sc, o->children[1], c1.v[k].position)) hit = 1;
+        for (int k = 0; k < c2.n && !hit; k++)
+            if (c2.v[k].time > SHADOW_EPS && obj_is_inside(sc, o->children[0], c2.v[k].position)) hit = 1;
+        hl_free(&c1);
+        hl_free(&c2);
+        return hit;
+    }
+    return 0;
+}
+
+/* ----------------------------------------------------------------- textures */
+/* texture.getpixel((i, j)) -> vec3(p[0] / 255, p[1] / 255, p[2] / 255); i, j truncated */
+static vec3 texel(scene_t* sc, int tex, double fi, double fj) {
+    const int w = sc->tex_w[tex], h = sc->tex_h[tex];
+    if (!(fi > -1.0 && fj > -1.0 && fi < (double)w && fj < (double)h)) {  /* IndexError / ValueError */
+        sc->error = 1;
+        return V3(0, 0, 0);
+    }
+    const int i = (int)fi, j = (int)fj;
+    const unsigned char* p = sc->tex_data + sc->tex_off[tex] + 3 * ((size_t)j * (size_t)w + (size_t)i);
+    return V3((float)(p[0] / 255.0), (float)(p[1] / 255.0), (float)(p[2] / 255.0));
+}
+
+/* Plane.get_diffuse (simple_geometry.py:150-173) */
+static vec3 plane_diffuse(scene_t* sc, const object_t* o, vec3 point) {
+    if (o->tex < 0) return sc->mats[plane_material(sc, o, point)].diffuse;
+    vec3 position = moved(sc, o, o->point);
+    const double scale = o->tex_scale;
+    point = vsub(point, vscale(o->normal, vdot(vsub(point, o->point), o->normal)));
+    const double u = (double)vdot(vsub(point, position), o->width_axis) * 1000.0 / scale;
+    const double v = (double)vdot(vsub(point, position), o->height_axis) * 1000.0 / scale;
+    const double i = trunc(pymod(u, (double)sc->tex_w[o->tex]));
+    const double j = trunc(pymod(v, (double)sc->tex_h[o->tex]));
+    return texel(sc, o->tex, i, j);
+}
+
+/* AABB.get_diffuse (simple_geometry.py:312-355) */
+static vec3 box_diffuse(scene_t* sc, const object_t* o, vec3 point) {
+    if (o->tex < 0) return sc->mats[o->mat[0]].diffuse;
+    vec3 mn = moved(sc, o, o->minpos), mx = moved(sc, o, o->maxpos);
+    const double px = point.x, py = point.y, pz = point.z;
+    const double x = (px - mn.x) / ((double)mx.x - mn.x);
+    const double y = (py - mn.y) / ((double)mx.y - mn.y);
+    const double z = (pz - mn.z) / ((double)mx.z - mn.z);
+    const double W = sc->tex_w[o->tex], H = sc->tex_h[o->tex];
+    double i, j;
+    if (fabs(px - mn.x) < EPSILON) { i = z * W; j = (1 - y) * H; }
+    else if (fabs(px - mx.x) < EPSILON) { i = (1 - z) * W; j = (1 - y) * H; }
+    else if (fabs(py - mn.y) < EPSILON) { i = x * W; j = (1 - z) * H; }
+    else if (fabs(py - mx.y) < EPSILON) { i = x * W; j = z * H; }
+    else if (fabs(pz - mn.z) < EPSILON) { i = (1 - x) * W; j = (1 - y) * H; }
+    else if (fabs(pz - mx.z) < EPSILON) { i = x * W; j = (1 - y) * H; }
+    else { i = 0; j = 0; }
+    /* min(max(0, i), width - 1): Python keeps the first argument on ties and NaN */
+    i = pymin(pymax(0.0, i), W - 1);
+    j = pymin(pymax(0.0, j), H - 1);
+    return texel(sc, o->tex, i, j);
 }
 
 /* ----------------------------------------------------------------- shading */
@@ -509,9 +876,11 @@ static int obj_shadow(const scene_t* sc, int oi, const ray_t* ray, double t_max)
 static vec3 regular_lighting(scene_t* sc, const ray_t* ray, const isect_t* it) {
     vec3 colour = V3(0, 0, 0);
     const material_t* m = &sc->mats[it->mat];
-    /* Plane/AABB get_diffuse without a texture returns the (checker) material's diffuse,
-     * which is it->mat (simple_geometry.py:150-173, :312-355). */
-    vec3 diffuse = m->diffuse;
+    /* scene.py:143-146: Plane/AABB hits take get_diffuse(position) of the geometry that
+     * was hit (for a hierarchy leaf: the world position in the leaf's own frame) */
+    const object_t* g = &sc->objs[it->obj];
+    vec3 diffuse = g->type == T_PLANE ? plane_diffuse(sc, g, it->position)
+                 : g->type == T_BOX ? box_diffuse(sc, g, it->position) : m->diffuse;
     sc->shade_points++;
     for (int li = 0; li < sc->n_lights; li++) {
         const light_t* L = &sc->lights[li];
@@ -527,8 +896,8 @@ static vec3 regular_lighting(scene_t* sc, const ray_t* ray, const isect_t* it) {
         }
         sc->shadow_rays++;
         int skip = 0;
-        for (int oi = 0; oi < sc->n_objs; oi++) {
-            if (obj_shadow(sc, oi, &sray, t_max)) { skip = 1; break; }
+        for (int r = 0; r < sc->n_roots; r++) {
+            if (obj_shadow(sc, sc->roots[r], &sray, t_max)) { skip = 1; break; }
         }
         if (skip) continue;
         vec3 light_dir = L->type == L_POINT ? vnormalize(vsub(L->vector, it->position)) : vnormalize(vneg(L->vector));
@@ -567,7 +936,7 @@ static vec3 cast_ray(scene_t* sc, const ray_t* ray, int max_recursion, int in_sh
     if (max_recursion == 0) return V3(0, 0, 0);
     sc->cast_depth[10 - max_recursion]++;
     hitlist_t hits = {0, 0, 0};
-    for (int oi = 0; oi < sc->n_objs; oi++) obj_intersect(sc, oi, ray, &hits);
+    for (int r = 0; r < sc->n_roots; r++) obj_intersect(sc, sc->roots[r], ray, &hits);
     if (hits.n == 0) { free(hits.v); return V3(0, 0, 0); }
     /* min(intersections, key=time): the first minimum in list order */
     isect_t first = hits.v[0];
@@ -673,6 +1042,7 @@ static void scene_free(scene_t* sc) {
         free(sc->objs[i].norms);
     }
     free(sc->objs);
+    free(sc->roots);
     free(sc->mats);
     free(sc->lights);
     free(sc->times);
@@ -776,8 +1146,29 @@ static scene_t* scene_build(const oracle_scene_in* in) {
             case T_MESH:
                 mesh_build(o, in, i);
                 break;
+            case T_NODE: {
+                /* Hierarchy.__init__ / make_matrices (hierarchy.py:12-40) */
+                o->htype = in->node_htype[i];
+                o->nchild = in->obj_nchild[i];
+                o->children = in->child_idx + in->obj_child_off[i];
+                const double* trs = &in->node_trs[9 * i];
+                make_matrices(vfrom(trs), vfrom(trs + 3), vfrom(trs + 6), &o->M, &o->Minv);
+                o->MinvT = mat_transpose(o->Minv);
+                break;
+            }
         }
+        o->tex = in->obj_tex[i];
+        o->tex_scale = in->obj_tex_scale[i];
     }
+    sc->roots = (int*)malloc(sizeof(int) * (size_t)(in->n_objs > 0 ? in->n_objs : 1));
+    sc->n_roots = 0;
+    for (int i = 0; i < in->n_objs; i++)
+        if (in->obj_parent[i] < 0) sc->roots[sc->n_roots++] = i;
+    sc->n_tex = in->n_tex;
+    sc->tex_w = in->tex_w;
+    sc->tex_h = in->tex_h;
+    sc->tex_off = in->tex_off;
+    sc->tex_data = in->tex_data;
     return sc;
 }
 
@@ -839,6 +1230,7 @@ int oracle_render(const oracle_scene_in* in, int subimage, int tasks, double* ou
         }
         x += dx;
     }
+    const int err = sc->error;
     if (tallies) {
         for (int k = 0; k < 11; k++) tallies[k] = sc->cast_depth[k];
         tallies[11] = sc->shadow_rays;
@@ -847,7 +1239,7 @@ int oracle_render(const oracle_scene_in* in, int subimage, int tasks, double* ou
     free(dof_origins);
     free(aa_origins);
     scene_free(sc);
-    return 0;
+    return err ? -3 : 0;
 }
 
 /* Geometry.intersect for one object (KAT vectors). Writes up to max_hits hits
@@ -890,17 +1282,22 @@ int oracle_closest_batch(const oracle_scene_in* in, double time, int n, const fl
         ray.origin = V3(o[3 * i], o[3 * i + 1], o[3 * i + 2]);
         ray.direction = V3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
         hits.n = 0;
-        for (int oi = 0; oi < sc->n_objs; oi++) obj_intersect(sc, oi, &ray, &hits);
+        int root_of_first = -1, kfirst = -1;
+        for (int r = 0; r < sc->n_roots; r++) {
+            const int n0 = hits.n;
+            obj_intersect(sc, sc->roots[r], &ray, &hits);
+            for (int k = n0; k < hits.n; k++)
+                if (kfirst < 0 || hits.v[k].time < hits.v[kfirst].time) { kfirst = k; root_of_first = r; }
+        }
         if (hits.n == 0) {
             t_out[i] = INFINITY; obj_out[i] = -1; sub_out[i] = -1; mat_out[i] = -1;
             n_out[3 * i] = n_out[3 * i + 1] = n_out[3 * i + 2] = 0;
             p_out[3 * i] = p_out[3 * i + 1] = p_out[3 * i + 2] = 0;
             continue;
         }
-        isect_t first = hits.v[0];
-        for (int k = 1; k < hits.n; k++)
-            if (hits.v[k].time < first.time) first = hits.v[k];
-        t_out[i] = first.time; obj_out[i] = first.obj; sub_out[i] = first.sub; mat_out[i] = first.mat;
+        isect_t first = hits.v[kfirst];
+        /* obj: position of the hit's top-level object in Scene.objects */
+        t_out[i] = first.time; obj_out[i] = root_of_first; sub_out[i] = first.sub; mat_out[i] = first.mat;
         n_out[3 * i] = first.normal.x; n_out[3 * i + 1] = first.normal.y; n_out[3 * i + 2] = first.normal.z;
         p_out[3 * i] = first.position.x; p_out[3 * i + 1] = first.position.y; p_out[3 * i + 2] = first.position.z;
     }
@@ -918,8 +1315,8 @@ int oracle_shadow_batch(const oracle_scene_in* in, double time, int n, const flo
         ray.origin = V3(o[3 * i], o[3 * i + 1], o[3 * i + 2]);
         ray.direction = V3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
         int occ = 0;
-        for (int oi = 0; oi < sc->n_objs; oi++)
-            if (obj_shadow(sc, oi, &ray, t_max[i])) { occ = 1; break; }
+        for (int r = 0; r < sc->n_roots; r++)
+            if (obj_shadow(sc, sc->roots[r], &ray, t_max[i])) { occ = 1; break; }
         occluded[i] = occ;
     }
     scene_free(sc);

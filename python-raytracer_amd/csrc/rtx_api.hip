@@ -77,9 +77,9 @@ __device__ __forceinline__ void flush_tally(const Tally& tl, unsigned long long*
 
 // scene.py:47-79 for pixel p of the output block (host/device: the tests-only host
 // emulation runs the same body).
-template <bool MESH, bool SEC, bool COUNT, bool JIT>
+template <bool MESH, bool SEC, bool X, bool COUNT, bool JIT>
 RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, int32_t cc, Tally& tl,
-                         const FrameStack& fs) {
+                         const FrameStack& fs, const HStack& hs) {
     const int64_t p = (int64_t)rr * P.ncols + cc;
     const int j = P.height - 1 - (row0 + rr);  // reference row index (y grows upward)
     const float fx = P.xs[cc];
@@ -106,7 +106,7 @@ RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, 
                 o = add(o, scale(normalize(rnd), P.jscale));
             }
             for (int kt = 0; kt < P.n_times; ++kt)
-                colour = add(colour, cast_ray<MESH, SEC, COUNT>(P.S, o, ddir, P.times[kt], tl, fs));
+                colour = add(colour, cast_ray<MESH, SEC, X, COUNT>(P.S, o, ddir, P.times[kt], tl, fs, hs));
         }
     }
     // colour / (samples * dof_samples * len(motion_times)) (scene.py:73); for a power of
@@ -169,58 +169,73 @@ __host__ __device__ inline int64_t launch_items(int32_t nrows, int32_t ncols) {
     return (waves + RTX_PPL - 1) / RTX_PPL * 64;
 }
 
-template <bool MESH, bool SEC, bool COUNT, bool JIT>
-__global__ __launch_bounds__(256, RTX_LB_WAVES(MESH, SEC)) void k_render(const KParams* __restrict__ Pp, const Launch L) {
+// Block size: 256 threads, or one wave for the hierarchy/texture (X) variants, whose
+// per-thread ray/point stacks (9 words per hierarchy level) share the CU's LDS.
+template <bool X>
+constexpr int kBlock = X ? 64 : 256;
+
+template <bool MESH, bool SEC, bool X, bool COUNT, bool JIT>
+__global__ __launch_bounds__(kBlock<X>, X ? 1 : RTX_LB_WAVES(MESH, SEC)) void k_render(const KParams* __restrict__ Pp,
+                                                                                  const Launch L) {
+    constexpr int B = kBlock<X>;
     const int32_t ncols = Pp->ncols;
     Tally tl = {};
     // secondary-ray frames: [frame][word][thread] in LDS (40 KB per 256-thread block)
-    __shared__ float frames[SEC ? kMaxDepth * 4 * 256 : 1];
-    const FrameStack fs{frames + threadIdx.x, 256};
+    __shared__ float frames[SEC ? kMaxDepth * 4 * B : 1];
+    extern __shared__ float hstack[];  // X: [level][9][thread] (dynamic size)
+    const FrameStack fs{frames + threadIdx.x, B};
+    const HStack hs{hstack + threadIdx.x, B};
     bool any_active = false;
     for (int sub = 0; sub < RTX_PPL; ++sub) {
         const PixelRC px = pixel_rc(ncols, sub);
         const bool active = px.r < L.nrows && px.c < ncols;
         any_active = any_active || active;
-        if (active) render_pixel<MESH, SEC, COUNT, JIT>(*Pp, L.fb, L.row0, px.r, px.c, tl, fs);
+        if (active) render_pixel<MESH, SEC, X, COUNT, JIT>(*Pp, L.fb, L.row0, px.r, px.c, tl, fs, hs);
     }
     flush_tally<COUNT>(tl, L.counters, any_active);
 }
 
-template <bool MESH>
+template <bool MESH, bool X>
 __global__ __launch_bounds__(256) void k_intersect(SceneView S, int64_t n, const float* __restrict__ ro,
                                                    const float* __restrict__ rd, float time, double* t_out,
                                                    int32_t* obj_out, int32_t* mat_out, float* n_out, float* p_out) {
+    extern __shared__ float hstack[];
+    const HStack hs{hstack + threadIdx.x, (int)blockDim.x};
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const f3 o = mk(ro[i], ro[n + i], ro[2 * n + i]);
     const f3 d = mk(rd[i], rd[n + i], rd[2 * n + i]);
     Tally tl = {};
-    const Hit h = closest_hit<MESH, false>(S, o, d, time, tl);
+    HHit hh;
+    const Hit h = closest_hit<MESH, X, false>(S, o, d, time, tl, hs, hh);
     int32_t mat = -1;
     f3 nn = mk(0.0f, 0.0f, 0.0f), pp = mk(0.0f, 0.0f, 0.0f);
-    if (h.obj >= 0) {
-        const Surface sf = resolve_hit<MESH>(S, h, o, d, time);
+    const bool hit = h.obj != -1;
+    if (hit) {
+        const Surface sf = resolve_hit<MESH, X>(S, h, hh, o, d, time);
         mat = sf.mat;
         nn = sf.normal;
         pp = sf.position;
     }
-    if (t_out) t_out[i] = h.obj >= 0 ? hit_t64(S, h.obj, h.sub, o, d, time) : (double)INFINITY;
-    if (obj_out) obj_out[i] = h.obj >= 0 ? S.objs[h.obj].oid : -1;
+    if (t_out) t_out[i] = !hit ? (double)INFINITY : h.obj == kHierHit ? hh.t64 : hit_t64(S, h.obj, h.sub, o, d, time);
+    if (obj_out) obj_out[i] = !hit ? -1 : h.obj == kHierHit ? h.sub : S.objs[h.obj].oid;
     if (mat_out) mat_out[i] = mat;
     if (n_out) { n_out[i] = nn.x; n_out[n + i] = nn.y; n_out[2 * n + i] = nn.z; }
     if (p_out) { p_out[i] = pp.x; p_out[n + i] = pp.y; p_out[2 * n + i] = pp.z; }
 }
 
-template <bool MESH>
+template <bool MESH, bool X>
 __global__ __launch_bounds__(256) void k_occluded(SceneView S, int64_t n, const float* __restrict__ ro,
                                                   const float* __restrict__ rd, const double* __restrict__ tmax,
                                                   float time, uint8_t* occ) {
+    extern __shared__ float hstack[];
+    const HStack hs{hstack + threadIdx.x, (int)blockDim.x};
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const f3 o = mk(ro[i], ro[n + i], ro[2 * n + i]);
     const f3 d = mk(rd[i], rd[n + i], rd[2 * n + i]);
     Tally tl = {};
-    occ[i] = occluded<MESH, false>(S, o, d, tmax[i], time, tl) ? 1 : 0;
+    occ[i] = occluded<MESH, X, false>(S, o, d, tmax[i], time, tl, hs) ? 1 : 0;
 }
 
 __global__ __launch_bounds__(256) void k_to_rgb8(const float* __restrict__ fb, uint8_t* __restrict__ out, int64_t n) {
@@ -240,7 +255,98 @@ void set3(float* dst, const float* s) { dst[0] = s[0]; dst[1] = s[1]; dst[2] = s
 void set3(float* dst, f3 s) { dst[0] = s.x; dst[1] = s.y; dst[2] = s.z; dst[3] = 0.0f; }
 bool finite3(const float* v) { return std::isfinite(v[0]) && std::isfinite(v[1]) && std::isfinite(v[2]); }
 
+// Hierarchy.make_matrices (hierarchy.py:30-40) with GLM's float mat4 code (PyGLM):
+// translate, rotate about x, y, z (glm.radians of a Python float is fp64, the angle is
+// then a float; cosf/sinf), scale, and the cofactor inverse. m[col * 4 + row].
+struct Mat4 {
+    float m[16];
+};
+Mat4 m4_identity() {
+    Mat4 r{};
+    r.m[0] = r.m[5] = r.m[10] = r.m[15] = 1.0f;
+    return r;
+}
+Mat4 m4_translate(const Mat4& m, f3 v) {  // Result[3] = m[0] v0 + m[1] v1 + m[2] v2 + m[3]
+    Mat4 r = m;
+    for (int k = 0; k < 4; ++k) r.m[12 + k] = ((m.m[k] * v.x + m.m[4 + k] * v.y) + m.m[8 + k] * v.z) + m.m[12 + k];
+    return r;
+}
+Mat4 m4_rotate(const Mat4& m, float angle, f3 v) {
+    const float c = cosf(angle), s = sinf(angle);
+    const f3 axis = normalize(v);
+    const f3 temp = scale(axis, 1.0f - c);
+    const float ax[3] = {axis.x, axis.y, axis.z}, tp[3] = {temp.x, temp.y, temp.z};
+    float R[3][3];
+    R[0][0] = c + tp[0] * ax[0];
+    R[0][1] = tp[0] * ax[1] + s * ax[2];
+    R[0][2] = tp[0] * ax[2] - s * ax[1];
+    R[1][0] = tp[1] * ax[0] - s * ax[2];
+    R[1][1] = c + tp[1] * ax[1];
+    R[1][2] = tp[1] * ax[2] + s * ax[0];
+    R[2][0] = tp[2] * ax[0] + s * ax[1];
+    R[2][1] = tp[2] * ax[1] - s * ax[0];
+    R[2][2] = c + tp[2] * ax[2];
+    Mat4 r = m;
+    for (int col = 0; col < 3; ++col)
+        for (int k = 0; k < 4; ++k)
+            r.m[4 * col + k] = (m.m[k] * R[col][0] + m.m[4 + k] * R[col][1]) + m.m[8 + k] * R[col][2];
+    return r;
+}
+Mat4 m4_scale(const Mat4& m, f3 v) {
+    Mat4 r = m;
+    const float sv[3] = {v.x, v.y, v.z};
+    for (int col = 0; col < 3; ++col)
+        for (int k = 0; k < 4; ++k) r.m[4 * col + k] = m.m[4 * col + k] * sv[col];
+    return r;
+}
+Mat4 m4_inverse(const Mat4& M) {  // glm compute_inverse<4, 4>
+    auto m = [&](int c, int r) { return M.m[4 * c + r]; };
+    const float C00 = m(2, 2) * m(3, 3) - m(3, 2) * m(2, 3), C02 = m(1, 2) * m(3, 3) - m(3, 2) * m(1, 3);
+    const float C03 = m(1, 2) * m(2, 3) - m(2, 2) * m(1, 3), C04 = m(2, 1) * m(3, 3) - m(3, 1) * m(2, 3);
+    const float C06 = m(1, 1) * m(3, 3) - m(3, 1) * m(1, 3), C07 = m(1, 1) * m(2, 3) - m(2, 1) * m(1, 3);
+    const float C08 = m(2, 1) * m(3, 2) - m(3, 1) * m(2, 2), C10 = m(1, 1) * m(3, 2) - m(3, 1) * m(1, 2);
+    const float C11 = m(1, 1) * m(2, 2) - m(2, 1) * m(1, 2), C12 = m(2, 0) * m(3, 3) - m(3, 0) * m(2, 3);
+    const float C14 = m(1, 0) * m(3, 3) - m(3, 0) * m(1, 3), C15 = m(1, 0) * m(2, 3) - m(2, 0) * m(1, 3);
+    const float C16 = m(2, 0) * m(3, 2) - m(3, 0) * m(2, 2), C18 = m(1, 0) * m(3, 2) - m(3, 0) * m(1, 2);
+    const float C19 = m(1, 0) * m(2, 2) - m(2, 0) * m(1, 2), C20 = m(2, 0) * m(3, 1) - m(3, 0) * m(2, 1);
+    const float C22 = m(1, 0) * m(3, 1) - m(3, 0) * m(1, 1), C23 = m(1, 0) * m(2, 1) - m(2, 0) * m(1, 1);
+    const float F0[4] = {C00, C00, C02, C03}, F1[4] = {C04, C04, C06, C07}, F2[4] = {C08, C08, C10, C11};
+    const float F3[4] = {C12, C12, C14, C15}, F4[4] = {C16, C16, C18, C19}, F5[4] = {C20, C20, C22, C23};
+    const float V0[4] = {m(1, 0), m(0, 0), m(0, 0), m(0, 0)}, V1[4] = {m(1, 1), m(0, 1), m(0, 1), m(0, 1)};
+    const float V2[4] = {m(1, 2), m(0, 2), m(0, 2), m(0, 2)}, V3[4] = {m(1, 3), m(0, 3), m(0, 3), m(0, 3)};
+    const float SA[4] = {+1, -1, +1, -1}, SB[4] = {-1, +1, -1, +1};
+    Mat4 inv;
+    for (int k = 0; k < 4; ++k) {
+        inv.m[k] = ((V1[k] * F0[k] - V2[k] * F1[k]) + V3[k] * F2[k]) * SA[k];
+        inv.m[4 + k] = ((V0[k] * F0[k] - V2[k] * F3[k]) + V3[k] * F4[k]) * SB[k];
+        inv.m[8 + k] = ((V0[k] * F1[k] - V1[k] * F3[k]) + V3[k] * F5[k]) * SA[k];
+        inv.m[12 + k] = ((V0[k] * F2[k] - V1[k] * F4[k]) + V2[k] * F5[k]) * SB[k];
+    }
+    float dot0[4];
+    for (int k = 0; k < 4; ++k) dot0[k] = M.m[k] * inv.m[4 * k];  // m[0] * Row0
+    const float det = (dot0[0] + dot0[1]) + (dot0[2] + dot0[3]);
+    const float one_over = 1.0f / det;
+    for (int k = 0; k < 16; ++k) inv.m[k] = inv.m[k] * one_over;
+    return inv;
+}
+void make_matrices(const float* trs, Mat4& M, Mat4& Minv) {
+    const double k = 0.017453292519943295;  // glm::radians
+    Mat4 m = m4_identity();
+    m = m4_translate(m, ld3(trs));
+    m = m4_rotate(m, (float)((double)trs[3] * k), mk(1, 0, 0));
+    m = m4_rotate(m, (float)((double)trs[4] * k), mk(0, 1, 0));
+    m = m4_rotate(m, (float)((double)trs[5] * k), mk(0, 0, 1));
+    m = m4_scale(m, ld3(trs + 6));
+    M = m;
+    Minv = m4_inverse(m);
+}
+
 struct HostScene {
+    std::vector<DNode> nodes;
+    std::vector<uint32_t> texels;
+    std::vector<float> lut255;
+    int32_t hlevels = 0;
+    bool has_ext = false;  // hierarchies or textures
     std::vector<DObj> objs;
     std::vector<DTri> tris;
     std::vector<DTriN> trins;
@@ -324,6 +430,54 @@ int convert_scene(const rtx_scene_desc* desc, HostScene& H) {
         set3(H.trins[i].n1, t.n1);
         set3(H.trins[i].n2, t.n2);
     }
+    // textures: RGBA8 texels (alpha unused), fl32(k / 255) table
+    if (desc->n_textures < 0 || (desc->n_textures && !desc->textures))
+        return fail(RTX_ERR_INVALID, "rtx_scene_create: bad texture array");
+    std::vector<int64_t> tex_off(desc->n_textures);
+    for (int t = 0; t < desc->n_textures; ++t) {
+        const rtx_texture& tx = desc->textures[t];
+        if (tx.width < 1 || tx.height < 1 || !tx.rgb || (int64_t)tx.width * tx.height > (1 << 28))
+            return fail(RTX_ERR_INVALID, "texture " + std::to_string(t) + ": bad size or data");
+        tex_off[t] = (int64_t)H.texels.size();
+        const int64_t n = (int64_t)tx.width * tx.height;
+        for (int64_t q = 0; q < n; ++q)
+            H.texels.push_back((uint32_t)tx.rgb[3 * q] | ((uint32_t)tx.rgb[3 * q + 1] << 8) | ((uint32_t)tx.rgb[3 * q + 2] << 16));
+    }
+    if ((int64_t)H.texels.size() > INT32_MAX) return fail(RTX_ERR_INVALID, "textures too large");
+    H.lut255.resize(256);
+    for (int k = 0; k < 256; ++k) H.lut255[k] = (float)(k / 255.0);  // pixel[c] / 255 (fp64) -> vec3
+    // hierarchy structure: parents precede children (preorder), parents are nodes
+    std::vector<int32_t> top_ordinal(desc->n_objects, -1), nchild(desc->n_objects, 0), cidx(desc->n_objects, 0);
+    std::vector<int32_t> depth(desc->n_objects, 0), root_of(desc->n_objects, -1);
+    int32_t n_top = 0;
+    for (int i = 0; i < desc->n_objects; ++i) {
+        const rtx_object& o = desc->objects[i];
+        const std::string tag = "object " + std::to_string(i) + ": ";
+        if (o.parent == -1) {
+            top_ordinal[i] = n_top++;
+            root_of[i] = i;
+        } else {
+            if (o.parent < 0 || o.parent >= i || desc->objects[o.parent].type != RTX_NODE)
+                return fail(RTX_ERR_INVALID, tag + "parent must be an earlier RTX_NODE record");
+            if (i > o.parent + 1) {  // preorder: the previous record is the parent or inside a sibling subtree
+                int a = i - 1;
+                while (a != -1 && a != o.parent) a = desc->objects[a].parent;
+                if (a != o.parent) return fail(RTX_ERR_INVALID, tag + "records are not in preorder");
+            }
+            cidx[i] = nchild[o.parent]++;
+            depth[i] = depth[o.parent] + 1;
+            root_of[i] = root_of[o.parent];
+            if (depth[i] >= kMaxHLevels - 2) return fail(RTX_ERR_INVALID, tag + "hierarchy too deep");
+        }
+        if (o.type == RTX_NODE && (o.hierarchy_type < RTX_UNION || o.hierarchy_type > RTX_HIER_OTHER))
+            return fail(RTX_ERR_INVALID, tag + "bad hierarchy type");
+        if (o.texture < -1 || o.texture >= desc->n_textures || (o.texture >= 0 && o.type != RTX_PLANE && o.type != RTX_BOX))
+            return fail(RTX_ERR_INVALID, tag + "bad texture index");
+    }
+    for (int i = 0; i < desc->n_objects; ++i)
+        if (desc->objects[i].type == RTX_NODE && desc->objects[i].hierarchy_type == RTX_DIFFERENCE && nchild[i] < 2)
+            return fail(RTX_ERR_INVALID, "object " + std::to_string(i) +
+                                             ": difference node needs two children (the reference raises IndexError)");
     for (int i = 0; i < desc->n_objects; ++i) {
         const rtx_object& o = desc->objects[i];
         DObj& d = H.objs[i];
@@ -331,6 +485,22 @@ int convert_scene(const rtx_scene_desc* desc, HostScene& H) {
         const std::string tag = "object " + std::to_string(i) + ": ";
         d.type = o.type;
         d.nmat = o.n_mats;
+        if (o.texture >= 0) {
+            const rtx_texture& tx = desc->textures[o.texture];
+            d.has_tex = 1;
+            d.tex_off = (int32_t)tex_off[o.texture];
+            d.tex_w = tx.width;
+            d.tex_h = tx.height;
+            d.tex_scale = o.texture_scale;
+            H.has_ext = true;
+        }
+        d.oid = top_ordinal[root_of[i]];
+        if (o.type == RTX_NODE) {
+            H.has_ext = true;
+            if (o.n_mats > 0 && (o.mat[0] < 0 || o.mat[0] >= desc->n_materials))
+                return fail(RTX_ERR_INVALID, tag + "material index out of range");
+            continue;
+        }
         if (o.n_mats < 1) return fail(RTX_ERR_INVALID, tag + "no material (the reference raises IndexError)");
         for (int k = 0; k < (o.n_mats < 2 ? o.n_mats : 2); ++k)
             if (o.mat[k] < 0 || o.mat[k] >= desc->n_materials) return fail(RTX_ERR_INVALID, tag + "material index out of range");
@@ -343,6 +513,7 @@ int convert_scene(const rtx_scene_desc* desc, HostScene& H) {
         switch (o.type) {
             case RTX_SPHERE:
                 d.r2 = std::pow(o.radius, 2.0);  // self.radius ** 2
+                d.radius = o.radius;
                 break;
             case RTX_PLANE: {
                 // Plane.__init__ axes (simple_geometry.py:93-103), exact vec3 compares
@@ -386,12 +557,12 @@ int convert_scene(const rtx_scene_desc* desc, HostScene& H) {
     int32_t counts[4] = {0, 0, 0, 0};
     for (int g = 0; g < 4; ++g)
         for (int i = 0; i < desc->n_objects; ++i)
-            if (H.objs[i].type == order[g]) {
-                DObj d = H.objs[i];
-                d.oid = i;
-                grouped.push_back(d);
+            if (desc->objects[i].parent == -1 && H.objs[i].type == order[g]) {
+                grouped.push_back(H.objs[i]);
                 counts[g]++;
             }
+    std::vector<DObj> all_objs;
+    all_objs.swap(H.objs);
     H.objs.swap(grouped);
     H.n_plane = counts[0]; H.n_sphere = counts[1]; H.n_box = counts[2]; H.n_mesh = counts[3];
     // Mesh face clusters: reorder each mesh's faces into spatially coherent leaves of <= 8
@@ -457,7 +628,43 @@ int convert_scene(const rtx_scene_desc* desc, HostScene& H) {
         d.leaf_count = (int32_t)H.leaves.size() - leaf0;
         d.cmax = cmax;
     }
-    H.n_objs = desc->n_objects;
+    // Hierarchies: the subtrees of the top-level nodes, in preorder, as DNode records;
+    // their leaves are appended to objs (after the top-level groups, faces in OBJ order).
+    std::vector<int32_t> node_of(desc->n_objects, -1);
+    for (int i = 0; i < desc->n_objects; ++i) {
+        const rtx_object& o = desc->objects[i];
+        if (root_of[i] < 0 || desc->objects[root_of[i]].type != RTX_NODE) continue;
+        DNode nd;
+        std::memset(&nd, 0, sizeof(nd));
+        node_of[i] = (int32_t)H.nodes.size();
+        nd.parent = o.parent >= 0 ? node_of[o.parent] : -1;
+        nd.pkind = o.parent >= 0 ? desc->objects[o.parent].hierarchy_type : -1;
+        nd.cidx = cidx[i];
+        nd.depth = depth[i];
+        nd.oid = top_ordinal[root_of[i]];
+        nd.mat0 = o.n_mats > 0 ? o.mat[0] : -1;
+        nd.obj = -1;
+        if (o.type == RTX_NODE) {
+            nd.kind = o.hierarchy_type;
+            Mat4 M, Mi;
+            make_matrices(o.trs, M, Mi);
+            std::memcpy(nd.M, M.m, sizeof(nd.M));
+            std::memcpy(nd.Minv, Mi.m, sizeof(nd.Minv));
+            H.hlevels = std::max(H.hlevels, nd.depth + 2);
+        } else {
+            nd.kind = HN_LEAF;
+            nd.obj = (int32_t)H.objs.size();
+            H.objs.push_back(all_objs[i]);
+        }
+        H.nodes.push_back(nd);
+    }
+    for (int i = (int)desc->n_objects - 1; i >= 0; --i) {  // subtree ends
+        if (node_of[i] < 0) continue;
+        DNode& nd = H.nodes[node_of[i]];
+        if (nd.end == 0) nd.end = node_of[i] + 1;
+        if (nd.parent >= 0) H.nodes[nd.parent].end = std::max(H.nodes[nd.parent].end, nd.end);
+    }
+    H.n_objs = (int32_t)H.objs.size();
     H.n_lights = desc->n_lights;
     set3(H.ambient, desc->ambient);
     return RTX_OK;
@@ -504,7 +711,11 @@ int convert_camera(const rtx_camera_desc* c, KParams& k) {
 struct rtx_scene {
     int device = 0;
     SceneView view{};
-    bool has_mesh = false, has_secondary = false;
+    bool has_mesh = false, has_secondary = false, has_ext = false;
+    int32_t hlevels = 0;
+    void* d_nodes = nullptr;
+    void* d_texels = nullptr;
+    void* d_lut = nullptr;
     void* d_objs = nullptr;
     void* d_tris = nullptr;
     void* d_trins = nullptr;
@@ -544,7 +755,8 @@ void free_camera(rtx_scene* s) {
 
 void free_scene(rtx_scene* s) {
     free_camera(s);
-    for (void* p : {s->d_objs, s->d_tris, s->d_trins, s->d_mats, s->d_lights, s->d_leaves, s->d_tri_orig})
+    for (void* p : {s->d_objs, s->d_tris, s->d_trins, s->d_mats, s->d_lights, s->d_leaves, s->d_tri_orig, s->d_nodes,
+                    s->d_texels, s->d_lut})
         (void)hipFree(p);
     delete s;
 }
@@ -567,12 +779,15 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
     if (hipGetDevice(&s->device) != hipSuccess) { delete s; return fail(RTX_ERR_HIP, "hipGetDevice failed"); }
     if ((rc = upload(&s->d_objs, H.objs)) || (rc = upload(&s->d_tris, H.tris)) || (rc = upload(&s->d_trins, H.trins)) ||
         (rc = upload(&s->d_mats, H.mats)) || (rc = upload(&s->d_lights, H.lights)) ||
-        (rc = upload(&s->d_leaves, H.leaves)) || (rc = upload(&s->d_tri_orig, H.tri_orig))) {
+        (rc = upload(&s->d_leaves, H.leaves)) || (rc = upload(&s->d_tri_orig, H.tri_orig)) ||
+        (rc = upload(&s->d_nodes, H.nodes)) || (rc = upload(&s->d_texels, H.texels)) || (rc = upload(&s->d_lut, H.lut255))) {
         free_scene(s);
         return rc;
     }
     s->has_mesh = H.has_mesh;
     s->has_secondary = H.has_secondary;
+    s->has_ext = H.has_ext;
+    s->hlevels = H.hlevels;
     SceneView& v = s->view;
     v.objs = (cptr<DObj>)s->d_objs;
     v.tris = (cptr<DTri>)s->d_tris;
@@ -586,6 +801,11 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
     v.n_plane = H.n_plane; v.n_sphere = H.n_sphere; v.n_box = H.n_box; v.n_mesh = H.n_mesh;
     v.pow_bits = H.pow_bits;
     std::memcpy(v.ambient, H.ambient, sizeof(v.ambient));
+    v.nodes = (cptr<DNode>)s->d_nodes;
+    v.texels = (cptr<uint32_t>)s->d_texels;
+    v.lut255 = (cptr<float>)s->d_lut;
+    v.n_nodes = (int32_t)H.nodes.size();
+    v.hlevels = H.hlevels;
     *out = s;
     return RTX_OK;
 }
@@ -639,32 +859,24 @@ int rtx_render(rtx_scene* s, int32_t row0, int32_t nrows, float* fb_dev, uint64_
     L.nrows = nrows;
     L.counters = reinterpret_cast<unsigned long long*>(counters_dev);
     const int64_t items = launch_items(nrows, s->kp.ncols);
-    const dim3 grid((unsigned)((items + 255) / 256)), block(256);
     hipStream_t st = (hipStream_t)stream;
     const bool cnt = counters_dev != nullptr;
     const bool jit = s->kp.jitter != RTX_JITTER_OFF;
-    const int sel = (s->has_mesh ? 8 : 0) | (s->has_secondary ? 4 : 0) | (cnt ? 2 : 0) | (jit ? 1 : 0);
+    const int sel = (s->has_mesh ? 16 : 0) | (s->has_secondary ? 8 : 0) | (s->has_ext ? 4 : 0) | (cnt ? 2 : 0) | (jit ? 1 : 0);
     const KParams* kp = s->d_kp;
-#define RTX_LAUNCH(M, S, C, J) \
-    hipLaunchKernelGGL((k_render<M, S, C, J>), grid, block, 0, st, kp, L)
+    const size_t hbytes = (size_t)s->hlevels * 9 * sizeof(float);
+#define RTX_LAUNCH(M, S, X, C, J)                                                                              \
+    hipLaunchKernelGGL((k_render<M, S, X, C, J>), dim3((unsigned)((items + kBlock<X> - 1) / kBlock<X>)),   \
+                       dim3(kBlock<X>), X ? hbytes * kBlock<X> : 0, st, kp, L)
+#define RTX_CASE(n) \
+    case n: RTX_LAUNCH(((n) & 16) != 0, ((n) & 8) != 0, ((n) & 4) != 0, ((n) & 2) != 0, ((n) & 1) != 0); break
     switch (sel) {
-        case 0: RTX_LAUNCH(false, false, false, false); break;
-        case 1: RTX_LAUNCH(false, false, false, true); break;
-        case 2: RTX_LAUNCH(false, false, true, false); break;
-        case 3: RTX_LAUNCH(false, false, true, true); break;
-        case 4: RTX_LAUNCH(false, true, false, false); break;
-        case 5: RTX_LAUNCH(false, true, false, true); break;
-        case 6: RTX_LAUNCH(false, true, true, false); break;
-        case 7: RTX_LAUNCH(false, true, true, true); break;
-        case 8: RTX_LAUNCH(true, false, false, false); break;
-        case 9: RTX_LAUNCH(true, false, false, true); break;
-        case 10: RTX_LAUNCH(true, false, true, false); break;
-        case 11: RTX_LAUNCH(true, false, true, true); break;
-        case 12: RTX_LAUNCH(true, true, false, false); break;
-        case 13: RTX_LAUNCH(true, true, false, true); break;
-        case 14: RTX_LAUNCH(true, true, true, false); break;
-        case 15: RTX_LAUNCH(true, true, true, true); break;
+        RTX_CASE(0); RTX_CASE(1); RTX_CASE(2); RTX_CASE(3); RTX_CASE(4); RTX_CASE(5); RTX_CASE(6); RTX_CASE(7);
+        RTX_CASE(8); RTX_CASE(9); RTX_CASE(10); RTX_CASE(11); RTX_CASE(12); RTX_CASE(13); RTX_CASE(14); RTX_CASE(15);
+        RTX_CASE(16); RTX_CASE(17); RTX_CASE(18); RTX_CASE(19); RTX_CASE(20); RTX_CASE(21); RTX_CASE(22); RTX_CASE(23);
+        RTX_CASE(24); RTX_CASE(25); RTX_CASE(26); RTX_CASE(27); RTX_CASE(28); RTX_CASE(29); RTX_CASE(30); RTX_CASE(31);
     }
+#undef RTX_CASE
 #undef RTX_LAUNCH
     RTX_HIP(hipGetLastError());
     return RTX_OK;
@@ -675,12 +887,13 @@ int rtx_intersect(rtx_scene* s, int64_t n, const float* ro, const float* rd, dou
     if (!s || n < 0 || (n > 0 && (!ro || !rd))) return fail(RTX_ERR_INVALID, "rtx_intersect: bad argument");
     if (n == 0) return RTX_OK;
     const dim3 grid((unsigned)((n + 255) / 256)), block(256);
-    if (s->has_mesh)
-        hipLaunchKernelGGL(k_intersect<true>, grid, block, 0, (hipStream_t)stream, s->view, n, ro, rd, (float)time,
-                           t_dev, obj_dev, mat_dev, normal_dev, position_dev);
-    else
-        hipLaunchKernelGGL(k_intersect<false>, grid, block, 0, (hipStream_t)stream, s->view, n, ro, rd, (float)time,
-                           t_dev, obj_dev, mat_dev, normal_dev, position_dev);
+    const size_t lds = s->has_ext ? (size_t)s->hlevels * 9 * sizeof(float) * 256 : 0;
+#define RTX_ISECT(M, X)                                                                                          \
+    hipLaunchKernelGGL((k_intersect<M, X>), grid, block, lds, (hipStream_t)stream, s->view, n, ro, rd, (float)time, \
+                       t_dev, obj_dev, mat_dev, normal_dev, position_dev)
+    if (s->has_mesh) { if (s->has_ext) RTX_ISECT(true, true); else RTX_ISECT(true, false); }
+    else { if (s->has_ext) RTX_ISECT(false, true); else RTX_ISECT(false, false); }
+#undef RTX_ISECT
     RTX_HIP(hipGetLastError());
     return RTX_OK;
 }
@@ -690,10 +903,12 @@ int rtx_occluded(rtx_scene* s, int64_t n, const float* ro, const float* rd, cons
     if (!s || n < 0 || (n > 0 && (!ro || !rd || !tmax || !occ))) return fail(RTX_ERR_INVALID, "rtx_occluded: bad argument");
     if (n == 0) return RTX_OK;
     const dim3 grid((unsigned)((n + 255) / 256)), block(256);
-    if (s->has_mesh)
-        hipLaunchKernelGGL(k_occluded<true>, grid, block, 0, (hipStream_t)stream, s->view, n, ro, rd, tmax, (float)time, occ);
-    else
-        hipLaunchKernelGGL(k_occluded<false>, grid, block, 0, (hipStream_t)stream, s->view, n, ro, rd, tmax, (float)time, occ);
+    const size_t lds = s->has_ext ? (size_t)s->hlevels * 9 * sizeof(float) * 256 : 0;
+#define RTX_OCC(M, X) \
+    hipLaunchKernelGGL((k_occluded<M, X>), grid, block, lds, (hipStream_t)stream, s->view, n, ro, rd, tmax, (float)time, occ)
+    if (s->has_mesh) { if (s->has_ext) RTX_OCC(true, true); else RTX_OCC(true, false); }
+    else { if (s->has_ext) RTX_OCC(false, true); else RTX_OCC(false, false); }
+#undef RTX_OCC
     RTX_HIP(hipGetLastError());
     return RTX_OK;
 }

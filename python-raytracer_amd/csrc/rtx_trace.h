@@ -101,6 +101,9 @@ struct alignas(16) DObj {
     float bv_b[4];    // mesh BV AABB max
     double r2;        // sphere radius ** 2
     double bv_r2;     // mesh BV sphere radius ** 2
+    double radius;    // sphere radius (is_inside, simple_geometry.py:80)
+    double tex_scale; // plane texture_scale (scene_parser.py:226)
+    int32_t has_tex, tex_off, tex_w, tex_h;   // texture: texels [tex_off, + w * h), RGBA8
 };
 
 struct alignas(16) DTri {
@@ -146,6 +149,18 @@ enum : int32_t { MAT_DIFFUSE = 0, MAT_MIRROR = 1, MAT_REFRACTIVE = 2 };
 enum : int32_t { LIGHT_POINT = 0, LIGHT_DIRECTIONAL = 1 };
 enum : int32_t { BV_AABB = 0, BV_SPHERE = 1 };
 
+// Hierarchy nodes (hierarchy.py:11-146), flattened in preorder: the subtree of node i is
+// [i, end), a node's children follow it in child order. Leaves point at a DObj.
+enum : int32_t { HN_UNION = 0, HN_INTER = 1, HN_DIFF = 2, HN_OTHER = 3, HN_LEAF = 4 };
+struct alignas(16) DNode {
+    int32_t kind, parent, cidx, depth;  // depth 0 = a top-level object
+    int32_t end, pkind, obj, mat0;      // pkind: parent's kind; obj: leaf DObj; mat0: materials[0] or -1
+    int32_t oid, pad0, pad1, pad2;      // oid: the root's position in Scene.objects
+    float M[16];                        // glm mat4, [column][row]
+    float Minv[16];
+};
+constexpr int kMaxHLevels = 16;  // hierarchy depth limit (levels of the ray/point stacks)
+
 template <class T>
 using cptr = const T RTX_CONST*;
 
@@ -161,6 +176,10 @@ struct SceneView {
     int32_t n_plane, n_sphere, n_box, n_mesh;
     int32_t pow_bits, pad0, pad1, pad2;   // bit length of the largest integer hardness
     float ambient[4];
+    cptr<DNode> nodes;               // hierarchy nodes (roots: 0, nodes[0].end, ...)
+    cptr<uint32_t> texels;           // all textures, RGBA8 (A unused)
+    cptr<float> lut255;              // fl32(k / 255) (simple_geometry.py:169)
+    int32_t n_nodes, hlevels, pad3, pad4;  // hlevels: stack levels the hierarchies need
 };
 
 // ------------------------------------------------------------------ counters
@@ -184,6 +203,45 @@ RTX_HD f3 moved(const DObj& o, const float* p, float time) {
 
 // Ray.getPoint(t) = origin + direction * t, t cast to fp32 (helperclasses.py:21-22)
 RTX_HD f3 get_point(f3 o, f3 d, double t) { return add(o, scale(d, (float)t)); }
+
+// ------------------------------------------------------------------ materials, normals
+// math.floor(a - b) of two floats, where the reference subtracts in fp64 (exactly). The
+// fp32 difference d = fl32(a - b) lies in [k, k + 1] when floor(a - b) = k (k and k + 1
+// are floats below 2^23), so floorf(d) is exact unless d is an integer: then use fp64.
+RTX_HD int32_t floor_diff(float a, float b) {
+    const float d = a - b;
+    const float f = floorf(d);
+    if (fabsf(d) < 0x1p23f && d != f) return (int32_t)f;
+    return (int32_t)(int64_t)floor((double)a - (double)b);
+}
+
+// Plane.get_material (simple_geometry.py:133-148): checker by floor of the projected
+// coordinates, Python modulo.
+RTX_HD int32_t plane_material(const DObj& ob, f3 point, float time) {
+    if (ob.nmat == 1) return ob.mat0;
+    f3 position = moved(ob, ob.a, time);
+    f3 n = ld3(ob.b);
+    point = sub(point, scale(n, dot(sub(point, position), n)));
+    float x = dot(sub(point, position), ld3(ob.c));
+    float z = dot(sub(point, position), ld3(ob.e));
+    const int32_t s = floor_diff(position.x, x) + floor_diff(position.z, z);
+    return (s & 1) ? ob.mat1 : ob.mat0;  // (dx + dz) % 2 with Python modulo
+}
+
+// Barycentric smooth normal (mesh.py:103-113; igl.barycentric_coordinates_tri on fp32 rows).
+RTX_HD f3 smooth_normal(const DTri& T, const DTriN& N, f3 p) {
+    f3 a = ld3(T.v0), b = ld3(T.v1), c = ld3(T.v2);
+    f3 v0 = sub(b, a), v1 = sub(c, a), v2 = sub(p, a);
+    float d00 = dot(v0, v0), d01 = dot(v0, v1), d11 = dot(v1, v1);
+    float d20 = dot(v2, v0), d21 = dot(v2, v1);
+    float den = d00 * d11 - d01 * d01;
+    float v = (d11 * d20 - d01 * d21) / den;
+    float w = (d00 * d21 - d01 * d20) / den;
+    float u = (1.0f - v) - w;
+    f3 n = add(add(scale(ld3(N.n0), u), scale(ld3(N.n1), v)), scale(ld3(N.n2), w));
+    return normalize(n);
+}
+
 
 // ------------------------------------------------------------------ exact fp32 proxies
 // Every `t` the reference compares is an fp64 value t64. We carry t32 = fl32(t64):
@@ -400,9 +458,465 @@ RTX_HD void offer(const SceneView& S, Hit& h, bool valid, float t32, int32_t obj
     h.sub = take ? sb : h.sub;
 }
 
+// ------------------------------------------------------------------ textures
+// Python `x % m` (float_rem: the result takes the sign of m).
+RTX_HD double py_mod(double x, double m) {
+    double r = fmod(x, m);
+    if (r != 0.0) {
+        if ((m < 0.0) != (r < 0.0)) r += m;
+    } else {
+        r = copysign(0.0, m);
+    }
+    return r;
+}
+// texture.getpixel((i, j)) with int() / float truncation; the reference raises for an
+// index outside the image (only reachable through `x % w == w` rounding or NaN), the
+// device reads texel 0 of that row/column instead.
+RTX_HD f3 texel(const SceneView& S, const DObj& ob, double fi, double fj) {
+    const int i = (fi > -1.0 && fi < (double)ob.tex_w) ? (int)fi : 0;
+    const int j = (fj > -1.0 && fj < (double)ob.tex_h) ? (int)fj : 0;
+    const uint32_t t = S.texels[ob.tex_off + j * ob.tex_w + i];
+    return f3{S.lut255[t & 255u], S.lut255[(t >> 8) & 255u], S.lut255[(t >> 16) & 255u]};
+}
+// Plane.get_diffuse (simple_geometry.py:150-173); the projection uses the unmoved point.
+RTX_HD f3 plane_diffuse(const SceneView& S, const DObj& ob, f3 point, float time) {
+    if (!ob.has_tex) return ld3(S.mats[plane_material(ob, point, time)].diffuse);
+    const f3 position = moved(ob, ob.a, time);
+    const f3 n = ld3(ob.b);
+    point = sub(point, scale(n, dot(sub(point, ld3(ob.a)), n)));
+    const double u = (double)dot(sub(point, position), ld3(ob.c)) * 1000.0 / ob.tex_scale;
+    const double v = (double)dot(sub(point, position), ld3(ob.e)) * 1000.0 / ob.tex_scale;
+    return texel(S, ob, trunc(py_mod(u, (double)ob.tex_w)), trunc(py_mod(v, (double)ob.tex_h)));
+}
+// AABB.get_diffuse (simple_geometry.py:312-355), fp64 like the reference's Python floats.
+RTX_HD f3 box_diffuse(const SceneView& S, const DObj& ob, f3 point, float time) {
+    if (!ob.has_tex) return ld3(S.mats[ob.mat0].diffuse);
+    const f3 mn = moved(ob, ob.a, time), mx = moved(ob, ob.b, time);
+    const double px = point.x, py = point.y, pz = point.z;
+    const double x = (px - mn.x) / ((double)mx.x - mn.x);
+    const double y = (py - mn.y) / ((double)mx.y - mn.y);
+    const double z = (pz - mn.z) / ((double)mx.z - mn.z);
+    const double W = ob.tex_w, H = ob.tex_h, e = 1e-4;
+    double i = 0.0, j = 0.0;
+    if (fabs(px - mn.x) < e) { i = z * W; j = (1 - y) * H; }
+    else if (fabs(px - mx.x) < e) { i = (1 - z) * W; j = (1 - y) * H; }
+    else if (fabs(py - mn.y) < e) { i = x * W; j = (1 - z) * H; }
+    else if (fabs(py - mx.y) < e) { i = x * W; j = z * H; }
+    else if (fabs(pz - mn.z) < e) { i = (1 - x) * W; j = (1 - y) * H; }
+    else if (fabs(pz - mx.z) < e) { i = x * W; j = (1 - y) * H; }
+    // min(max(0, i), width - 1): Python keeps the first argument unless the second wins
+    i = i > 0.0 ? i : 0.0;
+    j = j > 0.0 ? j : 0.0;
+    i = W - 1 < i ? W - 1 : i;
+    j = H - 1 < j ? H - 1 : j;
+    return texel(S, ob, i, j);
+}
+// Geometry.get_diffuse as _compute_regular_lighting calls it for Plane/AABB hits
+// (scene.py:143-146); other geometry uses the hit material's diffuse.
+RTX_HD f3 get_diffuse(const SceneView& S, const DObj& ob, f3 point, float time) {
+    return ob.type == OBJ_PLANE ? plane_diffuse(S, ob, point, time) : box_diffuse(S, ob, point, time);
+}
+
+// ------------------------------------------------------------------ hierarchies (CSG)
+// Hierarchy.intersect / shadow_intersect / is_inside / get_material (hierarchy.py:42-138)
+// without recursion. R[k] is the ray handed to the nodes and leaves at depth k (R[0] =
+// the world ray); a node at depth k hands R[k + 1] = Minv * R[k] to its children
+// (hierarchy.py:43-45). P[k] is a point in the frame of the children of the depth-k node
+// whose is_inside is being evaluated. Both stacks live in LDS on the device ([slot]
+// [thread], 9 words per level), a local array in the host emulation.
+struct HStack {
+    float* base;
+    int stride;
+    RTX_HD void put_ray(int k, f3 o, f3 d) const {
+        float* p = base + k * 9 * stride;
+        p[0] = o.x; p[stride] = o.y; p[2 * stride] = o.z;
+        p[3 * stride] = d.x; p[4 * stride] = d.y; p[5 * stride] = d.z;
+    }
+    RTX_HD void get_ray(int k, f3& o, f3& d) const {
+        const float* p = base + k * 9 * stride;
+        o = f3{p[0], p[stride], p[2 * stride]};
+        d = f3{p[3 * stride], p[4 * stride], p[5 * stride]};
+    }
+    RTX_HD void put_pt(int k, f3 q) const {
+        float* p = base + (k * 9 + 6) * stride;
+        p[0] = q.x; p[stride] = q.y; p[2 * stride] = q.z;
+    }
+    RTX_HD f3 get_pt(int k) const {
+        const float* p = base + (k * 9 + 6) * stride;
+        return f3{p[0], p[stride], p[2 * stride]};
+    }
+};
+
+// glm.vec3(m * glm.vec4(p, w)): GLM's mat4 * vec4 is (m[0] x + m[1] y) + (m[2] z + m[3] w).
+RTX_HD f3 xform(const float* m, f3 p, float w) {
+    float r[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) r[k] = (m[k] * p.x + m[4 + k] * p.y) + (m[8 + k] * p.z + m[12 + k] * w);
+    return f3{r[0], r[1], r[2]};
+}
+// glm.normalize(glm.transpose(Minv) * glm.vec4(n, 0)).xyz (hierarchy.py:76): the
+// normalisation is over all four components (vec4 dot = (x*x + y*y) + (z*z + w*w)).
+RTX_HD f3 normal_xform(const float* mi, f3 n) {
+    float o[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        o[r] = (mi[4 * r] * n.x + mi[4 * r + 1] * n.y) + (mi[4 * r + 2] * n.z + mi[4 * r + 3] * 0.0f);
+    const float d2 = (o[0] * o[0] + o[1] * o[1]) + (o[2] * o[2] + o[3] * o[3]);
+    const float inv = 1.0f / sqrtf(d2);
+    return f3{o[0] * inv, o[1] * inv, o[2] * inv};
+}
+
+// AABB hit normal from the entry-slab label and the direction's sign (simple_geometry.py:231-242)
+RTX_HD f3 box_normal(int label, f3 d) {
+    const float dl = label == 0 ? d.x : (label == 1 ? d.y : d.z);
+    const float sgn = dl < 0.0f ? 1.0f : (dl > 0.0f ? -1.0f : 0.0f);
+    return f3{label == 0 ? sgn : 0.0f, label == 1 ? sgn : 0.0f, label == 2 ? sgn : 0.0f};
+}
+
+// Every hit of one leaf, in the reference's list order, with fp64 t (leaves of
+// hierarchies are few: no fp32 proxies). emit(t64, position, normal, material).
+template <bool MESH, class Emit>
+RTX_HD void leaf_hits(const SceneView& S, const DObj& ob, f3 o, f3 d, float time, Emit&& emit) {
+    if (ob.type == OBJ_SPHERE) {  // simple_geometry.py:20-46
+        const f3 c = moved(ob, ob.a, time);
+        double b, s, two_a;
+        if (!sphere_roots(o, d, c, ob.r2, b, s, two_a)) return;
+        const double t1 = (-b - s) / two_a, t2 = (-b + s) / two_a;
+        if (t1 > 0.0) { const f3 p = get_point(o, d, t1); emit(t1, p, normalize(sub(p, c)), ob.mat0); }
+        if (t2 > 0.0) { const f3 p = get_point(o, d, t2); emit(t2, p, normalize(sub(p, c)), ob.mat0); }
+    } else if (ob.type == OBJ_PLANE) {  // :105-120
+        const f3 n = ld3(ob.b);
+        const float den = dot(d, n);
+        if (!(fabsf(den) >= kEps4Up)) return;
+        const double t = (double)dot(sub(moved(ob, ob.a, time), o), n) / (double)den;
+        if (!(t >= 0.0)) return;
+        const f3 p = get_point(o, d, t);
+        emit(t, p, n, plane_material(ob, p, time));
+    } else if (ob.type == OBJ_BOX) {  // :188-249 (entry, then exit, both with the entry normal)
+        double start, end;
+        int label;
+        if (!box_slabs(o, d, moved(ob, ob.a, time), moved(ob, ob.b, time), start, label, end)) return;
+        if (start > end || start < 0.0) return;
+        const f3 nb = box_normal(label, d);
+        emit(start, get_point(o, d, start), nb, ob.mat0);
+        emit(end, get_point(o, d, end), nb, ob.mat0);
+    } else if (MESH && ob.type == OBJ_MESH) {  // mesh.py:72-119, faces in OBJ order
+        if (!mesh_bv(ob, o, d)) return;
+        for (int f = 0; f < ob.tri_count; ++f) {
+            const DTri T = S.tris[ob.tri_begin + f];
+            const f3 n = ld3(T.n);
+            const float den = dot(d, n);
+            if (fabsf(den) < kEps4Up) continue;
+            const f3 v0 = ld3(T.v0);
+            const double t = (double)dot(sub(v0, o), n) / (double)den;
+            if (t < 0.0) continue;
+            const f3 p = get_point(o, d, t);
+            if (dot(cross(ld3(T.e01), sub(p, v0)), n) >= 0.0f && dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n) >= 0.0f &&
+                dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n) >= 0.0f)
+                emit(t, p, ob.flat ? n : smooth_normal(T, (DTriN)S.trins[ob.tri_begin + f], p), ob.mat0);
+        }
+    }
+}
+
+// Leaf shadow_intersect (simple_geometry.py:48-72, :122-131, :251-294; mesh.py:121-153).
+template <bool MESH>
+RTX_HD bool leaf_shadow(const SceneView& S, const DObj& ob, f3 o, f3 d, double t_max, float time) {
+    if (ob.type == OBJ_SPHERE) {
+        double b, s, two_a;
+        if (!sphere_roots(o, d, moved(ob, ob.a, time), ob.r2, b, s, two_a)) return false;
+        const double t1 = (-b - s) / two_a;
+        if (1e-3 < t1 && t1 < t_max) return true;
+        const double t2 = (-b + s) / two_a;
+        return 1e-3 < t2 && t2 < t_max;
+    }
+    if (ob.type == OBJ_PLANE) {
+        const f3 n = ld3(ob.b);
+        const float den = dot(d, n);
+        if (!(fabsf(den) >= kEps4Up)) return false;  // None
+        const double t = (double)dot(sub(moved(ob, ob.a, time), o), n) / (double)den;
+        return 1e-4 < t && t < t_max;
+    }
+    if (ob.type == OBJ_BOX) {
+        double start, end;
+        int label;
+        if (!box_slabs(o, d, moved(ob, ob.a, time), moved(ob, ob.b, time), start, label, end)) return false;
+        if (start > end) return false;
+        return 1e-4 < start && start < t_max;
+    }
+    if (MESH && ob.type == OBJ_MESH) {
+        if (!mesh_bv(ob, o, d)) return false;
+        for (int f = 0; f < ob.tri_count; ++f) {
+            const DTri T = S.tris[ob.tri_begin + f];
+            const f3 n = ld3(T.nu);
+            const float den = dot(d, n);
+            if (fabsf(den) < kEps4Up) continue;
+            const f3 v0 = ld3(T.v0);
+            const double t = (double)dot(sub(v0, o), n) / (double)den;
+            if (t < 1e-4) continue;
+            const f3 p = get_point(o, d, t);
+            if (dot(cross(ld3(T.e01), sub(p, v0)), n) >= 0.0f && dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n) >= 0.0f &&
+                dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n) >= 0.0f)
+                return true;
+        }
+    }
+    return false;
+}
+
+// Leaf is_inside: Sphere (simple_geometry.py:74-80, fp32 length vs the fp64 radius),
+// AABB (:296-307); Plane and Mesh keep Geometry's False.
+RTX_HD bool leaf_inside(const DObj& ob, f3 p, float time) {
+    if (ob.type == OBJ_SPHERE) {
+        const f3 q = sub(p, moved(ob, ob.a, time));
+        return (double)sqrtf(dot(q, q)) < ob.radius;
+    }
+    if (ob.type == OBJ_BOX) {
+        const f3 mn = moved(ob, ob.a, time), mx = moved(ob, ob.b, time);
+        return mn.x < p.x && p.x < mx.x && mn.y < p.y && p.y < mx.y && mn.z < p.z && p.z < mx.z;
+    }
+    return false;
+}
+
+// Folds child `cidx`'s value v into the accumulator bit of its parent (kind pk, depth pd):
+// union = any, intersection = all, difference = child 0 and not child 1.
+RTX_HD uint32_t hfold(uint32_t acc, int32_t pk, int32_t pd, int32_t cidx, bool v) {
+    const uint32_t bit = 1u << pd;
+    const bool a = (acc & bit) != 0u;
+    const bool r = pk == HN_UNION ? (a || v) : pk == HN_INTER ? (a && v) : (cidx == 0 ? v : (cidx == 1 ? (a && !v) : a));
+    return r ? (acc | bit) : (acc & ~bit);
+}
+RTX_HD uint32_t hinit(uint32_t acc, int32_t kind, int32_t depth) {
+    const uint32_t bit = 1u << depth;
+    return kind == HN_INTER ? (acc | bit) : (acc & ~bit);
+}
+
+// is_inside(x, p) for p in the frame of x's parent's children (hierarchy.py:111-129).
+RTX_HD bool is_inside(const SceneView& S, const HStack& hs, int x, f3 p, float time) {
+    const DNode X = S.nodes[x];
+    if (X.kind == HN_LEAF) return leaf_inside(S.objs[X.obj], p, time);
+    if (X.kind == HN_OTHER) return false;
+    hs.put_pt(X.depth, xform(X.Minv, p, 1.0f));
+    uint32_t acc = hinit(0u, X.kind, X.depth);
+    int open = x;
+    int32_t okind = X.kind, odepth = X.depth, oend = X.end, oparent = X.parent, ocidx = X.cidx;
+    int i = x + 1;
+    for (;;) {
+        while (i >= oend) {  // close finished subtrees
+            const bool v = ((acc >> odepth) & 1u) != 0u;
+            if (open == x) return v;
+            const DNode Pn = S.nodes[oparent];
+            acc = hfold(acc, Pn.kind, Pn.depth, ocidx, v);
+            open = oparent;
+            okind = Pn.kind; odepth = Pn.depth; oend = Pn.end; oparent = Pn.parent; ocidx = Pn.cidx;
+        }
+        const DNode c = S.nodes[i];
+        if (okind == HN_DIFF && c.cidx >= 2) { i = c.end; continue; }
+        if (c.kind == HN_LEAF) {
+            acc = hfold(acc, okind, odepth, c.cidx, leaf_inside(S.objs[c.obj], hs.get_pt(odepth), time));
+            ++i;
+        } else if (c.kind == HN_OTHER) {
+            acc = hfold(acc, okind, odepth, c.cidx, false);
+            i = c.end;
+        } else {
+            hs.put_pt(c.depth, xform(c.Minv, hs.get_pt(odepth), 1.0f));
+            acc = hinit(acc, c.kind, c.depth);
+            open = i;
+            okind = c.kind; odepth = c.depth; oend = c.end; oparent = c.parent; ocidx = c.cidx;
+            ++i;
+        }
+    }
+}
+
+// get_material(x, p) (hierarchy.py:131-138, Plane.get_material, Geometry.get_material):
+// the first child containing the point, recursively; -1 = None.
+RTX_HD int32_t get_material(const SceneView& S, const HStack& hs, int x, f3 p, float time) {
+    for (;;) {
+        const DNode X = S.nodes[x];
+        if (X.kind == HN_LEAF) {
+            const DObj ob = S.objs[X.obj];
+            return ob.type == OBJ_PLANE ? plane_material(ob, p, time) : ob.mat0;
+        }
+        const f3 q = xform(X.Minv, p, 1.0f);
+        int found = -1;
+        for (int j = x + 1; j < X.end; j = S.nodes[j].end)
+            if (is_inside(S, hs, j, q, time)) { found = j; break; }
+        if (found < 0) return -1;
+        x = found;
+        p = q;
+    }
+}
+
+// The filters and transforms a hit of leaf `cur` meets on its way up to node `stop`
+// (inclusive): intersection keeps hits inside every sibling, difference keeps child-0
+// hits outside child 1 and child-1 hits inside child 0 (material of child 0, normal
+// negated), then None materials fall back to the node's and position/normal move to the
+// parent frame (hierarchy.py:49-76). Returns false if a filter drops the hit.
+RTX_HD bool walk_up(const SceneView& S, const HStack& hs, int cur, int stop, float time, f3& pos, f3& n,
+                    int32_t& mat) {
+    while (cur != stop) {
+        const DNode c = S.nodes[cur];
+        const int a = c.parent;
+        const DNode A = S.nodes[a];
+        if (A.kind == HN_INTER) {
+            for (int j = a + 1; j < A.end; j = S.nodes[j].end)
+                if (j != cur && !is_inside(S, hs, j, pos, time)) return false;
+        } else if (A.kind == HN_DIFF) {
+            const int c0 = a + 1, c1 = S.nodes[c0].end;
+            if (c.cidx == 0) {
+                if (is_inside(S, hs, c1, pos, time)) return false;
+            } else {
+                if (!is_inside(S, hs, c0, pos, time)) return false;
+                mat = get_material(S, hs, c0, pos, time);
+                n = neg(n);
+            }
+        }
+        if (mat < 0) mat = A.mat0 < 0 ? 0 : A.mat0;  // the reference raises IndexError for A.mat0 < 0
+        pos = xform(A.M, pos, 1.0f);
+        n = normal_xform(A.Minv, n);
+        cur = a;
+    }
+    return true;
+}
+
+// Enumerates s.intersect(R[depth(s)]) in the reference's list order: want(t64) is asked
+// before a hit's filters run (t does not change on the way up), take(t64, position,
+// normal, material, leaf DObj) receives every surviving hit in the frame of s's parent.
+template <bool MESH, class Want, class Take>
+RTX_HD void hier_enum(const SceneView& S, const HStack& hs, int s, float time, Want& want, Take& take) {
+    const DNode root = S.nodes[s];
+    auto visit_leaf = [&](int li, int32_t depth, int32_t obj) {
+        f3 lo, ld;
+        hs.get_ray(depth, lo, ld);
+        const DObj ob = S.objs[obj];
+        leaf_hits<MESH>(S, ob, lo, ld, time, [&](double t, f3 pos, f3 n, int32_t mat) {
+            if (!want(t)) return;
+            if (walk_up(S, hs, li, s, time, pos, n, mat)) take(t, pos, n, mat, obj);
+        });
+    };
+    if (root.kind == HN_LEAF) { visit_leaf(s, root.depth, root.obj); return; }
+    if (root.kind == HN_OTHER) return;  // unknown hierarchy_type: no hits
+    {
+        f3 ro, rd;
+        hs.get_ray(root.depth, ro, rd);
+        hs.put_ray(root.depth + 1, xform(root.Minv, ro, 1.0f), xform(root.Minv, rd, 0.0f));
+    }
+    for (int i = s + 1; i < root.end;) {
+        const DNode c = S.nodes[i];
+        if (c.pkind == HN_DIFF && c.cidx >= 2) { i = c.end; continue; }  // difference reads children 0, 1
+        if (c.kind == HN_LEAF) { visit_leaf(i, c.depth, c.obj); ++i; continue; }
+        if (c.kind == HN_OTHER) { i = c.end; continue; }
+        f3 ro, rd;
+        hs.get_ray(c.depth, ro, rd);
+        hs.put_ray(c.depth + 1, xform(c.Minv, ro, 1.0f), xform(c.Minv, rd, 0.0f));
+        ++i;
+    }
+}
+
+// Difference.shadow_intersect (hierarchy.py:95-107): every hit of child 0 / child 1 past
+// the shadow epsilon that the other child does not veto; no t_max test.
+template <bool MESH>
+RTX_HD bool diff_shadow(const SceneView& S, const HStack& hs, int x, float time) {
+    const DNode X = S.nodes[x];
+    {
+        f3 ro, rd;
+        hs.get_ray(X.depth, ro, rd);
+        hs.put_ray(X.depth + 1, xform(X.Minv, ro, 1.0f), xform(X.Minv, rd, 0.0f));
+    }
+    const int c0 = x + 1, c1 = S.nodes[c0].end;
+    bool found = false;
+    auto want = [&](double t) { return !found && t > 1e-4; };
+    auto take0 = [&](double, f3 pos, f3, int32_t, int32_t) { found = !is_inside(S, hs, c1, pos, time); };
+    hier_enum<MESH>(S, hs, c0, time, want, take0);
+    auto take1 = [&](double, f3 pos, f3, int32_t, int32_t) { found = is_inside(S, hs, c0, pos, time); };
+    hier_enum<MESH>(S, hs, c1, time, want, take1);
+    return found;
+}
+
+// Hierarchy.shadow_intersect of root r for the world ray (o, d): union = any child,
+// intersection = every child (each tested on its own), difference = diff_shadow.
+template <bool MESH>
+RTX_HD bool hier_shadow(const SceneView& S, const HStack& hs, int r, f3 o, f3 d, double t_max, float time) {
+    hs.put_ray(0, o, d);
+    const DNode R = S.nodes[r];
+    if (R.kind == HN_OTHER) return false;
+    if (R.kind == HN_DIFF) return diff_shadow<MESH>(S, hs, r, time);
+    hs.put_ray(1, xform(R.Minv, o, 1.0f), xform(R.Minv, d, 0.0f));
+    uint32_t acc = hinit(0u, R.kind, 0);
+    int open = r;
+    int32_t okind = R.kind, odepth = R.depth, oend = R.end, oparent = R.parent, ocidx = R.cidx;
+    int i = r + 1;
+    for (;;) {
+        while (i >= oend) {
+            const bool v = ((acc >> odepth) & 1u) != 0u;
+            if (open == r) return v;
+            const DNode Pn = S.nodes[oparent];
+            acc = hfold(acc, Pn.kind, Pn.depth, ocidx, v);
+            open = oparent;
+            okind = Pn.kind; odepth = Pn.depth; oend = Pn.end; oparent = Pn.parent; ocidx = Pn.cidx;
+        }
+        const DNode c = S.nodes[i];
+        if (c.kind == HN_LEAF) {
+            f3 lo, ld;
+            hs.get_ray(c.depth, lo, ld);
+            acc = hfold(acc, okind, odepth, c.cidx, leaf_shadow<MESH>(S, S.objs[c.obj], lo, ld, t_max, time));
+            ++i;
+        } else if (c.kind == HN_OTHER) {
+            acc = hfold(acc, okind, odepth, c.cidx, false);
+            i = c.end;
+        } else if (c.kind == HN_DIFF) {
+            acc = hfold(acc, okind, odepth, c.cidx, diff_shadow<MESH>(S, hs, i, time));
+            i = c.end;
+        } else {
+            f3 ro, rd;
+            hs.get_ray(c.depth, ro, rd);
+            hs.put_ray(c.depth + 1, xform(c.Minv, ro, 1.0f), xform(c.Minv, rd, 0.0f));
+            acc = hinit(acc, c.kind, c.depth);
+            open = i;
+            okind = c.kind; odepth = c.depth; oend = c.end; oparent = c.parent; ocidx = c.cidx;
+            ++i;
+        }
+    }
+}
+
+// Best hierarchy hit: the surface the walk-up produced (world frame).
+constexpr int32_t kHierHit = -2;  // Hit.obj of a hierarchy hit; Hit.sub then holds the root's oid
+struct HHit {
+    double t64;
+    f3 pos, n;
+    int32_t mat, gobj;  // gobj: the leaf DObj (Plane/AABB get_diffuse), -1 otherwise
+};
+
+// Closest hit over the hierarchies, merged into h (flat objects done): a candidate wins
+// with a smaller t, or an equal t and an earlier top-level object (scene.py:94).
+template <bool MESH>
+RTX_HD void hier_closest(const SceneView& S, const HStack& hs, f3 o, f3 d, float time, Hit& h, HHit& hh) {
+    hs.put_ray(0, o, d);
+    for (int r = 0; r < S.n_nodes; r = S.nodes[r].end) {
+        const int32_t oid = S.nodes[r].oid;
+        auto want = [&](double t) {
+            const float t32 = (float)t;
+            if (t32 < h.t32) return true;
+            if (!(t32 == h.t32)) return false;
+            if (h.obj == -1) return t < INFINITY;
+            double bt;
+            int32_t bo;
+            if (h.obj == kHierHit) { bt = hh.t64; bo = h.sub; }
+            else { bt = hit_t64(S, h.obj, h.sub, o, d, time); bo = S.objs[h.obj].oid; }
+            return t < bt || (t == bt && oid < bo);
+        };
+        auto take = [&](double t, f3 pos, f3 n, int32_t mat, int32_t leaf) {
+            const int32_t ty = S.objs[leaf].type;
+            h.t32 = (float)t;
+            h.obj = kHierHit;
+            h.sub = oid;
+            hh = HHit{t, pos, n, mat, (ty == OBJ_PLANE || ty == OBJ_BOX) ? leaf : -1};
+        };
+        hier_enum<MESH>(S, hs, r, time, want, take);
+    }
+}
+
 // ------------------------------------------------------------------ closest hit
-template <bool MESH, bool COUNT>
-RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl) {
+template <bool MESH, bool X, bool COUNT>
+RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const HStack& hs, HHit& hh) {
     Hit h{INFINITY, -1, 0};
     int oi = 0;
     for (int k = 0; k < S.n_plane; ++k, ++oi) {  // simple_geometry.py:105-120
@@ -470,14 +984,15 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl) {
             }
         }
     }
+    if (X) hier_closest<MESH>(S, hs, o, d, time, h, hh);  // hierarchies (hierarchy.py:42-78)
     return h;
 }
 
 // ------------------------------------------------------------------ shadow any-hit
 // Any order gives the same answer; cheap objects first, and the wave leaves as soon as
 // every active lane is occluded.
-template <bool MESH, bool COUNT>
-RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, Tally& tl) {
+template <bool MESH, bool X, bool COUNT>
+RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, Tally& tl, const HStack& hs) {
     const float tmax32 = (float)t_max;
     bool occ = false;
     int oi = 0;
@@ -548,56 +1063,33 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
             }
         }
     }
+    if (X) {  // hierarchies (hierarchy.py:80-109)
+        for (int r = 0; r < S.n_nodes; r = S.nodes[r].end) {
+            if (RTX_ALL(occ)) break;
+            if (!occ) occ = hier_shadow<MESH>(S, hs, r, o, d, t_max, time);
+        }
+    }
     return occ;
-}
-
-// ------------------------------------------------------------------ hit record
-// math.floor(a - b) of two floats, where the reference subtracts in fp64 (exactly). The
-// fp32 difference d = fl32(a - b) lies in [k, k + 1] when floor(a - b) = k (k and k + 1
-// are floats below 2^23), so floorf(d) is exact unless d is an integer: then use fp64.
-RTX_HD int32_t floor_diff(float a, float b) {
-    const float d = a - b;
-    const float f = floorf(d);
-    if (fabsf(d) < 0x1p23f && d != f) return (int32_t)f;
-    return (int32_t)(int64_t)floor((double)a - (double)b);
-}
-
-// Plane.get_material (simple_geometry.py:133-148): checker by floor of the projected
-// coordinates, Python modulo.
-RTX_HD int32_t plane_material(const DObj& ob, f3 point, float time) {
-    if (ob.nmat == 1) return ob.mat0;
-    f3 position = moved(ob, ob.a, time);
-    f3 n = ld3(ob.b);
-    point = sub(point, scale(n, dot(sub(point, position), n)));
-    float x = dot(sub(point, position), ld3(ob.c));
-    float z = dot(sub(point, position), ld3(ob.e));
-    const int32_t s = floor_diff(position.x, x) + floor_diff(position.z, z);
-    return (s & 1) ? ob.mat1 : ob.mat0;  // (dx + dz) % 2 with Python modulo
-}
-
-// Barycentric smooth normal (mesh.py:103-113; igl.barycentric_coordinates_tri on fp32 rows).
-RTX_HD f3 smooth_normal(const DTri& T, const DTriN& N, f3 p) {
-    f3 a = ld3(T.v0), b = ld3(T.v1), c = ld3(T.v2);
-    f3 v0 = sub(b, a), v1 = sub(c, a), v2 = sub(p, a);
-    float d00 = dot(v0, v0), d01 = dot(v0, v1), d11 = dot(v1, v1);
-    float d20 = dot(v2, v0), d21 = dot(v2, v1);
-    float den = d00 * d11 - d01 * d01;
-    float v = (d11 * d20 - d01 * d21) / den;
-    float w = (d00 * d21 - d01 * d20) / den;
-    float u = (1.0f - v) - w;
-    f3 n = add(add(scale(ld3(N.n0), u), scale(ld3(N.n1), v)), scale(ld3(N.n2), w));
-    return normalize(n);
 }
 
 struct Surface {
     f3 position, normal;
     int32_t mat;
+    int32_t gobj;  // DObj whose get_diffuse shades the hit (textured or hierarchy Plane/AABB), or -1
 };
 
-template <bool MESH>
-RTX_HD Surface resolve_hit(const SceneView& S, const Hit& h, f3 o, f3 d, float time) {
+template <bool MESH, bool X>
+RTX_HD Surface resolve_hit(const SceneView& S, const Hit& h, const HHit& hh, f3 o, f3 d, float time) {
     Surface sf;
+    if (X && h.obj == kHierHit) {
+        sf.position = hh.pos;
+        sf.normal = hh.n;
+        sf.mat = hh.mat;
+        sf.gobj = hh.gobj;
+        return sf;
+    }
     const DObj ob = S.objs[h.obj];
+    sf.gobj = (X && ob.has_tex) ? h.obj : -1;
     sf.position = add(o, scale(d, h.t32));  // getPoint(t): fl32(t64) == t32
     sf.mat = ob.mat0;
     const int32_t type = ob.type;
@@ -607,10 +1099,7 @@ RTX_HD Surface resolve_hit(const SceneView& S, const Hit& h, f3 o, f3 d, float t
         sf.normal = ld3(ob.b);
         sf.mat = plane_material(ob, sf.position, time);
     } else if (type == OBJ_BOX) {
-        // simple_geometry.py:231-242: entry-slab label and the direction's sign
-        const float dl = h.sub == 0 ? d.x : (h.sub == 1 ? d.y : d.z);
-        float sgn = dl < 0.0f ? 1.0f : (dl > 0.0f ? -1.0f : 0.0f);
-        sf.normal = f3{h.sub == 0 ? sgn : 0.0f, h.sub == 1 ? sgn : 0.0f, h.sub == 2 ? sgn : 0.0f};
+        sf.normal = box_normal(h.sub, d);  // entry-slab label and the direction's sign
     } else if (MESH) {
         const DTri T = S.tris[ob.tri_begin + h.sub];
         if (ob.flat)
@@ -652,10 +1141,10 @@ RTX_HD double spec_pow(double x, const DMat& m, int pow_bits) {
 }
 
 // _compute_regular_lighting (scene.py:140-187)
-template <bool MESH, bool COUNT>
-RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const DMat& m, float time, Tally& tl) {
+template <bool MESH, bool X, bool COUNT>
+RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const DMat& m, f3 diffuse, float time,
+                           Tally& tl, const HStack& hs) {
     f3 colour = mk(0.0f, 0.0f, 0.0f);
-    const f3 diffuse = ld3(m.diffuse);
     tally_inc<COUNT>(tl, &Tally::shade);
     for (int li = 0; li < S.n_lights; ++li) {
         const DLight L = S.lights[li];
@@ -669,7 +1158,7 @@ RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const 
             t_max = INFINITY;
         }
         tally_inc<COUNT>(tl, &Tally::shadow);
-        if (RTX_ABLATE != 1 && occluded<MESH, COUNT>(S, pos, sdir, t_max, time, tl)) continue;
+        if (RTX_ABLATE != 1 && occluded<MESH, X, COUNT>(S, pos, sdir, t_max, time, tl, hs)) continue;
         if (RTX_ABLATE == 3) { colour = add(colour, mul(ld3(L.cp), diffuse)); continue; }
         f3 light_dir = L.type == LIGHT_POINT ? normalize(sdir) : ld3(L.ndir);
         f3 lambert = scale(diffuse, pos_part(dot(normal, light_dir)));
@@ -712,17 +1201,18 @@ struct FrameStack {
     }
 };
 
-template <bool MESH, bool SEC, bool COUNT>
-RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const FrameStack& fs) {
+template <bool MESH, bool SEC, bool X, bool COUNT>
+RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const FrameStack& fs, const HStack& hs) {
     int nfr = 0;
     f3 tail = mk(0.0f, 0.0f, 0.0f);
     bool in_shape = false;
     for (int level = 0; level < (SEC ? kMaxDepth : 1); ++level) {
         if (COUNT) tl.cast[level]++;
         if (RTX_ABLATE == 8) { tail = d; break; }  // cost probe: camera + store only
-        const Hit h = closest_hit<MESH, COUNT>(S, o, d, time, tl);
-        if (h.obj < 0) break;  // miss -> black
-        const Surface sf = resolve_hit<MESH>(S, h, o, d, time);
+        HHit hh;
+        const Hit h = closest_hit<MESH, X, COUNT>(S, o, d, time, tl, hs, hh);
+        if (h.obj == -1) break;  // miss -> black
+        const Surface sf = resolve_hit<MESH, X>(S, h, hh, o, d, time);
         const DMat m = S.mats[sf.mat];
         f3 n = sf.normal;
         bool chain = false, tir = false;
@@ -742,7 +1232,9 @@ RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const 
             chain = true;
         }
         if ((RTX_ABLATE == 2 || RTX_ABLATE == 7) && !chain) { tail = ld3(m.diffuse); break; }
-        const f3 L = regular_lighting<MESH, COUNT>(S, d, sf.position, n, m, time, tl);
+        // scene.py:143-146: Plane/AABB hits shade with get_diffuse(position)
+        const f3 diffuse = (X && sf.gobj >= 0) ? get_diffuse(S, S.objs[sf.gobj], sf.position, time) : ld3(m.diffuse);
+        const f3 L = regular_lighting<MESH, X, COUNT>(S, d, sf.position, n, m, diffuse, time, tl, hs);
         if (!SEC || !chain) {
             tail = clamp01(L);
             break;

@@ -15,10 +15,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_lib", "librtx.so")
 # Experiment builds (tools/ablate.sh) point this at another build of the same HIP source.
 LIB_PATH = os.environ.get("RTX_LIB_OVERRIDE", LIB_PATH)
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 RTX_OK, RTX_ERR_INVALID, RTX_ERR_HIP, RTX_ERR_UNSUPPORTED, RTX_ERR_STATE = 0, -1, -2, -3, -4
-RTX_SPHERE, RTX_PLANE, RTX_BOX, RTX_MESH = 0, 1, 2, 3
+RTX_SPHERE, RTX_PLANE, RTX_BOX, RTX_MESH, RTX_NODE = 0, 1, 2, 3, 4
+RTX_UNION, RTX_INTERSECTION, RTX_DIFFERENCE, RTX_HIER_OTHER = 0, 1, 2, 3
 RTX_MAT_DIFFUSE, RTX_MAT_MIRROR, RTX_MAT_REFRACTIVE = 0, 1, 2
 RTX_LIGHT_POINT, RTX_LIGHT_DIRECTIONAL = 0, 1
 RTX_BV_AABB, RTX_BV_SPHERE = 0, 1
@@ -34,7 +35,12 @@ class rtx_object(C.Structure):
                 ("has_speed", C.c_int32), ("speed", _f3), ("a", _f3), ("b", _f3),
                 ("radius", C.c_double), ("tri_begin", C.c_int32), ("tri_count", C.c_int32),
                 ("bv_type", C.c_int32), ("flat", C.c_int32), ("bv_a", _f3), ("bv_b", _f3),
-                ("bv_radius", C.c_double)]
+                ("bv_radius", C.c_double), ("parent", C.c_int32), ("hierarchy_type", C.c_int32),
+                ("trs", C.c_float * 9), ("texture", C.c_int32), ("texture_scale", C.c_double)]
+
+
+class rtx_texture(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("rgb", C.POINTER(C.c_uint8))]
 
 
 class rtx_triangle(C.Structure):
@@ -55,7 +61,7 @@ class rtx_scene_desc(C.Structure):
                 ("n_materials", C.c_int32), ("materials", C.POINTER(rtx_material)),
                 ("n_lights", C.c_int32), ("lights", C.POINTER(rtx_light)),
                 ("n_triangles", C.c_int32), ("triangles", C.POINTER(rtx_triangle)),
-                ("ambient", _f3)]
+                ("ambient", _f3), ("n_textures", C.c_int32), ("textures", C.POINTER(rtx_texture))]
 
 
 _pf = C.POINTER(C.c_float)

@@ -44,13 +44,15 @@ class Sphere(Geometry):
 
 
 class Plane(Geometry):
-    """simple_geometry.py:86-176 (textures: not built yet)."""
+    """simple_geometry.py:86-176. ``texture`` is the PIL image the parser opened
+    (scene_parser.py:222-229); ``texture_scale`` defaults to 1.0 (simple_geometry.py:157-160)."""
 
     def __init__(self, name, gtype, materials, point, normal, speed):
         super().__init__(name, gtype, materials, speed)
         self.point = F.vec3(point)
         self.normal = F.vec3(normal)
         self.texture = None
+        self.texture_scale = 1.0
 
 
 class AABB(Geometry):
@@ -151,3 +153,54 @@ def resolve_path(path, base_dir):
         return path
     alt = os.path.join(base_dir, path)
     return alt if os.path.exists(alt) else path
+
+
+class Hierarchy(Geometry):
+    """hierarchy.py:11-146: a CSG node (union / intersection / difference) with a
+    translate-rotate-scale transform. The matrices are built on the device side of the
+    ABI from (t, r, s) exactly as make_matrices does (hierarchy.py:30-40)."""
+
+    def __init__(self, name, gtype, materials, hierarchy_type, t, r, s, speed):
+        super().__init__(name, gtype, materials, speed)
+        self.hierarchy_type = hierarchy_type
+        self.children = []
+        self.make_matrices(t, r, s)
+
+    def make_matrices(self, t, r, s):
+        self.t = F.vec3(t)
+        self.r = F.vec3(r)
+        self.s = F.vec3(s)
+
+    def set_fallback_material(self, materials):
+        """hierarchy.py:21-28: leaves get the root's materials appended (nested nodes pass them on)."""
+        if len(materials) == 0:
+            return
+        for child in self.children:
+            if isinstance(child, Hierarchy):
+                child.set_fallback_material(materials)
+            else:
+                child.materials += materials
+
+    def set_scene(self, scene):
+        self.scene = scene
+        for child in self.children:
+            child.set_scene(scene)
+
+    def __repr__(self):
+        return "Hierarchy(%s, t: %s, r: %s, s: %s, children: %d)" % (self.name, self.t, self.r, self.s,
+                                                                      len(self.children))
+
+
+def open_texture(path, base_dir=None):
+    """Image.open(texture) (scene_parser.py:224) as the RGB8 array getpixel((i, j))[:3]
+    reads; modes whose getpixel is not an RGB-indexable tuple raise like the reference."""
+    from PIL import Image
+    im = Image.open(resolve_path(path, base_dir))
+    if im.mode not in ("RGB", "RGBA", "RGBX", "CMYK", "RGBa", "YCbCr", "LAB", "HSV"):
+        raise TypeError("texture %s: getpixel of mode %s is not indexable as RGB" % (path, im.mode))
+    return im
+
+
+def texture_rgb8(im):
+    """getpixel((i, j))[:3] for every texel: uint8 [height, width, 3]."""
+    return np.ascontiguousarray(np.asarray(im)[:, :, :3], dtype=np.uint8)

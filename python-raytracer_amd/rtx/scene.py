@@ -19,6 +19,7 @@ from . import geometry as geom
 from .helperclasses import sunflower
 
 _MAT_CODE = {"diffuse": N.RTX_MAT_DIFFUSE, "mirror": N.RTX_MAT_MIRROR, "refractive": N.RTX_MAT_REFRACTIVE}
+_HIER_CODE = {"union": N.RTX_UNION, "intersection": N.RTX_INTERSECTION, "difference": N.RTX_DIFFERENCE}
 
 DEFAULT_SEED = 0x5EED
 
@@ -86,31 +87,69 @@ class Scene:
         mats = list(self.materials)
         index = {id(m): i for i, m in enumerate(mats)}
 
+        def value(m):
+            return (m.ID, m.name, m.mat_type, tuple(F.vec3(m.diffuse)), tuple(F.vec3(m.specular)), float(m.hardness),
+                    float(m.tint), float(m.refr_index))
+        by_value = {}
+        for i, m in enumerate(mats):
+            by_value.setdefault(value(m), i)
+
         def mat_index(m):
+            # a `ref` node's deep copy carries copies of the scene materials: same values,
+            # same slot
             if id(m) not in index:
-                index[id(m)] = len(mats)
-                mats.append(m)
+                v = value(m)
+                if v not in by_value:
+                    by_value[v] = len(mats)
+                    mats.append(m)
+                index[id(m)] = by_value[v]
             return index[id(m)]
 
-        objs = (N.rtx_object * max(1, len(self.objects)))()
+        # Records in preorder: top-level objects in scene order, each hierarchy followed by
+        # its subtree (rtx.h: parent indices, children in child order).
+        records = []
+
+        def walk(g, parent):
+            records.append((g, parent))
+            if isinstance(g, geom.Hierarchy):
+                me = len(records) - 1
+                for c in g.children:
+                    walk(c, me)
+        for g in self.objects:
+            walk(g, -1)
+        objs = (N.rtx_object * max(1, len(records)))()
         tris = []
-        for i, g in enumerate(self.objects):
+        textures, tex_index = [], {}
+
+        def texture_index(im):
+            if id(im) not in tex_index:
+                tex_index[id(im)] = len(textures)
+                textures.append(geom.texture_rgb8(im))
+            return tex_index[id(im)]
+        for i, (g, parent) in enumerate(records):
             o = objs[i]
+            o.parent = parent
+            o.texture = -1
+            o.texture_scale = 1.0
             o.n_mats = len(g.materials)
             for k, m in enumerate(g.materials[:2]):
                 o.mat[k] = mat_index(m)
             o.has_speed = 0 if g.speed is None else 1
             o.speed = N.f3(g.speed if g.speed is not None else (0, 0, 0))
-            if isinstance(g, geom.Sphere):
+            if isinstance(g, geom.Hierarchy):
+                o.type = N.RTX_NODE
+                o.hierarchy_type = _HIER_CODE.get(g.hierarchy_type, N.RTX_HIER_OTHER)
+                o.trs[:] = [float(x) for x in np.concatenate([g.t, g.r, g.s]).astype(np.float32)]
+            elif isinstance(g, geom.Sphere):
                 o.type, o.a, o.radius = N.RTX_SPHERE, N.f3(g.center), float(g.radius)
             elif isinstance(g, geom.Plane):
-                if g.texture is not None:
-                    raise NotImplementedError("plane textures (SURVEY.md §8f row 2)")
                 o.type, o.a, o.b = N.RTX_PLANE, N.f3(g.point), N.f3(g.normal)
-            elif isinstance(g, geom.AABB):
                 if g.texture is not None:
-                    raise NotImplementedError("box textures (SURVEY.md §8f row 2)")
+                    o.texture, o.texture_scale = texture_index(g.texture), float(g.texture_scale)
+            elif isinstance(g, geom.AABB):
                 o.type, o.a, o.b = N.RTX_BOX, N.f3(g.minpos), N.f3(g.maxpos)
+                if g.texture is not None:
+                    o.texture = texture_index(g.texture)
             elif isinstance(g, geom.Mesh):
                 o.type = N.RTX_MESH
                 o.tri_begin = sum(len(t) for t in tris)
@@ -124,6 +163,9 @@ class Scene:
                     o.bv_type, o.bv_a, o.bv_radius = N.RTX_BV_SPHERE, N.f3(g.bv_center), float(g.bv_radius)
             else:
                 raise NotImplementedError("unsupported geometry %r" % (g,))
+            if not isinstance(g, geom.Hierarchy) and not g.materials:
+                raise IndexError("%r has no material: the reference raises IndexError (list index out of "
+                                 "range) when it is hit" % (g,))
         cm = (N.rtx_material * max(1, len(mats)))()
         for i, m in enumerate(mats):
             cm[i].diffuse, cm[i].specular = N.f3(m.diffuse), N.f3(m.specular)
@@ -136,13 +178,18 @@ class Scene:
             cl[i].colour, cl[i].vector, cl[i].power = N.f3(L.colour), N.f3(L.vector), float(L.power)
         tri = np.ascontiguousarray(np.concatenate(tris).astype(np.float32)) if tris else np.zeros((1, 6, 3), np.float32)
         desc = N.rtx_scene_desc()
-        desc.n_objects, desc.objects = len(self.objects), objs
+        desc.n_objects, desc.objects = len(records), objs
         desc.n_materials, desc.materials = len(mats), cm
         desc.n_lights, desc.lights = len(self.lights), cl
         desc.n_triangles = sum(len(t) for t in tris)
         desc.triangles = tri.ctypes.data_as(C.POINTER(N.rtx_triangle))
         desc.ambient = N.f3(self.ambient)
-        desc._keep = (objs, cm, cl, tri)
+        ct = (N.rtx_texture * max(1, len(textures)))()
+        for i, t in enumerate(textures):
+            ct[i].height, ct[i].width = t.shape[0], t.shape[1]
+            ct[i].rgb = t.ctypes.data_as(C.POINTER(C.c_uint8))
+        desc.n_textures, desc.textures = len(textures), ct
+        desc._keep = (objs, cm, cl, tri, ct, textures)
         return desc
 
     def native(self):

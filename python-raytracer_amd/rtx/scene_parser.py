@@ -7,8 +7,12 @@ Defaults (scene_parser.py:62-142): resolution [1080, 720], ambient [0,0,0], AA
 {time: 0, samples: 1, final: 0}, material {type: diffuse, diffuse/specular: [0,0,0],
 hardness: 32, tint: 0.0, refr_index: 1.0}; directional lights get power 1.0; a KeyError
 inside the light list drops every light; unknown light/object types are skipped with a
-message. ``load_scene`` also accepts an already-parsed dict (used by the bench and tests).
+message. Hierarchy nodes (scene_parser.py:177-205, :261-285) become ``geometry.Hierarchy``
+trees, `ref` nodes deep-copy an earlier root, and every top-level hierarchy passes its
+materials to its leaves (hierarchy.py:21-28). Textures are opened with PIL like the
+reference. ``load_scene`` also accepts an already-parsed dict (used by the bench and tests).
 """
+import copy
 import json
 import os
 
@@ -140,8 +144,14 @@ def load_scene(infile, verbose=True):
         materials.append(m)
 
     objects = []
+    rootNames = []   # hierarchies other nodes may reference (scene_parser.py:147-149)
+    roots = []
     for geometry in data["objects"]:
-        parse_geometry(geometry, objects, materials, base_dir, log)
+        parse_geometry(geometry, objects, rootNames, roots, materials, base_dir, log)
+
+    for obj in objects:
+        if isinstance(obj, geom.Hierarchy):
+            obj.set_fallback_material(obj.materials)
 
     log("Parsing complete")
     sc = Scene(vc, jitter, samples, ambient, lights, materials, objects)
@@ -150,8 +160,9 @@ def load_scene(infile, verbose=True):
     return sc
 
 
-def parse_geometry(geometry, objects, materials, base_dir=None, log=print):
-    """scene_parser.py:166-209 (hierarchy nodes: SURVEY.md §8f row 1, not built yet)."""
+def parse_geometry(geometry, objects, rootNames, roots, materials, base_dir=None, log=print):
+    """scene_parser.py:166-209: basic shapes, hierarchy roots, and nodes that deep-copy an
+    earlier root (`ref`) with their own materials and transform."""
     g_name = geometry["name"]
     g_type = geometry["type"]
     g_pos = populateVec(get_or(geometry, "position", [0, 0, 0]))
@@ -160,13 +171,32 @@ def parse_geometry(geometry, objects, materials, base_dir=None, log=print):
     if add_basic_shape(g_name, g_type, g_pos, g_speed, g_mats, geometry, objects, base_dir):
         return
     if g_type == "node":
-        raise NotImplementedError("hierarchy nodes (%r) are not supported by the GPU path yet "
-                                  "(SURVEY.md §8f row 1)" % g_name)
+        g_ref = get_or(geometry, "ref", "")
+        g_r = populateVec(get_or(geometry, "rotation", [0, 0, 0]))
+        g_s = populateVec(get_or(geometry, "scale", [1, 1, 1]))
+        g_hierarchy_type = get_or(geometry, "hierarchy_type", "union")
+        if g_ref == "":
+            rootNames.append(g_name)
+            node = geom.Hierarchy(g_name, g_type, g_mats, g_hierarchy_type, g_pos, g_r, g_s, g_speed)
+            traverse_children(node, geometry["children"], materials, rootNames, roots, g_speed, base_dir, log)
+            roots.append(node)
+            objects.append(node)
+        else:
+            rid = rootNames.index(g_ref) if g_ref in rootNames else -1
+            if rid != -1:
+                node = copy.deepcopy(roots[rid])
+                node.name = g_name
+                node.materials = g_mats
+                node.make_matrices(g_pos, g_r, g_s)
+                objects.append(node)
+            else:
+                log("Node reference", g_ref, "not found, skipping creation")
+        return
     log("Unkown object type", g_type, ", skipping initialization")
 
 
 def add_basic_shape(g_name, g_type, g_pos, g_speed, g_mats, geometry, objects, base_dir=None):
-    """scene_parser.py:212-258."""
+    """scene_parser.py:212-258 (textures: Image.open of the path, scale default 1.0)."""
     if g_type == "sphere":
         g_radius = geometry["radius"]
         objects.append(geom.Sphere(g_name, g_type, g_mats, g_pos, g_radius, g_speed))
@@ -174,7 +204,8 @@ def add_basic_shape(g_name, g_type, g_pos, g_speed, g_mats, geometry, objects, b
         g_normal = populateVec(geometry["normal"])
         plane = geom.Plane(g_name, g_type, g_mats, g_pos, g_normal, g_speed)
         if "texture" in geometry:
-            raise NotImplementedError("plane textures are not supported by the GPU path yet (SURVEY.md §8f row 2)")
+            plane.texture = geom.open_texture(geometry["texture"], base_dir)
+            plane.texture_scale = get_or(geometry, "texture_scale", 1.0)
         objects.append(plane)
     elif g_type == "box":
         try:
@@ -185,7 +216,7 @@ def add_basic_shape(g_name, g_type, g_pos, g_speed, g_mats, geometry, objects, b
             box.minpos = geom.F.vec3(populateVec(geometry["min"]))
             box.maxpos = geom.F.vec3(populateVec(geometry["max"]))
         if "texture" in geometry:
-            raise NotImplementedError("box textures are not supported by the GPU path yet (SURVEY.md §8f row 2)")
+            box.texture = geom.open_texture(geometry["texture"], base_dir)
         objects.append(box)
     elif g_type == "mesh":
         g_path = geom.resolve_path(geometry["filepath"], base_dir)
@@ -195,6 +226,31 @@ def add_basic_shape(g_name, g_type, g_pos, g_speed, g_mats, geometry, objects, b
     else:
         return False
     return True
+
+
+def traverse_children(node, children, materials, rootNames, roots, speed, base_dir=None, log=print):
+    """scene_parser.py:261-285: a child's speed is the root's speed plus its own (fp32);
+    nested nodes pass the ROOT's speed on to their own children (:283)."""
+    for geometry in children:
+        g_name = geometry["name"]
+        g_type = geometry["type"]
+        g_pos = populateVec(get_or(geometry, "position", [0, 0, 0]))
+        g_mats = associate_material(materials, get_or(geometry, "materials", []))
+        if speed is None:
+            g_speed = None
+        else:
+            g_speed = geom.F.vec3(speed) + geom.F.vec3(populateVec(get_or(geometry, "speed", [0, 0, 0])))
+        if add_basic_shape(g_name, g_type, g_pos, g_speed, g_mats, geometry, node.children, base_dir):
+            continue
+        elif g_type == "node":
+            g_r = populateVec(get_or(geometry, "rotation", [0, 0, 0]))
+            g_s = populateVec(get_or(geometry, "scale", [1, 1, 1]))
+            g_hierarchy_type = get_or(geometry, "hierarchy_type", "union")
+            inner = geom.Hierarchy(g_name, g_type, g_mats, g_hierarchy_type, g_pos, g_r, g_s, g_speed)
+            node.children.append(inner)
+            traverse_children(inner, geometry["children"], materials, rootNames, roots, speed, base_dir, log)
+        else:
+            parse_geometry(geometry, node.children, rootNames, roots, materials, base_dir, log)
 
 
 def associate_material(mats, ids):

@@ -20,6 +20,33 @@ void bind_view(const HostScene& H, SceneView& v) {
     v.n_plane = H.n_plane; v.n_sphere = H.n_sphere; v.n_box = H.n_box; v.n_mesh = H.n_mesh;
     v.pow_bits = H.pow_bits;
     std::memcpy(v.ambient, H.ambient, sizeof(v.ambient));
+    v.nodes = (cptr<DNode>)H.nodes.data();
+    v.texels = (cptr<uint32_t>)H.texels.data();
+    v.lut255 = (cptr<float>)H.lut255.data();
+    v.n_nodes = (int32_t)H.nodes.size();
+    v.hlevels = H.hlevels;
+}
+
+// Dispatch over the kernel template flags, as rtx_render's launch switch does.
+template <bool MESH, bool SEC, bool X>
+void pixel_jit(const KParams& k, float* fb, int32_t row0, int32_t rr, int32_t cc, Tally& tl, const FrameStack& fs,
+               const HStack& hs, bool jit) {
+    if (jit) render_pixel<MESH, SEC, X, true, true>(k, fb, row0, rr, cc, tl, fs, hs);
+    else render_pixel<MESH, SEC, X, true, false>(k, fb, row0, rr, cc, tl, fs, hs);
+}
+void pixel_any(const HostScene& H, const KParams& k, float* fb, int32_t row0, int32_t rr, int32_t cc, Tally& tl,
+               const FrameStack& fs, const HStack& hs, bool jit) {
+    const int sel = (H.has_mesh ? 4 : 0) | (H.has_secondary ? 2 : 0) | (H.has_ext ? 1 : 0);
+    switch (sel) {
+        case 0: pixel_jit<false, false, false>(k, fb, row0, rr, cc, tl, fs, hs, jit); break;
+        case 1: pixel_jit<false, false, true>(k, fb, row0, rr, cc, tl, fs, hs, jit); break;
+        case 2: pixel_jit<false, true, false>(k, fb, row0, rr, cc, tl, fs, hs, jit); break;
+        case 3: pixel_jit<false, true, true>(k, fb, row0, rr, cc, tl, fs, hs, jit); break;
+        case 4: pixel_jit<true, false, false>(k, fb, row0, rr, cc, tl, fs, hs, jit); break;
+        case 5: pixel_jit<true, false, true>(k, fb, row0, rr, cc, tl, fs, hs, jit); break;
+        case 6: pixel_jit<true, true, false>(k, fb, row0, rr, cc, tl, fs, hs, jit); break;
+        case 7: pixel_jit<true, true, true>(k, fb, row0, rr, cc, tl, fs, hs, jit); break;
+    }
 }
 }  // namespace
 
@@ -48,20 +75,11 @@ extern "C" int rtx_hostemu_render(const rtx_scene_desc* sd, const rtx_camera_des
         for (int64_t p = 0; p < npix; ++p) {
             Tally tl = {};
             float frames[kMaxDepth * 4];
+            float hst[kMaxHLevels * 9];
             const FrameStack fs{frames, 1};
+            const HStack hs{hst, 1};
             const int32_t rr = (int32_t)(p / k.ncols), cc = (int32_t)(p % k.ncols);
-            const bool jit = k.jitter != RTX_JITTER_OFF;
-            if (H.has_mesh) {
-                if (H.has_secondary) jit ? render_pixel<true, true, true, true>(k, fb, row0, rr, cc, tl, fs)
-                                         : render_pixel<true, true, true, false>(k, fb, row0, rr, cc, tl, fs);
-                else jit ? render_pixel<true, false, true, true>(k, fb, row0, rr, cc, tl, fs)
-                         : render_pixel<true, false, true, false>(k, fb, row0, rr, cc, tl, fs);
-            } else {
-                if (H.has_secondary) jit ? render_pixel<false, true, true, true>(k, fb, row0, rr, cc, tl, fs)
-                                         : render_pixel<false, true, true, false>(k, fb, row0, rr, cc, tl, fs);
-                else jit ? render_pixel<false, false, true, true>(k, fb, row0, rr, cc, tl, fs)
-                         : render_pixel<false, false, true, false>(k, fb, row0, rr, cc, tl, fs);
-            }
+            pixel_any(H, k, fb, row0, rr, cc, tl, fs, hs, k.jitter != RTX_JITTER_OFF);
             for (int q = 0; q < kMaxDepth; ++q) loc[q] += tl.cast[q];
             loc[RTX_CNT_SHADOW] += tl.shadow;
             loc[RTX_CNT_SHADE] += tl.shade;
@@ -86,15 +104,22 @@ extern "C" int rtx_hostemu_intersect(const rtx_scene_desc* sd, int64_t n, const 
         const f3 o = mk(ro[i], ro[n + i], ro[2 * n + i]);
         const f3 d = mk(rd[i], rd[n + i], rd[2 * n + i]);
         Tally tl = {};
-        Hit h = H.has_mesh ? closest_hit<true, false>(v, o, d, (float)time, tl) : closest_hit<false, false>(v, o, d, (float)time, tl);
+        float hst[kMaxHLevels * 9];
+        const HStack hs{hst, 1};
+        HHit hh;
+        const float tm = (float)time;
+        Hit h = H.has_mesh ? closest_hit<true, true, false>(v, o, d, tm, tl, hs, hh)
+                           : closest_hit<false, true, false>(v, o, d, tm, tl, hs, hh);
         int32_t mat = -1;
         f3 nn = mk(0, 0, 0), pp = mk(0, 0, 0);
-        if (h.obj >= 0) {
-            Surface sf = H.has_mesh ? resolve_hit<true>(v, h, o, d, (float)time) : resolve_hit<false>(v, h, o, d, (float)time);
+        const bool hit = h.obj != -1;
+        if (hit) {
+            Surface sf = H.has_mesh ? resolve_hit<true, true>(v, h, hh, o, d, tm) : resolve_hit<false, true>(v, h, hh, o, d, tm);
             mat = sf.mat; nn = sf.normal; pp = sf.position;
         }
-        t_out[i] = h.obj >= 0 ? hit_t64(v, h.obj, h.sub, o, d, (float)time) : (double)INFINITY;
-        obj_out[i] = h.obj >= 0 ? v.objs[h.obj].oid : -1; mat_out[i] = mat;
+        t_out[i] = !hit ? (double)INFINITY : h.obj == kHierHit ? hh.t64 : hit_t64(v, h.obj, h.sub, o, d, tm);
+        obj_out[i] = !hit ? -1 : h.obj == kHierHit ? h.sub : v.objs[h.obj].oid;
+        mat_out[i] = mat;
         n_out[i] = nn.x; n_out[n + i] = nn.y; n_out[2 * n + i] = nn.z;
         p_out[i] = pp.x; p_out[n + i] = pp.y; p_out[2 * n + i] = pp.z;
     }
@@ -112,8 +137,10 @@ extern "C" int rtx_hostemu_occluded(const rtx_scene_desc* sd, int64_t n, const f
         const f3 o = mk(ro[i], ro[n + i], ro[2 * n + i]);
         const f3 d = mk(rd[i], rd[n + i], rd[2 * n + i]);
         Tally tl = {};
-        bool r = H.has_mesh ? occluded<true, false>(v, o, d, tmax[i], (float)time, tl)
-                            : occluded<false, false>(v, o, d, tmax[i], (float)time, tl);
+        float hst[kMaxHLevels * 9];
+        const HStack hs{hst, 1};
+        bool r = H.has_mesh ? occluded<true, true, false>(v, o, d, tmax[i], (float)time, tl, hs)
+                            : occluded<false, true, false>(v, o, d, tmax[i], (float)time, tl, hs);
         occ[i] = r ? 1 : 0;
     }
     return RTX_OK;
@@ -129,6 +156,7 @@ extern "C" int64_t rtx_hostemu_sizeof(int which) {
         case 3: return sizeof(rtx_light);
         case 4: return sizeof(rtx_scene_desc);
         case 5: return sizeof(rtx_camera_desc);
+        case 6: return sizeof(rtx_texture);
     }
     return -1;
 }

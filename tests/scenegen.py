@@ -68,3 +68,82 @@ def tie_scene(res=(40, 30)):
                         {"name": "box", "type": "box", "min": [0.5, -1.0, -1.0], "max": [2.5, 0.0, 1.0], "materials": [0]},
                         {"name": "box2", "type": "box", "min": [0.5, -1.0, -1.0], "max": [2.5, 0.0, 1.0], "materials": [1]}],
             "lights": [{"name": "l", "type": "point", "position": [2, 5, 3], "colour": [1, 1, 1], "power": 1.0}]}
+
+
+def random_hier_scene(seed, res=(48, 36), mesh=False):
+    """Random hierarchy (CSG) scenes: nested union / intersection / difference / unknown
+    nodes with translate-rotate-scale, fallback materials, root and child speeds, a `ref`
+    copy, difference nodes with a third (ignored) child, and textured planes and boxes."""
+    rng = np.random.RandomState(1000 + seed)
+    r = lambda lo, hi, n=None: np.round(rng.uniform(lo, hi, n), 3).tolist()  # noqa: E731
+    sc = random_scene(seed, res=res, mesh=False)
+    ids = [m["ID"] for m in sc["materials"]]
+    tex = ["textures/axes.png", "textures/brick.jpg", "textures/ground.png", "textures/wall2.png"]
+    counter = [0]
+
+    def name():
+        counter[0] += 1
+        return "g%d" % counter[0]
+
+    def leaf(depth):
+        k = rng.choice(["sphere", "sphere", "box", "box", "plane"] + (["mesh"] if mesh else []))
+        g = {"name": name(), "type": str(k), "position": r(-1, 1, 3)}
+        if rng.rand() < 0.7:
+            g["materials"] = [int(rng.choice(ids))] + ([int(rng.choice(ids))] if rng.rand() < 0.3 else [])
+        if k == "sphere":
+            g["radius"] = float(r(0.3, 1.2))
+        elif k == "box":
+            if rng.rand() < 0.5:
+                g["size"] = r(0.4, 1.6, 3)
+            else:
+                lo = np.array(r(-1, 0, 3))
+                g["min"], g["max"] = lo.tolist(), (lo + np.array(r(0.4, 1.5, 3))).round(3).tolist()
+            if rng.rand() < 0.3:
+                g["texture"] = str(rng.choice(tex))
+        elif k == "plane":
+            g["normal"] = [[0.0, 1.0, 0.0], [1.0, 0.0, 0.0], [0.0, 0.0, 1.0], r(-1, 1, 3)][rng.randint(4)]
+            if rng.rand() < 0.5:
+                g["texture"] = str(rng.choice(tex))
+                if rng.rand() < 0.7:
+                    g["texture_scale"] = float(r(1, 40))
+        else:
+            g.update({"filepath": "torus_mesh.obj", "scale": float(r(0.3, 0.6)), "flat_shaded": bool(rng.rand() < 0.5)})
+        if rng.rand() < 0.2:
+            g["speed"] = r(-0.5, 0.5, 3)
+        return g
+
+    def node(depth):
+        ht = str(rng.choice(["union", "intersection", "difference", "difference", "xor"], p=[0.3, 0.25, 0.2, 0.2, 0.05]))
+        n = {"name": name(), "type": "node", "hierarchy_type": ht}
+        if rng.rand() < 0.2:
+            del n["hierarchy_type"]  # default: union
+        if rng.rand() < 0.8:
+            n["position"] = r(-1.5, 1.5, 3)
+        if rng.rand() < 0.6:
+            n["rotation"] = [float(rng.choice([0.0, 15.0, 30.0, 45.0, 90.0, -20.0, 7.5])) for _ in range(3)]
+        if rng.rand() < 0.6:
+            n["scale"] = r(0.5, 1.6, 3)
+        nc = rng.randint(2, 4) if ht == "difference" else rng.randint(1, 4)
+        n["children"] = [node(depth + 1) if (depth < 3 and rng.rand() < 0.35) else leaf(depth + 1) for _ in range(nc)]
+        return n
+
+    roots = []
+    for k in range(rng.randint(1, 4)):
+        n = node(0)
+        n["materials"] = [int(rng.choice(ids))]
+        if rng.rand() < 0.3:
+            n["speed"] = r(-0.4, 0.4, 3)
+        roots.append(n)
+    objs = sc["objects"] + roots
+    if rng.rand() < 0.6:
+        ref = {"name": "copy", "type": "node", "ref": roots[0]["name"], "position": r(-2, 2, 3),
+               "materials": [int(rng.choice(ids))]}
+        if rng.rand() < 0.5:
+            ref["rotation"] = [0.0, float(rng.choice([30.0, 90.0])), 0.0]
+        objs.append(ref)
+    if rng.rand() < 0.5:  # a textured ground
+        objs[0] = dict(objs[0], texture="textures/ground.png", texture_scale=float(r(1, 8)))
+    order = rng.permutation(len(objs))
+    sc["objects"] = [objs[i] for i in order]
+    # leaves without materials need a root that has some (else the reference raises)
+    return sc

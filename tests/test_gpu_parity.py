@@ -155,3 +155,65 @@ def test_ties_follow_scene_order():
     from scenegen import tie_scene
     d = tie_scene((80, 60))
     assert compare(product_scene_dict(d).render(), oracle_render_dict(d))["frac_diff"] == 0.0
+
+
+HIER_CASES = [
+    ("NovelScene1", (256, 128), {"AA": {"jitter": False, "samples": 1}}),
+    ("NovelScene2", (128, 64), {"AA": {"jitter": False, "samples": 1}}),
+]
+
+
+@pytest.mark.parametrize("name,res,edits", HIER_CASES)
+def test_hierarchy_scenes_match_oracle(name, res, edits):
+    """CSG hierarchies + textures (+ motion blur, DOF for NovelScene2) vs the oracle."""
+    sc = product_scene(name, res, **edits)
+    s = assert_parity(sc.render(), oracle_render(name, res, **edits), name)
+    assert s["frac_diff"] == 0.0, s
+
+
+@pytest.mark.parametrize("name,max_mean", [("NovelScene1", 0.1), ("NovelScene2", 0.2)])
+def test_novel_scenes_full_size_match_published_render(name, max_mean):
+    """The full configs of renders/NovelScene{1,2}.png (2048x1024 AA32, and 1024x512
+    AA2 x DOF15 x 16 motion times, both jittered with the reference's unseeded RNG) against
+    the published PNGs: Philox jitter vs unseeded numpy, so the comparison is statistical."""
+    import os
+    from PIL import Image
+    from oracle import oracle as O
+    sc = product_scene(name)
+    png = sc.render_rgb8()
+    pub = np.asarray(Image.open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "published",
+                                             name + ".png")).convert("RGB"))
+    assert png.shape == pub.shape
+    d = png.astype(int) - pub.astype(int)
+    print(name, "mean|d| %.4f bias %.4f exact %.4f" % (np.abs(d).mean(), d.mean(), (np.abs(d).max(axis=2) == 0).mean()))
+    assert np.abs(d).mean() < max_mean and abs(d.mean()) < 0.05
+    assert (np.abs(d).max(axis=2) == 0).mean() > 0.93
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_random_hierarchy_scenes_match_oracle(seed):
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import random_hier_scene
+    d = random_hier_scene(seed, res=(64, 48), mesh=(seed % 4 == 0))
+    s = assert_parity(product_scene_dict(d).render(), oracle_render_dict(d), "hier seed %d" % seed)
+    assert s["frac_diff"] == 0.0, s
+
+
+def test_hierarchy_geometry_kat():
+    from oracle import oracle as O
+    rng = np.random.RandomState(3)
+    n = 20000
+    o = (np.array([0, 1, 0]) + rng.uniform(-3, 3, (n, 3))).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    sc = product_scene("NovelScene1", (8, 8))
+    dd, base = O.load_bundle("NovelScene1")
+    osc = O.OracleScene(dd, base)
+    for time in (0.0, 0.5):
+        got = sc.intersect(o, d, time)
+        t, ob, _, m, nn, pp = osc.closest(time, o, d)
+        assert np.array_equal(got["obj"], ob)
+        hit = ob >= 0
+        assert np.array_equal(got["t"][hit], t[hit]) and np.array_equal(got["mat"], m)
+        assert np.array_equal(got["normal"][hit], nn[hit]) and np.array_equal(got["position"][hit], pp[hit])
+        for tmax in (1.0, np.inf):
+            assert np.array_equal(sc.occluded(o, d, tmax, time), osc.shadow(time, o, d, tmax).astype(bool))

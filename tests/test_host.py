@@ -31,7 +31,7 @@ def test_abi_struct_layouts_match_the_header():
     lib = hostemu.lib()
     lib.rtx_hostemu_sizeof.restype = C.c_int64
     for i, st in enumerate([N.rtx_object, N.rtx_triangle, N.rtx_material, N.rtx_light, N.rtx_scene_desc,
-                            N.rtx_camera_desc]):
+                            N.rtx_camera_desc, N.rtx_texture]):
         assert lib.rtx_hostemu_sizeof(i) == C.sizeof(st), st.__name__
 
 
@@ -86,12 +86,91 @@ def test_parser_light_keyerror_drops_all_lights():
     assert rtx.load_scene(d, verbose=False).lights == []
 
 
-def test_hierarchy_nodes_fail_loudly():
+def _novel(name="NovelScene1"):
     with open(os.path.join(REPO, "assets", "scenes.json")) as f:
-        d = json.load(f)["NovelScene1"]
+        d = json.load(f)[name]
     d["__base_dir__"] = os.path.join(REPO, "assets")
-    with pytest.raises(NotImplementedError):
-        rtx.load_scene(d, verbose=False)
+    return d
+
+
+def test_hierarchy_parsing_follows_reference():
+    """scene_parser.py:177-205, :261-285 and hierarchy.py:21-28 on NovelScene1."""
+    from rtx import geometry as geom
+    sc = rtx.load_scene(_novel(), verbose=False)
+    names = [o.name for o in sc.objects]
+    assert names == ["ground", "wall1", "wall2", "wall4", "wall3", "bike", "bike2", "trail1", "trail2"]
+    bike, bike2 = sc.objects[5], sc.objects[6]
+    assert isinstance(bike, geom.Hierarchy) and bike.hierarchy_type == "union"
+    # ref copy: its own name, materials and transform, the copied subtree (and its speeds)
+    assert bike2.name == "bike2" and [m.ID for m in bike2.materials] == [9]
+    assert np.array_equal(bike2.t, np.float32([-2.0, -2.5, 2.0]))
+    assert len(bike2.children) == len(bike.children)
+    assert bike2.children[0] is not bike.children[0]
+    # fallback: leaves get the root's materials appended, nested node materials untouched
+    inner = bike.children[0].children[0].children[0].children[0]   # front_wheel/cutout/main/inner
+    assert inner.name == "inner" and [m.ID for m in inner.materials] == [1, 0]
+    inner2 = bike2.children[0].children[0].children[0].children[0]
+    assert [m.ID for m in inner2.materials] == [1, 9]
+    outer = bike.children[0].children[0].children[0].children[1]
+    assert [m.ID for m in outer.materials] == [0]
+    assert bike.children[0].materials == []
+    # speeds: root speed + own speed for every leaf, at any depth
+    assert np.array_equal(inner.speed, np.float32([0, 0, 0.5]))
+    # walls: no root materials, so nothing is appended; planes keep their texture
+    wall = sc.objects[1]
+    assert [m.ID for m in wall.children[0].materials] == [8] and wall.children[0].texture is not None
+    assert wall.children[0].texture_scale == 35.0 and wall.children[1].speed is None
+    assert sc.objects[0].texture.size == (1024, 1024) and sc.objects[0].texture_scale == 4.0
+
+
+def test_unknown_ref_is_skipped():
+    d = _novel()
+    d["objects"] = [o for o in d["objects"] if o["name"] != "bike"]
+    sc = rtx.load_scene(d, verbose=False)
+    assert "bike2" not in [o.name for o in sc.objects]
+
+
+def test_descriptor_is_preorder_with_parents():
+    sc = rtx.load_scene(_novel(), verbose=False)
+    desc = sc.scene_desc()
+    n = desc.n_objects
+    par = [desc.objects[i].parent for i in range(n)]
+    top = [i for i in range(n) if par[i] == -1]
+    assert len(top) == len(sc.objects)
+    for i in range(n):
+        assert par[i] < i
+        if par[i] >= 0:
+            assert desc.objects[par[i]].type == N.RTX_NODE
+    assert desc.n_textures == 5  # ground + four walls, each opened once per plane
+    t = desc.textures[0]
+    assert (t.width, t.height) == (1024, 1024)
+
+
+def test_texture_rgb8_matches_getpixel():
+    from PIL import Image
+    from rtx import geometry as geom
+    for name in ("wall1.png", "brick.jpg", "axes.png"):
+        im = geom.open_texture(os.path.join(REPO, "assets", "textures", name))
+        a = geom.texture_rgb8(im)
+        for (i, j) in ((0, 0), (5, 17), (im.width - 1, im.height - 1), (100, 3)):
+            assert tuple(a[j, i]) == tuple(im.getpixel((i, j))[:3])
+
+
+def test_invalid_hierarchy_is_rejected_without_gpu():
+    lib = N.load()
+    objs = (N.rtx_object * 2)()
+    objs[0].type, objs[0].parent, objs[0].hierarchy_type = N.RTX_NODE, -1, N.RTX_DIFFERENCE
+    objs[1].type, objs[1].parent, objs[1].n_mats, objs[1].texture = N.RTX_SPHERE, 0, 1, -1
+    objs[0].texture = -1
+    mats = (N.rtx_material * 1)()
+    d = N.rtx_scene_desc()
+    d.n_objects, d.objects, d.n_materials, d.materials = 2, objs, 1, mats
+    h = C.c_void_p()
+    assert lib.rtx_scene_create(C.byref(d), C.byref(h)) == N.RTX_ERR_INVALID
+    assert b"two children" in lib.rtx_last_error()
+    objs[1].parent = 1  # not an earlier node
+    assert lib.rtx_scene_create(C.byref(d), C.byref(h)) == N.RTX_ERR_INVALID
+    assert b"parent" in lib.rtx_last_error()
 
 
 def test_camera_tables_follow_reference_sequences():

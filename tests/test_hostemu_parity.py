@@ -15,6 +15,8 @@ CASES = [
     ("TorusMesh", (64, 64), {"flat_shaded": False}),
     ("MotionBlur", (75, 64), {}),
     ("DepthOfField", (40, 30), {"AA": {"jitter": False, "samples": 2}}),
+    ("NovelScene1", (128, 64), {"AA": {"jitter": False, "samples": 1}}),     # CSG hierarchies + textures
+    ("NovelScene2", (64, 32), {"AA": {"jitter": False, "samples": 1}}),      # + motion blur, DOF
 ]
 
 
@@ -99,3 +101,49 @@ def test_hostemu_ties_follow_scene_order():
     assert assert_parity(img, ref)["frac_diff"] == 0.0
     # the red/blue coincident spheres: s1 (blue) is first in scene order
     assert (ref[..., 2] > ref[..., 0]).any()
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_hostemu_random_hierarchy_scenes(seed):
+    """Random CSG trees (every node type, nesting, transforms, fallback materials, speeds,
+    `ref` copies, textured planes/boxes) vs the oracle: bit-exact image and ray tallies."""
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import random_hier_scene
+    d = random_hier_scene(seed, mesh=(seed % 4 == 0))
+    img, cnt = hostemu.render(product_scene_dict(d))
+    ref, tl = oracle_render_dict(d, tallies=True)
+    s = assert_parity(img, ref, "seed %d" % seed)
+    assert s["frac_diff"] == 0.0, s
+    assert list(cnt[:10]) == tl[:10] and cnt[10] == tl[11]
+
+
+@pytest.mark.parametrize("seed", [None, 3, 8])
+def test_hostemu_hierarchy_geometry_kat(seed):
+    """Batched closest hit / shadow rays through hierarchies vs the oracle."""
+    from oracle import oracle as O
+    from common import product_scene_dict
+    from scenegen import random_hier_scene
+    import os
+    rng = np.random.RandomState(5)
+    if seed is None:
+        dd, base = O.load_bundle("NovelScene1")
+        o, d = _rays(rng, 3000, np.array([0, 1, 0]), spread=3.0)
+        sc = product_scene("NovelScene1", (8, 8))
+    else:
+        dd = random_hier_scene(seed)
+        base = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets")
+        o, d = _rays(rng, 3000, np.array([0, 0.5, 0]), spread=2.5)
+        sc = product_scene_dict(dd)
+    osc = O.OracleScene(dd, base)
+    for time in (0.0, 0.5):
+        got = hostemu.intersect(sc, o, d, time)
+        t, ob, _, m, nn, pp = osc.closest(time, o, d)
+        assert np.array_equal(got["obj"], ob)
+        hit = ob >= 0
+        assert hit.mean() > 0.1
+        assert np.array_equal(got["t"][hit], t[hit])
+        assert np.array_equal(got["mat"], m)
+        assert np.array_equal(got["normal"][hit], nn[hit])
+        assert np.array_equal(got["position"][hit], pp[hit])
+        for tmax in (1.0, np.inf):
+            assert np.array_equal(hostemu.occluded(sc, o, d, tmax, time), osc.shadow(time, o, d, tmax).astype(bool))

@@ -50,3 +50,34 @@ def test_oracle_tallies_match_survey_appendix_c():
     assert abs(t[1] / n - 0.326) < 1e-3 and abs(t[2] / n - 0.182) < 1e-3 and abs(t[11] / n - 1.241) < 1e-3
     _, t = oracle_render("TorusMesh", res=(192, 108), tallies=True)
     assert t[11] == 3 * n and t[12] == n
+
+
+def _novel_strip(args):
+    name, tasks, k, seed = args
+    d, base = O.load_bundle(name)
+    sc = O.OracleScene(d, base)
+    base_, extra = divmod(sc.width, tasks)
+    ncol = base_ + (1 if k < extra else 0)
+    c0 = k * base_ + min(k, extra)
+    noise = np.random.RandomState(seed).rand(ncol * sc.height * sc.spp_rays * 3)
+    return c0, O.to_png_array(sc.render(k, tasks, noise=noise))
+
+
+@pytest.mark.parametrize("name,tasks,strips,max_mean", [
+    ("NovelScene1", 64, (30, 33), 0.1),   # 2048x1024, AA 32 jittered: hierarchies + textures
+    ("NovelScene2", 128, (64,), 0.2),     # 1024x512, AA 2 x DOF 15 x 16 motion times
+])
+def test_oracle_novel_scenes_statistical(name, tasks, strips, max_mean):
+    """NovelScene1/2.png (CSG hierarchies, `ref` copies, fallback materials, plane
+    textures; NovelScene2 also motion blur through hierarchies and DOF) used unseeded
+    jitter: column strips through the bikes compare statistically (full-frame check:
+    tools/pin_novel.py, 98.7% / 97% of pixels identical)."""
+    from multiprocessing import Pool
+    ref = _png(name)
+    with Pool(len(strips)) as pool:
+        outs = pool.map(_novel_strip, [(name, tasks, k, 100 + k) for k in strips])
+    for c0, png in outs:
+        d = png.astype(int) - ref[:, c0:c0 + png.shape[1]].astype(int)
+        assert np.abs(d).mean() < max_mean, (name, c0, np.abs(d).mean())
+        assert abs(d.mean()) < 0.05
+        assert (np.abs(d).max(axis=2) == 0).mean() > 0.93
