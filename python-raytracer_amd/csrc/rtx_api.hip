@@ -341,6 +341,148 @@ void make_matrices(const float* trs, Mat4& M, Mat4& Minv) {
     Minv = m4_inverse(m);
 }
 
+// ------------------------------------------------------------------ hierarchy bounds
+// Conservative boxes per hierarchy node (DBound, rtx_trace.h), in double precision, for
+// the motion-time range [tlo, thi]; each box is padded by 1e-4 of its coordinate scale,
+// orders of magnitude above the fp32 rounding of the device's transforms and hit points.
+struct HBox {
+    double lo[3], hi[3];
+};
+HBox hb_all() { return HBox{{-INFINITY, -INFINITY, -INFINITY}, {INFINITY, INFINITY, INFINITY}}; }
+HBox hb_none() { return HBox{{INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}}; }
+bool hb_empty(const HBox& b) { return !(b.lo[0] <= b.hi[0] && b.lo[1] <= b.hi[1] && b.lo[2] <= b.hi[2]); }
+bool hb_finite(const HBox& b) {
+    for (int k = 0; k < 3; ++k)
+        if (!std::isfinite(b.lo[k]) || !std::isfinite(b.hi[k])) return false;
+    return true;
+}
+HBox hb_union(const HBox& a, const HBox& b) {
+    if (hb_empty(a)) return b;
+    if (hb_empty(b)) return a;
+    HBox r;
+    for (int k = 0; k < 3; ++k) { r.lo[k] = std::min(a.lo[k], b.lo[k]); r.hi[k] = std::max(a.hi[k], b.hi[k]); }
+    return r;
+}
+HBox hb_inter(const HBox& a, const HBox& b) {
+    HBox r;
+    for (int k = 0; k < 3; ++k) { r.lo[k] = std::max(a.lo[k], b.lo[k]); r.hi[k] = std::min(a.hi[k], b.hi[k]); }
+    return hb_empty(r) ? hb_none() : r;
+}
+HBox hb_point(const float* p) { return HBox{{p[0], p[1], p[2]}, {p[0], p[1], p[2]}}; }
+HBox hb_pad(HBox b) {
+    if (hb_empty(b) || !hb_finite(b)) return b;
+    double m = 0.0;
+    for (int k = 0; k < 3; ++k) m = std::max({m, std::fabs(b.lo[k]), std::fabs(b.hi[k]), b.hi[k] - b.lo[k]});
+    const double pad = 1e-4 * m + 1e-6;
+    for (int k = 0; k < 3; ++k) { b.lo[k] -= pad; b.hi[k] += pad; }
+    return b;
+}
+double hb_volume(const HBox& b) {
+    if (hb_empty(b)) return 0.0;
+    return (b.hi[0] - b.lo[0]) * (b.hi[1] - b.lo[1]) * (b.hi[2] - b.lo[2]);
+}
+// M * (x, y, z, 1) of the eight corners (node frame -> parent frame)
+HBox hb_xform(const float* M, const HBox& b) {
+    if (hb_empty(b)) return b;
+    if (!hb_finite(b)) return hb_all();
+    HBox r = hb_none();
+    for (int c = 0; c < 8; ++c) {
+        const double x = (c & 1) ? b.hi[0] : b.lo[0], y = (c & 2) ? b.hi[1] : b.lo[1], z = (c & 4) ? b.hi[2] : b.lo[2];
+        double q[3];
+        for (int k = 0; k < 3; ++k) q[k] = (double)M[k] * x + (double)M[4 + k] * y + (double)M[8 + k] * z + (double)M[12 + k];
+        r = hb_union(r, HBox{{q[0], q[1], q[2]}, {q[0], q[1], q[2]}});
+    }
+    return hb_pad(r);
+}
+void hb_store(const HBox& b, float* lo, float* hi) {
+    for (int k = 0; k < 3; ++k) {  // round outwards
+        lo[k] = (float)b.lo[k];
+        hi[k] = (float)b.hi[k];
+        if ((double)lo[k] > b.lo[k]) lo[k] = std::nextafter(lo[k], -INFINITY);
+        if ((double)hi[k] < b.hi[k]) hi[k] = std::nextafter(hi[k], INFINITY);
+    }
+    lo[3] = hi[3] = 0.0f;
+}
+
+struct NodeBoxes {
+    HBox h, i, s;
+};
+
+NodeBoxes leaf_boxes(const DObj& o, const std::vector<DTri>& tris, double tlo, double thi) {
+    auto moved_box = [&](const float* p) {
+        HBox b = hb_point(p);
+        if (o.has_speed)
+            for (double t : {tlo, thi}) {
+                float q[3];
+                for (int k = 0; k < 3; ++k) q[k] = p[k] + o.speed[k] * (float)t;
+                b = hb_union(b, hb_point(q));
+            }
+        return b;
+    };
+    NodeBoxes nb;
+    if (o.type == OBJ_SPHERE) {
+        HBox b = moved_box(o.a);
+        for (int k = 0; k < 3; ++k) { b.lo[k] -= o.radius; b.hi[k] += o.radius; }
+        nb.h = nb.i = nb.s = hb_pad(b);
+    } else if (o.type == OBJ_BOX) {
+        const HBox b = hb_pad(hb_union(moved_box(o.a), moved_box(o.b)));
+        nb.h = nb.i = nb.s = b;
+    } else if (o.type == OBJ_PLANE) {
+        nb.h = nb.s = hb_all();
+        nb.i = hb_none();
+    } else {  // mesh (no motion: mesh.py never reads speed)
+        HBox b = hb_none();
+        for (int f = 0; f < o.tri_count; ++f) {
+            const DTri& T = tris[o.tri_begin + f];
+            b = hb_union(b, hb_union(hb_point(T.v0), hb_union(hb_point(T.v1), hb_point(T.v2))));
+        }
+        nb.h = nb.s = hb_pad(b);
+        nb.i = hb_none();
+    }
+    return nb;
+}
+
+std::vector<DBound> compute_bounds(const std::vector<DNode>& nodes, const std::vector<DObj>& objs,
+                                   const std::vector<DTri>& tris, double tlo, double thi) {
+    const int n = (int)nodes.size();
+    std::vector<NodeBoxes> nb(n);
+    for (int x = n - 1; x >= 0; --x) {  // children before parents
+        const DNode& X = nodes[x];
+        if (X.kind == HN_LEAF) { nb[x] = leaf_boxes(objs[X.obj], tris, tlo, thi); continue; }
+        std::vector<int> ch;
+        for (int j = x + 1; j < X.end; j = nodes[j].end) ch.push_back(j);
+        NodeBoxes r{hb_none(), hb_none(), hb_none()};
+        if (X.kind == HN_UNION) {
+            for (int c : ch) { r.h = hb_union(r.h, nb[c].h); r.i = hb_union(r.i, nb[c].i); r.s = hb_union(r.s, nb[c].s); }
+        } else if (X.kind == HN_INTER) {
+            r.i = hb_all();
+            r.s = hb_all();
+            double best = INFINITY;
+            for (int c : ch) {
+                HBox hc = nb[c].h;
+                for (int c2 : ch)
+                    if (c2 != c) hc = hb_inter(hc, nb[c2].i);
+                r.h = hb_union(r.h, hc);
+                r.i = hb_inter(r.i, nb[c].i);
+                const double v = hb_empty(nb[c].s) ? -1.0 : (hb_finite(nb[c].s) ? hb_volume(nb[c].s) : INFINITY);
+                if (v < best) { best = v; r.s = nb[c].s; }  // every child must shadow: any one child bounds it
+            }
+        } else if (X.kind == HN_DIFF && ch.size() >= 2) {
+            r.h = hb_union(nb[ch[0]].h, hb_inter(nb[ch[1]].h, nb[ch[0]].i));
+            r.i = nb[ch[0]].i;
+            r.s = r.h;  // diff shadow = some surviving hit past the epsilon
+        }
+        nb[x] = NodeBoxes{hb_xform(X.M, r.h), hb_xform(X.M, r.i), hb_xform(X.M, r.s)};
+    }
+    std::vector<DBound> out(n);
+    for (int x = 0; x < n; ++x) {
+        hb_store(nb[x].h, out[x].hlo, out[x].hhi);
+        hb_store(nb[x].i, out[x].ilo, out[x].ihi);
+        hb_store(nb[x].s, out[x].slo, out[x].shi);
+    }
+    return out;
+}
+
 struct HostScene {
     std::vector<DNode> nodes;
     std::vector<uint32_t> texels;
@@ -713,6 +855,13 @@ struct rtx_scene {
     SceneView view{};
     bool has_mesh = false, has_secondary = false, has_ext = false;
     int32_t hlevels = 0;
+    // host copies for the per-time-range hierarchy bounds
+    std::vector<DNode> h_nodes;
+    std::vector<DObj> h_objs;
+    std::vector<DTri> h_tris;
+    std::vector<DBound> h_bounds_abi;
+    void* d_bounds_cam = nullptr;   // for the camera's motion times
+    void* d_bounds_abi = nullptr;   // for the time of the last rtx_intersect / rtx_occluded
     void* d_nodes = nullptr;
     void* d_texels = nullptr;
     void* d_lut = nullptr;
@@ -747,6 +896,8 @@ int upload(void** dptr, const std::vector<T>& v) {
 
 void free_camera(rtx_scene* s) {
     for (float* p : {s->d_xs, s->d_ys, s->d_dof, s->d_aa, s->d_times, s->d_noise}) (void)hipFree(p);
+    (void)hipFree(s->d_bounds_cam);
+    s->d_bounds_cam = nullptr;
     (void)hipFree(s->d_kp);
     s->d_xs = s->d_ys = s->d_dof = s->d_aa = s->d_times = s->d_noise = nullptr;
     s->d_kp = nullptr;
@@ -756,7 +907,7 @@ void free_camera(rtx_scene* s) {
 void free_scene(rtx_scene* s) {
     free_camera(s);
     for (void* p : {s->d_objs, s->d_tris, s->d_trins, s->d_mats, s->d_lights, s->d_leaves, s->d_tri_orig, s->d_nodes,
-                    s->d_texels, s->d_lut})
+                    s->d_texels, s->d_lut, s->d_bounds_abi})
         (void)hipFree(p);
     delete s;
 }
@@ -788,6 +939,15 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
     s->has_secondary = H.has_secondary;
     s->has_ext = H.has_ext;
     s->hlevels = H.hlevels;
+    if (!H.nodes.empty()) {
+        s->h_nodes = H.nodes;
+        s->h_objs = H.objs;
+        s->h_tris = H.tris;
+        if ((rc = upload(&s->d_bounds_abi, std::vector<DBound>(H.nodes.size())))) {
+            free_scene(s);
+            return rc;
+        }
+    }
     SceneView& v = s->view;
     v.objs = (cptr<DObj>)s->d_objs;
     v.tris = (cptr<DTri>)s->d_tris;
@@ -837,6 +997,12 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     if (c->jitter == RTX_JITTER_REPLAY && (rc = up(&s->d_noise, c->noise, 3 * (size_t)c->ncols * c->height * nsamp)))
         return rc;
     k.S = s->view;
+    if (!s->h_nodes.empty()) {  // hierarchy bounds over the frame's motion-time range
+        const auto mm = std::minmax_element(times.begin(), times.end());
+        if ((rc = upload(&s->d_bounds_cam, compute_bounds(s->h_nodes, s->h_objs, s->h_tris, *mm.first, *mm.second))))
+            return rc;
+        k.S.bounds = (cptr<DBound>)s->d_bounds_cam;
+    }
     k.xs = (cptr<float>)s->d_xs; k.ys = (cptr<float>)s->d_ys; k.dof_o = (cptr<float>)s->d_dof;
     k.aa_o = (cptr<float>)s->d_aa; k.times = (cptr<float>)s->d_times; k.noise = (cptr<float>)s->d_noise;
     RTX_HIP(hipMalloc((void**)&s->d_kp, sizeof(KParams)));
@@ -882,14 +1048,31 @@ int rtx_render(rtx_scene* s, int32_t row0, int32_t nrows, float* fb_dev, uint64_
     return RTX_OK;
 }
 
+namespace {
+// The scene view for one motion time (hierarchy bounds uploaded in stream order).
+int view_at(rtx_scene* s, double time, hipStream_t stream, SceneView& v) {
+    v = s->view;
+    if (s->h_nodes.empty()) return RTX_OK;
+    const float t = (float)time;
+    s->h_bounds_abi = compute_bounds(s->h_nodes, s->h_objs, s->h_tris, t, t);
+    RTX_HIP(hipMemcpyAsync(s->d_bounds_abi, s->h_bounds_abi.data(), sizeof(DBound) * s->h_bounds_abi.size(),
+                           hipMemcpyHostToDevice, stream));
+    v.bounds = (cptr<DBound>)s->d_bounds_abi;
+    return RTX_OK;
+}
+}  // namespace
+
 int rtx_intersect(rtx_scene* s, int64_t n, const float* ro, const float* rd, double time, double* t_dev,
                   int32_t* obj_dev, int32_t* mat_dev, float* normal_dev, float* position_dev, void* stream) {
     if (!s || n < 0 || (n > 0 && (!ro || !rd))) return fail(RTX_ERR_INVALID, "rtx_intersect: bad argument");
     if (n == 0) return RTX_OK;
+    SceneView view;
+    int rc = view_at(s, time, (hipStream_t)stream, view);
+    if (rc) return rc;
     const dim3 grid((unsigned)((n + 255) / 256)), block(256);
     const size_t lds = s->has_ext ? (size_t)s->hlevels * 9 * sizeof(float) * 256 : 0;
 #define RTX_ISECT(M, X)                                                                                          \
-    hipLaunchKernelGGL((k_intersect<M, X>), grid, block, lds, (hipStream_t)stream, s->view, n, ro, rd, (float)time, \
+    hipLaunchKernelGGL((k_intersect<M, X>), grid, block, lds, (hipStream_t)stream, view, n, ro, rd, (float)time, \
                        t_dev, obj_dev, mat_dev, normal_dev, position_dev)
     if (s->has_mesh) { if (s->has_ext) RTX_ISECT(true, true); else RTX_ISECT(true, false); }
     else { if (s->has_ext) RTX_ISECT(false, true); else RTX_ISECT(false, false); }
@@ -902,10 +1085,13 @@ int rtx_occluded(rtx_scene* s, int64_t n, const float* ro, const float* rd, cons
                  uint8_t* occ, void* stream) {
     if (!s || n < 0 || (n > 0 && (!ro || !rd || !tmax || !occ))) return fail(RTX_ERR_INVALID, "rtx_occluded: bad argument");
     if (n == 0) return RTX_OK;
+    SceneView view;
+    int rc = view_at(s, time, (hipStream_t)stream, view);
+    if (rc) return rc;
     const dim3 grid((unsigned)((n + 255) / 256)), block(256);
     const size_t lds = s->has_ext ? (size_t)s->hlevels * 9 * sizeof(float) * 256 : 0;
 #define RTX_OCC(M, X) \
-    hipLaunchKernelGGL((k_occluded<M, X>), grid, block, lds, (hipStream_t)stream, s->view, n, ro, rd, tmax, (float)time, occ)
+    hipLaunchKernelGGL((k_occluded<M, X>), grid, block, lds, (hipStream_t)stream, view, n, ro, rd, tmax, (float)time, occ)
     if (s->has_mesh) { if (s->has_ext) RTX_OCC(true, true); else RTX_OCC(true, false); }
     else { if (s->has_ext) RTX_OCC(false, true); else RTX_OCC(false, false); }
 #undef RTX_OCC

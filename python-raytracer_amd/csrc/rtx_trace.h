@@ -161,6 +161,16 @@ struct alignas(16) DNode {
 };
 constexpr int kMaxHLevels = 16;  // hierarchy depth limit (levels of the ray/point stacks)
 
+// Conservative regions of a hierarchy subtree, in its parent's frame, for the frame's
+// motion-time range (computed on the host, padded far beyond fp32 rounding): every
+// surviving intersect() hit lies in h, is_inside() can only be true in i, and
+// shadow_intersect() can only be true for a ray that meets s. Empty: lo > hi.
+struct alignas(16) DBound {
+    float hlo[4], hhi[4];
+    float ilo[4], ihi[4];
+    float slo[4], shi[4];
+};
+
 template <class T>
 using cptr = const T RTX_CONST*;
 
@@ -179,6 +189,7 @@ struct SceneView {
     cptr<DNode> nodes;               // hierarchy nodes (roots: 0, nodes[0].end, ...)
     cptr<uint32_t> texels;           // all textures, RGBA8 (A unused)
     cptr<float> lut255;              // fl32(k / 255) (simple_geometry.py:169)
+    cptr<DBound> bounds;             // per node, for the current motion-time range
     int32_t n_nodes, hlevels, pad3, pad4;  // hlevels: stack levels the hierarchies need
 };
 
@@ -689,8 +700,43 @@ RTX_HD uint32_t hinit(uint32_t acc, int32_t kind, int32_t depth) {
     return kind == HN_INTER ? (acc | bit) : (acc & ~bit);
 }
 
+// Culling tests against DBound boxes (conservative: a false answer is exact).
+RTX_HD bool box_nonempty(const float RTX_CONST* lo, const float RTX_CONST* hi) {
+    return lo[0] <= hi[0] && lo[1] <= hi[1] && lo[2] <= hi[2];
+}
+// The ray o + t d, t in [0, tcap], meets the box. The box is widened by
+// 2^-8 (|o|_max + |box|_max): the reference's sphere test forms its discriminant from
+// fp32 dot products of o - c, whose rounding (~2^-23 |o - c|^2 against a (dist^2 - r^2))
+// lets it report hits up to ~2^-10.5 |o - c| outside the sphere; every other test is
+// far tighter (plane/box/triangle points: ~2^-23 (|o| + |geometry|)).
+RTX_HD bool ray_meets(const float RTX_CONST* lo, const float RTX_CONST* hi, f3 o, f3 d, float tcap) {
+#if defined(RTX_NO_CULL)
+    return true;
+#endif
+    if (!box_nonempty(lo, hi)) return false;
+    const float om = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
+    const float bm = fmaxf(fmaxf(fmaxf(fabsf(lo[0]), fabsf(lo[1])), fmaxf(fabsf(lo[2]), fabsf(hi[0]))),
+                           fmaxf(fabsf(hi[1]), fabsf(hi[2])));
+    const float pad = 0x1p-8f * (om + bm);
+    auto inv = [](float v) { return 1.0f / (fabsf(v) < 1e-30f ? copysignf(1e-30f, v) : v); };
+    const float ix = inv(d.x), iy = inv(d.y), iz = inv(d.z);
+    const float tx1 = (lo[0] - pad - o.x) * ix, tx2 = (hi[0] + pad - o.x) * ix;
+    const float ty1 = (lo[1] - pad - o.y) * iy, ty2 = (hi[1] + pad - o.y) * iy;
+    const float tz1 = (lo[2] - pad - o.z) * iz, tz2 = (hi[2] + pad - o.z) * iz;
+    const float tn = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+    const float tf = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+    return tn <= tf && tf >= 0.0f && tn <= tcap;
+}
+RTX_HD bool pt_in(const float RTX_CONST* lo, const float RTX_CONST* hi, f3 p) {
+#if defined(RTX_NO_CULL)
+    return true;
+#endif
+    return lo[0] <= p.x && p.x <= hi[0] && lo[1] <= p.y && p.y <= hi[1] && lo[2] <= p.z && p.z <= hi[2];
+}
+
 // is_inside(x, p) for p in the frame of x's parent's children (hierarchy.py:111-129).
 RTX_HD bool is_inside(const SceneView& S, const HStack& hs, int x, f3 p, float time) {
+    if (!pt_in(S.bounds[x].ilo, S.bounds[x].ihi, p)) return false;
     const DNode X = S.nodes[x];
     if (X.kind == HN_LEAF) return leaf_inside(S.objs[X.obj], p, time);
     if (X.kind == HN_OTHER) return false;
@@ -780,9 +826,16 @@ RTX_HD bool walk_up(const SceneView& S, const HStack& hs, int cur, int stop, flo
 // Enumerates s.intersect(R[depth(s)]) in the reference's list order: want(t64) is asked
 // before a hit's filters run (t does not change on the way up), take(t64, position,
 // normal, material, leaf DObj) receives every surviving hit in the frame of s's parent.
-template <bool MESH, class Want, class Take>
-RTX_HD void hier_enum(const SceneView& S, const HStack& hs, int s, float time, Want& want, Take& take) {
+template <bool MESH, class Want, class Take, class Cap>
+RTX_HD void hier_enum(const SceneView& S, const HStack& hs, int s, float time, Want& want, Take& take, Cap& cap) {
+    // subtrees whose hit region the ray cannot meet before cap() are skipped (wave-uniform)
+    auto culled = [&](int c, int32_t depth) {
+        f3 ro, rd;
+        hs.get_ray(depth, ro, rd);
+        return !RTX_ANY(ray_meets(S.bounds[c].hlo, S.bounds[c].hhi, ro, rd, cap()));
+    };
     const DNode root = S.nodes[s];
+    if (culled(s, root.depth)) return;
     auto visit_leaf = [&](int li, int32_t depth, int32_t obj) {
         f3 lo, ld;
         hs.get_ray(depth, lo, ld);
@@ -802,6 +855,7 @@ RTX_HD void hier_enum(const SceneView& S, const HStack& hs, int s, float time, W
     for (int i = s + 1; i < root.end;) {
         const DNode c = S.nodes[i];
         if (c.pkind == HN_DIFF && c.cidx >= 2) { i = c.end; continue; }  // difference reads children 0, 1
+        if (culled(i, c.depth)) { i = c.end; continue; }
         if (c.kind == HN_LEAF) { visit_leaf(i, c.depth, c.obj); ++i; continue; }
         if (c.kind == HN_OTHER) { i = c.end; continue; }
         f3 ro, rd;
@@ -824,10 +878,11 @@ RTX_HD bool diff_shadow(const SceneView& S, const HStack& hs, int x, float time)
     const int c0 = x + 1, c1 = S.nodes[c0].end;
     bool found = false;
     auto want = [&](double t) { return !found && t > 1e-4; };
+    auto cap = [&]() { return found ? -1.0f : INFINITY; };
     auto take0 = [&](double, f3 pos, f3, int32_t, int32_t) { found = !is_inside(S, hs, c1, pos, time); };
-    hier_enum<MESH>(S, hs, c0, time, want, take0);
+    hier_enum<MESH>(S, hs, c0, time, want, take0, cap);
     auto take1 = [&](double, f3 pos, f3, int32_t, int32_t) { found = is_inside(S, hs, c0, pos, time); };
-    hier_enum<MESH>(S, hs, c1, time, want, take1);
+    hier_enum<MESH>(S, hs, c1, time, want, take1, cap);
     return found;
 }
 
@@ -836,6 +891,7 @@ RTX_HD bool diff_shadow(const SceneView& S, const HStack& hs, int x, float time)
 template <bool MESH>
 RTX_HD bool hier_shadow(const SceneView& S, const HStack& hs, int r, f3 o, f3 d, double t_max, float time) {
     hs.put_ray(0, o, d);
+    if (!RTX_ANY(ray_meets(S.bounds[r].slo, S.bounds[r].shi, o, d, INFINITY))) return false;
     const DNode R = S.nodes[r];
     if (R.kind == HN_OTHER) return false;
     if (R.kind == HN_DIFF) return diff_shadow<MESH>(S, hs, r, time);
@@ -854,16 +910,25 @@ RTX_HD bool hier_shadow(const SceneView& S, const HStack& hs, int r, f3 o, f3 d,
             okind = Pn.kind; odepth = Pn.depth; oend = Pn.end; oparent = Pn.parent; ocidx = Pn.cidx;
         }
         const DNode c = S.nodes[i];
-        if (c.kind == HN_LEAF) {
+        bool live;
+        {
+            f3 ro, rd;
+            hs.get_ray(c.depth, ro, rd);
+            live = ray_meets(S.bounds[i].slo, S.bounds[i].shi, ro, rd, INFINITY);
+        }
+        if (!RTX_ANY(live)) {  // shadow_intersect is False for every lane
+            acc = hfold(acc, okind, odepth, c.cidx, false);
+            i = c.end;
+        } else if (c.kind == HN_LEAF) {
             f3 lo, ld;
             hs.get_ray(c.depth, lo, ld);
-            acc = hfold(acc, okind, odepth, c.cidx, leaf_shadow<MESH>(S, S.objs[c.obj], lo, ld, t_max, time));
+            acc = hfold(acc, okind, odepth, c.cidx, live && leaf_shadow<MESH>(S, S.objs[c.obj], lo, ld, t_max, time));
             ++i;
         } else if (c.kind == HN_OTHER) {
             acc = hfold(acc, okind, odepth, c.cidx, false);
             i = c.end;
         } else if (c.kind == HN_DIFF) {
-            acc = hfold(acc, okind, odepth, c.cidx, diff_shadow<MESH>(S, hs, i, time));
+            acc = hfold(acc, okind, odepth, c.cidx, live && diff_shadow<MESH>(S, hs, i, time));
             i = c.end;
         } else {
             f3 ro, rd;
@@ -910,7 +975,9 @@ RTX_HD void hier_closest(const SceneView& S, const HStack& hs, f3 o, f3 d, float
             h.sub = oid;
             hh = HHit{t, pos, n, mat, (ty == OBJ_PLANE || ty == OBJ_BOX) ? leaf : -1};
         };
-        hier_enum<MESH>(S, hs, r, time, want, take);
+        // a hit can win only at t <= the current best (the box test pads far beyond rounding)
+        auto cap = [&]() { return h.t32; };
+        hier_enum<MESH>(S, hs, r, time, want, take, cap);
     }
 }
 

@@ -61,6 +61,9 @@ extern "C" int rtx_hostemu_render(const rtx_scene_desc* sd, const rtx_camera_des
     bind_view(H, k.S);
     std::vector<float> times(cd->n_times);
     for (int i = 0; i < cd->n_times; ++i) times[i] = (float)cd->times[i];
+    const auto mm = std::minmax_element(times.begin(), times.end());
+    const std::vector<DBound> bounds = compute_bounds(H.nodes, H.objs, H.tris, *mm.first, *mm.second);
+    k.S.bounds = (cptr<DBound>)bounds.data();
     std::vector<float> noise;
     const size_t nsamp = (size_t)cd->n_dof * cd->n_aa;
     if (cd->jitter == RTX_JITTER_REPLAY) noise.assign(cd->noise, cd->noise + 3 * (size_t)cd->ncols * cd->height * nsamp);
@@ -100,6 +103,8 @@ extern "C" int rtx_hostemu_intersect(const rtx_scene_desc* sd, int64_t n, const 
     if (rc) return rc;
     SceneView v;
     bind_view(H, v);
+    const std::vector<DBound> bounds = compute_bounds(H.nodes, H.objs, H.tris, (float)time, (float)time);
+    v.bounds = (cptr<DBound>)bounds.data();
     for (int64_t i = 0; i < n; ++i) {
         const f3 o = mk(ro[i], ro[n + i], ro[2 * n + i]);
         const f3 d = mk(rd[i], rd[n + i], rd[2 * n + i]);
@@ -133,6 +138,8 @@ extern "C" int rtx_hostemu_occluded(const rtx_scene_desc* sd, int64_t n, const f
     if (rc) return rc;
     SceneView v;
     bind_view(H, v);
+    const std::vector<DBound> bounds = compute_bounds(H.nodes, H.objs, H.tris, (float)time, (float)time);
+    v.bounds = (cptr<DBound>)bounds.data();
     for (int64_t i = 0; i < n; ++i) {
         const f3 o = mk(ro[i], ro[n + i], ro[2 * n + i]);
         const f3 d = mk(rd[i], rd[n + i], rd[2 * n + i]);
