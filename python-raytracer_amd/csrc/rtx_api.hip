@@ -474,9 +474,28 @@ std::vector<DBound> compute_bounds(const std::vector<DNode>& nodes, const std::v
         }
         nb[x] = NodeBoxes{hb_xform(X.M, r.h), hb_xform(X.M, r.i), hb_xform(X.M, r.s)};
     }
+    // The culling box of a child also carries its parent's filter on the child's hits:
+    // intersection keeps hits inside every sibling, difference keeps child-1 hits inside
+    // child 0 (hierarchy.py:52-70); both are boxes in the child's (parent) frame.
+    std::vector<HBox> hcull(n);
+    for (int x = 0; x < n; ++x) hcull[x] = nb[x].h;
+    for (int x = 0; x < n; ++x) {
+        const DNode& X = nodes[x];
+        if (X.kind != HN_INTER && X.kind != HN_DIFF) continue;
+        std::vector<int> ch;
+        for (int j = x + 1; j < X.end; j = nodes[j].end) ch.push_back(j);
+        for (size_t a = 0; a < ch.size(); ++a) {
+            if (X.kind == HN_INTER) {
+                for (size_t b = 0; b < ch.size(); ++b)
+                    if (b != a) hcull[ch[a]] = hb_inter(hcull[ch[a]], nb[ch[b]].i);
+            } else if (a == 1) {
+                hcull[ch[1]] = hb_inter(hcull[ch[1]], nb[ch[0]].i);
+            }
+        }
+    }
     std::vector<DBound> out(n);
     for (int x = 0; x < n; ++x) {
-        hb_store(nb[x].h, out[x].hlo, out[x].hhi);
+        hb_store(hcull[x], out[x].hlo, out[x].hhi);
         hb_store(nb[x].i, out[x].ilo, out[x].ihi);
         hb_store(nb[x].s, out[x].slo, out[x].shi);
     }

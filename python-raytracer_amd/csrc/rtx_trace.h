@@ -163,8 +163,9 @@ constexpr int kMaxHLevels = 16;  // hierarchy depth limit (levels of the ray/poi
 
 // Conservative regions of a hierarchy subtree, in its parent's frame, for the frame's
 // motion-time range (computed on the host, padded far beyond fp32 rounding): every
-// surviving intersect() hit lies in h, is_inside() can only be true in i, and
-// shadow_intersect() can only be true for a ray that meets s. Empty: lo > hi.
+// intersect() hit of the subtree that also passes its parent's filter lies in h,
+// is_inside() can only be true in i, and shadow_intersect() can only be true for a ray
+// that meets s. Empty: lo > hi.
 struct alignas(16) DBound {
     float hlo[4], hhi[4];
     float ilo[4], ihi[4];
@@ -173,6 +174,8 @@ struct alignas(16) DBound {
 
 template <class T>
 using cptr = const T RTX_CONST*;
+template <class T>
+using cref = const T RTX_CONST&;  // a record read field by field where it is used
 
 struct SceneView {
     cptr<DObj> objs;   // [planes | spheres | boxes | meshes]
@@ -205,7 +208,8 @@ RTX_HD void tally_inc(Tally& t, uint32_t Tally::*field) {
 }
 
 // ------------------------------------------------------------------ geometry helpers
-RTX_HD f3 moved(const DObj& o, const float* p, float time) {
+template <class O, class P>
+RTX_HD f3 moved(const O& o, P p, float time) {
     // `p + self.speed * self.scene.current_time` (simple_geometry.py:21-24, :106-109, :189-194)
     f3 q = ld3(p);
     if (o.has_speed) q = add(q, scale(ld3(o.speed), time));
@@ -228,7 +232,8 @@ RTX_HD int32_t floor_diff(float a, float b) {
 
 // Plane.get_material (simple_geometry.py:133-148): checker by floor of the projected
 // coordinates, Python modulo.
-RTX_HD int32_t plane_material(const DObj& ob, f3 point, float time) {
+template <class O>
+RTX_HD int32_t plane_material(const O& ob, f3 point, float time) {
     if (ob.nmat == 1) return ob.mat0;
     f3 position = moved(ob, ob.a, time);
     f3 n = ld3(ob.b);
@@ -240,7 +245,8 @@ RTX_HD int32_t plane_material(const DObj& ob, f3 point, float time) {
 }
 
 // Barycentric smooth normal (mesh.py:103-113; igl.barycentric_coordinates_tri on fp32 rows).
-RTX_HD f3 smooth_normal(const DTri& T, const DTriN& N, f3 p) {
+template <class TT>
+RTX_HD f3 smooth_normal(const TT& T, const DTriN& N, f3 p) {
     f3 a = ld3(T.v0), b = ld3(T.v1), c = ld3(T.v2);
     f3 v0 = sub(b, a), v1 = sub(c, a), v2 = sub(p, a);
     float d00 = dot(v0, v0), d01 = dot(v0, v1), d11 = dot(v1, v1);
@@ -380,7 +386,8 @@ RTX_HD bool box_slabs(f3 o, f3 d, f3 mn, f3 mx, double& start, int& label, doubl
 }
 
 // Mesh bounding volume (bounding_volumes.py:18-37 sphere, :49-83 AABB).
-RTX_HD bool mesh_bv(const DObj& ob, f3 o, f3 d) {
+template <class O>
+RTX_HD bool mesh_bv(const O& ob, f3 o, f3 d) {
     if (ob.bv_type == BV_AABB) {
         double start, end;
         int label;
@@ -483,14 +490,16 @@ RTX_HD double py_mod(double x, double m) {
 // texture.getpixel((i, j)) with int() / float truncation; the reference raises for an
 // index outside the image (only reachable through `x % w == w` rounding or NaN), the
 // device reads texel 0 of that row/column instead.
-RTX_HD f3 texel(const SceneView& S, const DObj& ob, double fi, double fj) {
+template <class O>
+RTX_HD f3 texel(const SceneView& S, const O& ob, double fi, double fj) {
     const int i = (fi > -1.0 && fi < (double)ob.tex_w) ? (int)fi : 0;
     const int j = (fj > -1.0 && fj < (double)ob.tex_h) ? (int)fj : 0;
     const uint32_t t = S.texels[ob.tex_off + j * ob.tex_w + i];
     return f3{S.lut255[t & 255u], S.lut255[(t >> 8) & 255u], S.lut255[(t >> 16) & 255u]};
 }
 // Plane.get_diffuse (simple_geometry.py:150-173); the projection uses the unmoved point.
-RTX_HD f3 plane_diffuse(const SceneView& S, const DObj& ob, f3 point, float time) {
+template <class O>
+RTX_HD f3 plane_diffuse(const SceneView& S, const O& ob, f3 point, float time) {
     if (!ob.has_tex) return ld3(S.mats[plane_material(ob, point, time)].diffuse);
     const f3 position = moved(ob, ob.a, time);
     const f3 n = ld3(ob.b);
@@ -500,7 +509,8 @@ RTX_HD f3 plane_diffuse(const SceneView& S, const DObj& ob, f3 point, float time
     return texel(S, ob, trunc(py_mod(u, (double)ob.tex_w)), trunc(py_mod(v, (double)ob.tex_h)));
 }
 // AABB.get_diffuse (simple_geometry.py:312-355), fp64 like the reference's Python floats.
-RTX_HD f3 box_diffuse(const SceneView& S, const DObj& ob, f3 point, float time) {
+template <class O>
+RTX_HD f3 box_diffuse(const SceneView& S, const O& ob, f3 point, float time) {
     if (!ob.has_tex) return ld3(S.mats[ob.mat0].diffuse);
     const f3 mn = moved(ob, ob.a, time), mx = moved(ob, ob.b, time);
     const double px = point.x, py = point.y, pz = point.z;
@@ -524,7 +534,8 @@ RTX_HD f3 box_diffuse(const SceneView& S, const DObj& ob, f3 point, float time) 
 }
 // Geometry.get_diffuse as _compute_regular_lighting calls it for Plane/AABB hits
 // (scene.py:143-146); other geometry uses the hit material's diffuse.
-RTX_HD f3 get_diffuse(const SceneView& S, const DObj& ob, f3 point, float time) {
+template <class O>
+RTX_HD f3 get_diffuse(const SceneView& S, const O& ob, f3 point, float time) {
     return ob.type == OBJ_PLANE ? plane_diffuse(S, ob, point, time) : box_diffuse(S, ob, point, time);
 }
 
@@ -559,7 +570,8 @@ struct HStack {
 };
 
 // glm.vec3(m * glm.vec4(p, w)): GLM's mat4 * vec4 is (m[0] x + m[1] y) + (m[2] z + m[3] w).
-RTX_HD f3 xform(const float* m, f3 p, float w) {
+template <class P>
+RTX_HD f3 xform(P m, f3 p, float w) {
     float r[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) r[k] = (m[k] * p.x + m[4 + k] * p.y) + (m[8 + k] * p.z + m[12 + k] * w);
@@ -567,7 +579,8 @@ RTX_HD f3 xform(const float* m, f3 p, float w) {
 }
 // glm.normalize(glm.transpose(Minv) * glm.vec4(n, 0)).xyz (hierarchy.py:76): the
 // normalisation is over all four components (vec4 dot = (x*x + y*y) + (z*z + w*w)).
-RTX_HD f3 normal_xform(const float* mi, f3 n) {
+template <class P>
+RTX_HD f3 normal_xform(P mi, f3 n) {
     float o[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -586,8 +599,8 @@ RTX_HD f3 box_normal(int label, f3 d) {
 
 // Every hit of one leaf, in the reference's list order, with fp64 t (leaves of
 // hierarchies are few: no fp32 proxies). emit(t64, position, normal, material).
-template <bool MESH, class Emit>
-RTX_HD void leaf_hits(const SceneView& S, const DObj& ob, f3 o, f3 d, float time, Emit&& emit) {
+template <bool MESH, class O, class Emit>
+RTX_HD void leaf_hits(const SceneView& S, const O& ob, f3 o, f3 d, float time, Emit&& emit) {
     if (ob.type == OBJ_SPHERE) {  // simple_geometry.py:20-46
         const f3 c = moved(ob, ob.a, time);
         double b, s, two_a;
@@ -614,7 +627,7 @@ RTX_HD void leaf_hits(const SceneView& S, const DObj& ob, f3 o, f3 d, float time
     } else if (MESH && ob.type == OBJ_MESH) {  // mesh.py:72-119, faces in OBJ order
         if (!mesh_bv(ob, o, d)) return;
         for (int f = 0; f < ob.tri_count; ++f) {
-            const DTri T = S.tris[ob.tri_begin + f];
+            cref<DTri> T = S.tris[ob.tri_begin + f];
             const f3 n = ld3(T.n);
             const float den = dot(d, n);
             if (fabsf(den) < kEps4Up) continue;
@@ -630,8 +643,8 @@ RTX_HD void leaf_hits(const SceneView& S, const DObj& ob, f3 o, f3 d, float time
 }
 
 // Leaf shadow_intersect (simple_geometry.py:48-72, :122-131, :251-294; mesh.py:121-153).
-template <bool MESH>
-RTX_HD bool leaf_shadow(const SceneView& S, const DObj& ob, f3 o, f3 d, double t_max, float time) {
+template <bool MESH, class O>
+RTX_HD bool leaf_shadow(const SceneView& S, const O& ob, f3 o, f3 d, double t_max, float time) {
     if (ob.type == OBJ_SPHERE) {
         double b, s, two_a;
         if (!sphere_roots(o, d, moved(ob, ob.a, time), ob.r2, b, s, two_a)) return false;
@@ -657,7 +670,7 @@ RTX_HD bool leaf_shadow(const SceneView& S, const DObj& ob, f3 o, f3 d, double t
     if (MESH && ob.type == OBJ_MESH) {
         if (!mesh_bv(ob, o, d)) return false;
         for (int f = 0; f < ob.tri_count; ++f) {
-            const DTri T = S.tris[ob.tri_begin + f];
+            cref<DTri> T = S.tris[ob.tri_begin + f];
             const f3 n = ld3(T.nu);
             const float den = dot(d, n);
             if (fabsf(den) < kEps4Up) continue;
@@ -675,7 +688,8 @@ RTX_HD bool leaf_shadow(const SceneView& S, const DObj& ob, f3 o, f3 d, double t
 
 // Leaf is_inside: Sphere (simple_geometry.py:74-80, fp32 length vs the fp64 radius),
 // AABB (:296-307); Plane and Mesh keep Geometry's False.
-RTX_HD bool leaf_inside(const DObj& ob, f3 p, float time) {
+template <class O>
+RTX_HD bool leaf_inside(const O& ob, f3 p, float time) {
     if (ob.type == OBJ_SPHERE) {
         const f3 q = sub(p, moved(ob, ob.a, time));
         return (double)sqrtf(dot(q, q)) < ob.radius;
@@ -698,6 +712,15 @@ RTX_HD uint32_t hfold(uint32_t acc, int32_t pk, int32_t pd, int32_t cidx, bool v
 RTX_HD uint32_t hinit(uint32_t acc, int32_t kind, int32_t depth) {
     const uint32_t bit = 1u << depth;
     return kind == HN_INTER ? (acc | bit) : (acc & ~bit);
+}
+// The remaining children of an open node (kind k, depth dep) cannot change its value in
+// any active lane: a union already true, an intersection already false, a difference
+// false after child 0 (next child index nc). Wave-uniform.
+RTX_HD bool hdecided(uint32_t acc, int32_t k, int32_t dep, int32_t nc) {
+    const bool v = ((acc >> dep) & 1u) != 0u;
+    if (k == HN_UNION) return RTX_ALL(v);
+    if (k == HN_INTER || (k == HN_DIFF && nc >= 1)) return RTX_ALL(!v);
+    return false;
 }
 
 // Culling tests against DBound boxes (conservative: a false answer is exact).
@@ -734,10 +757,22 @@ RTX_HD bool pt_in(const float RTX_CONST* lo, const float RTX_CONST* hi, f3 p) {
     return lo[0] <= p.x && p.x <= hi[0] && lo[1] <= p.y && p.y <= hi[1] && lo[2] <= p.z && p.z <= hi[2];
 }
 
+// Inlining of the rarely-divergent CSG helpers (experiment knob; see tools/ablate.sh).
+// 2: everything inlined; 1: is_inside / get_material / walk_up out of line; 0: also
+// hier_closest / hier_shadow.
+#ifndef RTX_HIER_INLINE
+#define RTX_HIER_INLINE 1
+#endif
+#if RTX_HIER_INLINE >= 2
+#define RTX_HX RTX_HD
+#else
+#define RTX_HX __host__ __device__ __attribute__((noinline))
+#endif
+
 // is_inside(x, p) for p in the frame of x's parent's children (hierarchy.py:111-129).
-RTX_HD bool is_inside(const SceneView& S, const HStack& hs, int x, f3 p, float time) {
+RTX_HX bool is_inside(const SceneView& S, const HStack& hs, int x, f3 p, float time) {
     if (!pt_in(S.bounds[x].ilo, S.bounds[x].ihi, p)) return false;
-    const DNode X = S.nodes[x];
+    cref<DNode> X = S.nodes[x];
     if (X.kind == HN_LEAF) return leaf_inside(S.objs[X.obj], p, time);
     if (X.kind == HN_OTHER) return false;
     hs.put_pt(X.depth, xform(X.Minv, p, 1.0f));
@@ -749,13 +784,13 @@ RTX_HD bool is_inside(const SceneView& S, const HStack& hs, int x, f3 p, float t
         while (i >= oend) {  // close finished subtrees
             const bool v = ((acc >> odepth) & 1u) != 0u;
             if (open == x) return v;
-            const DNode Pn = S.nodes[oparent];
+            cref<DNode> Pn = S.nodes[oparent];
             acc = hfold(acc, Pn.kind, Pn.depth, ocidx, v);
             open = oparent;
             okind = Pn.kind; odepth = Pn.depth; oend = Pn.end; oparent = Pn.parent; ocidx = Pn.cidx;
         }
-        const DNode c = S.nodes[i];
-        if (okind == HN_DIFF && c.cidx >= 2) { i = c.end; continue; }
+        cref<DNode> c = S.nodes[i];
+        if ((okind == HN_DIFF && c.cidx >= 2) || hdecided(acc, okind, odepth, c.cidx)) { i = oend; continue; }
         if (c.kind == HN_LEAF) {
             acc = hfold(acc, okind, odepth, c.cidx, leaf_inside(S.objs[c.obj], hs.get_pt(odepth), time));
             ++i;
@@ -774,11 +809,11 @@ RTX_HD bool is_inside(const SceneView& S, const HStack& hs, int x, f3 p, float t
 
 // get_material(x, p) (hierarchy.py:131-138, Plane.get_material, Geometry.get_material):
 // the first child containing the point, recursively; -1 = None.
-RTX_HD int32_t get_material(const SceneView& S, const HStack& hs, int x, f3 p, float time) {
+RTX_HX int32_t get_material(const SceneView& S, const HStack& hs, int x, f3 p, float time) {
     for (;;) {
-        const DNode X = S.nodes[x];
+        cref<DNode> X = S.nodes[x];
         if (X.kind == HN_LEAF) {
-            const DObj ob = S.objs[X.obj];
+            cref<DObj> ob = S.objs[X.obj];
             return ob.type == OBJ_PLANE ? plane_material(ob, p, time) : ob.mat0;
         }
         const f3 q = xform(X.Minv, p, 1.0f);
@@ -796,12 +831,12 @@ RTX_HD int32_t get_material(const SceneView& S, const HStack& hs, int x, f3 p, f
 // hits outside child 1 and child-1 hits inside child 0 (material of child 0, normal
 // negated), then None materials fall back to the node's and position/normal move to the
 // parent frame (hierarchy.py:49-76). Returns false if a filter drops the hit.
-RTX_HD bool walk_up(const SceneView& S, const HStack& hs, int cur, int stop, float time, f3& pos, f3& n,
+RTX_HX bool walk_up(const SceneView& S, const HStack& hs, int cur, int stop, float time, f3& pos, f3& n,
                     int32_t& mat) {
     while (cur != stop) {
-        const DNode c = S.nodes[cur];
+        cref<DNode> c = S.nodes[cur];
         const int a = c.parent;
-        const DNode A = S.nodes[a];
+        cref<DNode> A = S.nodes[a];
         if (A.kind == HN_INTER) {
             for (int j = a + 1; j < A.end; j = S.nodes[j].end)
                 if (j != cur && !is_inside(S, hs, j, pos, time)) return false;
@@ -834,12 +869,12 @@ RTX_HD void hier_enum(const SceneView& S, const HStack& hs, int s, float time, W
         hs.get_ray(depth, ro, rd);
         return !RTX_ANY(ray_meets(S.bounds[c].hlo, S.bounds[c].hhi, ro, rd, cap()));
     };
-    const DNode root = S.nodes[s];
+    cref<DNode> root = S.nodes[s];
     if (culled(s, root.depth)) return;
     auto visit_leaf = [&](int li, int32_t depth, int32_t obj) {
         f3 lo, ld;
         hs.get_ray(depth, lo, ld);
-        const DObj ob = S.objs[obj];
+        cref<DObj> ob = S.objs[obj];
         leaf_hits<MESH>(S, ob, lo, ld, time, [&](double t, f3 pos, f3 n, int32_t mat) {
             if (!want(t)) return;
             if (walk_up(S, hs, li, s, time, pos, n, mat)) take(t, pos, n, mat, obj);
@@ -853,7 +888,7 @@ RTX_HD void hier_enum(const SceneView& S, const HStack& hs, int s, float time, W
         hs.put_ray(root.depth + 1, xform(root.Minv, ro, 1.0f), xform(root.Minv, rd, 0.0f));
     }
     for (int i = s + 1; i < root.end;) {
-        const DNode c = S.nodes[i];
+        cref<DNode> c = S.nodes[i];
         if (c.pkind == HN_DIFF && c.cidx >= 2) { i = c.end; continue; }  // difference reads children 0, 1
         if (culled(i, c.depth)) { i = c.end; continue; }
         if (c.kind == HN_LEAF) { visit_leaf(i, c.depth, c.obj); ++i; continue; }
@@ -869,7 +904,7 @@ RTX_HD void hier_enum(const SceneView& S, const HStack& hs, int s, float time, W
 // the shadow epsilon that the other child does not veto; no t_max test.
 template <bool MESH>
 RTX_HD bool diff_shadow(const SceneView& S, const HStack& hs, int x, float time) {
-    const DNode X = S.nodes[x];
+    cref<DNode> X = S.nodes[x];
     {
         f3 ro, rd;
         hs.get_ray(X.depth, ro, rd);
@@ -888,11 +923,16 @@ RTX_HD bool diff_shadow(const SceneView& S, const HStack& hs, int x, float time)
 
 // Hierarchy.shadow_intersect of root r for the world ray (o, d): union = any child,
 // intersection = every child (each tested on its own), difference = diff_shadow.
+#if RTX_HIER_INLINE >= 1
+#define RTX_HY RTX_HD
+#else
+#define RTX_HY __host__ __device__ __attribute__((noinline))
+#endif
 template <bool MESH>
-RTX_HD bool hier_shadow(const SceneView& S, const HStack& hs, int r, f3 o, f3 d, double t_max, float time) {
+RTX_HY bool hier_shadow(const SceneView& S, const HStack& hs, int r, f3 o, f3 d, double t_max, float time) {
     hs.put_ray(0, o, d);
     if (!RTX_ANY(ray_meets(S.bounds[r].slo, S.bounds[r].shi, o, d, INFINITY))) return false;
-    const DNode R = S.nodes[r];
+    cref<DNode> R = S.nodes[r];
     if (R.kind == HN_OTHER) return false;
     if (R.kind == HN_DIFF) return diff_shadow<MESH>(S, hs, r, time);
     hs.put_ray(1, xform(R.Minv, o, 1.0f), xform(R.Minv, d, 0.0f));
@@ -904,12 +944,13 @@ RTX_HD bool hier_shadow(const SceneView& S, const HStack& hs, int r, f3 o, f3 d,
         while (i >= oend) {
             const bool v = ((acc >> odepth) & 1u) != 0u;
             if (open == r) return v;
-            const DNode Pn = S.nodes[oparent];
+            cref<DNode> Pn = S.nodes[oparent];
             acc = hfold(acc, Pn.kind, Pn.depth, ocidx, v);
             open = oparent;
             okind = Pn.kind; odepth = Pn.depth; oend = Pn.end; oparent = Pn.parent; ocidx = Pn.cidx;
         }
-        const DNode c = S.nodes[i];
+        cref<DNode> c = S.nodes[i];
+        if (hdecided(acc, okind, odepth, c.cidx)) { i = oend; continue; }
         bool live;
         {
             f3 ro, rd;
@@ -953,7 +994,7 @@ struct HHit {
 // Closest hit over the hierarchies, merged into h (flat objects done): a candidate wins
 // with a smaller t, or an equal t and an earlier top-level object (scene.py:94).
 template <bool MESH>
-RTX_HD void hier_closest(const SceneView& S, const HStack& hs, f3 o, f3 d, float time, Hit& h, HHit& hh) {
+RTX_HY void hier_closest(const SceneView& S, const HStack& hs, f3 o, f3 d, float time, Hit& h, HHit& hh) {
     hs.put_ray(0, o, d);
     for (int r = 0; r < S.n_nodes; r = S.nodes[r].end) {
         const int32_t oid = S.nodes[r].oid;
@@ -1051,7 +1092,7 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
             }
         }
     }
-    if (X) hier_closest<MESH>(S, hs, o, d, time, h, hh);  // hierarchies (hierarchy.py:42-78)
+    if (X && RTX_ABLATE != 9) hier_closest<MESH>(S, hs, o, d, time, h, hh);  // hierarchies (hierarchy.py:42-78)
     return h;
 }
 
@@ -1130,7 +1171,7 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
             }
         }
     }
-    if (X) {  // hierarchies (hierarchy.py:80-109)
+    if (X && RTX_ABLATE != 10) {  // hierarchies (hierarchy.py:80-109)
         for (int r = 0; r < S.n_nodes; r = S.nodes[r].end) {
             if (RTX_ALL(occ)) break;
             if (!occ) occ = hier_shadow<MESH>(S, hs, r, o, d, t_max, time);
