@@ -39,10 +39,28 @@ CONFIGS = {
     "ns1": ("NovelScene1", (2048, 1024), None, "NovelScene1 2048x1024 AA32 jittered (CSG hierarchies + textures)"),
     "ns2": ("NovelScene2", (1024, 512), None,
             "NovelScene2 1024x512 AA2 x DOF15 x 16 motion times, jittered (CSG hierarchies + textures)"),
+    "blob1080": ("blob", (1920, 1080), None,
+                 "81,920-face smooth mesh 1920x1080 1spp (bunny-sized stand-in; reference bunny.obj is absent)"),
 }
 # CPU-baseline sub-sampling for the configs whose full frame takes minutes on one core:
 # the first of N column strips (np.array_split(arange(W), N)[0]) per repeat.
-CPU_STRIPS = {"tm1080": 16, "dof4k": 16, "ns1": 32, "ns2": 128}
+CPU_STRIPS = {"tm1080": 16, "dof4k": 16, "ns1": 32, "ns2": 128, "blob1080": 64}
+
+
+def scene_dict(cfg):
+    """(scene dict, asset dir) of a config: a bundled scene, or the synthetic large mesh."""
+    name, res, spp, _ = CONFIGS[cfg]
+    if name == "blob":
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        from scenegen import blob_obj, blob_scene
+        path = os.path.join("/tmp", "rtx_blob6_%d.obj" % os.getpid())
+        if not os.path.exists(path):
+            blob_obj(path, level=6)
+        return blob_scene(path, res), os.path.dirname(path)
+    from rtx.io import bundled_scene_dict
+    d = bundled_scene_dict(name, resolution=res, spp=spp)
+    base = d.pop("__base_dir__")
+    return d, base
 
 
 def parse():
@@ -73,11 +91,11 @@ def pmc_traffic(path):
 
 def make_scene(cfg):
     import rtx
-    name, res, spp, _ = CONFIGS[cfg]
-    kw = dict(resolution=res, spp=spp)
+    d, base = scene_dict(cfg)
     if cfg == "dof4k":
-        kw["AA"] = {"jitter": True, "samples": spp[0]}
-    return rtx.load_bundled_scene(name, **kw)
+        d["AA"] = {"jitter": True, "samples": CONFIGS[cfg][2][0]}
+    d["__base_dir__"] = base
+    return rtx.load_scene(d, verbose=False)
 
 
 def cpu_baseline(cfg, budget_s):
@@ -85,10 +103,7 @@ def cpu_baseline(cfg, budget_s):
     full frames, repeated until the budget is used (whole frames only)."""
     from oracle import oracle as O
     name, res, spp, _ = CONFIGS[cfg]
-    d, base = O.load_bundle(name)
-    d["resolution"] = list(res)
-    if spp is not None:
-        d.setdefault("AA", {"jitter": False, "samples": 1})["samples"] = spp[0]
+    d, base = scene_dict(cfg)
     osc = O.OracleScene(d, base)
     W, H = res
     rows = H

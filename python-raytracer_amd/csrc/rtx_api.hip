@@ -15,6 +15,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -726,8 +727,9 @@ int convert_scene(const rtx_scene_desc* desc, HostScene& H) {
     all_objs.swap(H.objs);
     H.objs.swap(grouped);
     H.n_plane = counts[0]; H.n_sphere = counts[1]; H.n_box = counts[2]; H.n_mesh = counts[3];
-    // Mesh face clusters: reorder each mesh's faces into spatially coherent leaves of <= 8
-    // faces (median splits on face centroids) and record each face's OBJ order index.
+    // Mesh BVH: median splits on face centroids down to clusters of <= 8 faces, stored in
+    // preorder with skip indices (stackless traversal); faces are reordered by cluster and
+    // keep their OBJ order index (tri_orig) for closest-hit ties.
     H.tri_orig.assign(desc->n_triangles, 0);
     for (DObj& d : H.objs) {
         if (d.type != RTX_MESH) continue;
@@ -738,55 +740,65 @@ int convert_scene(const rtx_scene_desc* desc, HostScene& H) {
             const DTri& t = H.tris[b0 + i];
             return (double)t.v0[ax] + (double)t.v1[ax] + (double)t.v2[ax];
         };
-        const int32_t leaf0 = (int32_t)H.leaves.size();
-        std::vector<std::pair<int32_t, int32_t>> stack{{0, n}};
-        std::vector<std::pair<int32_t, int32_t>> ranges;
-        while (!stack.empty()) {
-            auto [a, e] = stack.back();
-            stack.pop_back();
-            if (e - a <= 8) { ranges.push_back({a, e}); continue; }
-            double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-            for (int32_t k = a; k < e; ++k)
-                for (int ax = 0; ax < 3; ++ax) {
-                    const double c = centroid(idx[k], ax);
-                    lo[ax] = std::min(lo[ax], c);
-                    hi[ax] = std::max(hi[ax], c);
+        const int32_t node0 = (int32_t)H.leaves.size();
+        float cmax = 0.0f;
+        std::function<void(int32_t, int32_t)> build = [&](int32_t a, int32_t e) {
+            const int32_t me = (int32_t)H.leaves.size();
+            H.leaves.push_back(DLeaf{});
+            DLeaf L{};
+            for (int ax = 0; ax < 3; ++ax) { L.lo[ax] = INFINITY; L.hi[ax] = -INFINITY; }
+            if (e - a <= 8) {
+                L.first = a;
+                L.count = e - a;
+                for (int32_t k = a; k < e; ++k) {
+                    const DTri& t = H.tris[b0 + idx[k]];
+                    for (const float* v : {t.v0, t.v1, t.v2})
+                        for (int ax = 0; ax < 3; ++ax) {
+                            L.lo[ax] = std::min(L.lo[ax], v[ax]);
+                            L.hi[ax] = std::max(L.hi[ax], v[ax]);
+                            cmax = std::max(cmax, std::fabs(v[ax]));
+                        }
                 }
-            int ax = 0;
-            for (int q = 1; q < 3; ++q)
-                if (hi[q] - lo[q] > hi[ax] - lo[ax]) ax = q;
-            const int32_t mid = (a + e) / 2;
-            std::nth_element(idx.begin() + a, idx.begin() + mid, idx.begin() + e,
-                             [&](int32_t x, int32_t y) { return centroid(x, ax) < centroid(y, ax); });
-            stack.push_back({mid, e});
-            stack.push_back({a, mid});
-        }
+            } else {
+                double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+                for (int32_t k = a; k < e; ++k)
+                    for (int ax = 0; ax < 3; ++ax) {
+                        const double c = centroid(idx[k], ax);
+                        lo[ax] = std::min(lo[ax], c);
+                        hi[ax] = std::max(hi[ax], c);
+                    }
+                int ax = 0;
+                for (int q = 1; q < 3; ++q)
+                    if (hi[q] - lo[q] > hi[ax] - lo[ax]) ax = q;
+                const int32_t mid = (a + e) / 2;
+                std::nth_element(idx.begin() + a, idx.begin() + mid, idx.begin() + e,
+                                 [&](int32_t x, int32_t y) { return centroid(x, ax) < centroid(y, ax); });
+                const int32_t left = me + 1;
+                build(a, mid);
+                const int32_t right = (int32_t)H.leaves.size();
+                build(mid, e);
+                L.first = -1;
+                L.count = 0;
+                for (int q = 0; q < 3; ++q) {
+                    L.lo[q] = std::min(H.leaves[left].lo[q], H.leaves[right].lo[q]);
+                    L.hi[q] = std::max(H.leaves[left].hi[q], H.leaves[right].hi[q]);
+                }
+            }
+            L.skip = (int32_t)H.leaves.size() - node0;  // next node after this subtree (mesh-relative)
+            H.leaves[me] = L;
+        };
+        if (n > 0) build(0, n);
         std::vector<DTri> tris(n);
         std::vector<DTriN> trins(n);
-        float cmax = 0.0f;
-        for (auto [a, e] : ranges) {
-            DLeaf L;
-            L.first = a;
-            L.count = e - a;
-            for (int ax = 0; ax < 3; ++ax) { L.lo[ax] = INFINITY; L.hi[ax] = -INFINITY; }
-            for (int32_t k = a; k < e; ++k) {
-                const DTri& t = H.tris[b0 + idx[k]];
-                tris[k] = t;
-                trins[k] = H.trins[b0 + idx[k]];
-                H.tri_orig[b0 + k] = idx[k];
-                for (const float* v : {t.v0, t.v1, t.v2})
-                    for (int ax = 0; ax < 3; ++ax) {
-                        L.lo[ax] = std::min(L.lo[ax], v[ax]);
-                        L.hi[ax] = std::max(L.hi[ax], v[ax]);
-                        cmax = std::max(cmax, std::fabs(v[ax]));
-                    }
-            }
-            H.leaves.push_back(L);
+        for (int32_t k = 0; k < n; ++k) {
+            tris[k] = H.tris[b0 + idx[k]];
+            trins[k] = H.trins[b0 + idx[k]];
+            H.tri_orig[b0 + k] = idx[k];
         }
         std::copy(tris.begin(), tris.end(), H.tris.begin() + b0);
         std::copy(trins.begin(), trins.end(), H.trins.begin() + b0);
-        d.leaf_begin = leaf0;
-        d.leaf_count = (int32_t)H.leaves.size() - leaf0;
+        d.leaf_begin = node0;
+        d.leaf_count = (int32_t)H.leaves.size() - node0;
         d.cmax = cmax;
     }
     // Hierarchies: the subtrees of the top-level nodes, in preorder, as DNode records;

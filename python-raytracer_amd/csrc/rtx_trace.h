@@ -90,7 +90,7 @@ RTX_HD f3 clamp01(f3 c) { return f3{clamp01(c.x), clamp01(c.y), clamp01(c.z)}; }
 struct alignas(16) DObj {
     int32_t type, nmat, mat0, mat1;
     int32_t has_speed, tri_begin, tri_count, bv_type;
-    int32_t flat, oid, leaf_begin, leaf_count;   // mesh: face clusters (DLeaf range)
+    int32_t flat, oid, leaf_begin, leaf_count;   // mesh: BVH nodes (DLeaf range, preorder)
     float cmax, pad3, pad4, pad5;                // mesh: max |vertex coordinate|
     float a[4];       // sphere centre | plane point | box minpos
     float b[4];       // plane normal | box maxpos
@@ -117,14 +117,16 @@ struct alignas(16) DTriN {
     float n0[4], n1[4], n2[4];     // smooth vertex normals (mesh.py:53-70)
 };
 
-// A cluster of <= 8 spatially sorted faces of one mesh with the bounds of their vertices.
-// Used only to skip faces conservatively (see leaf_maybe_hit); faces keep their original
-// index for tie breaks (tri_orig).
+// A mesh BVH node in preorder: the bounds of the vertices of its faces; a leaf holds a
+// cluster of <= 8 spatially sorted faces (count > 0), an internal node's children follow
+// it. Used only to skip faces conservatively (see leaf_maybe_hit); faces keep their
+// original index for tie breaks (tri_orig).
 struct alignas(16) DLeaf {
     float lo[3];
-    int32_t first;                 // into the mesh's (cluster-ordered) faces
+    int32_t first;                 // leaf: into the mesh's (cluster-ordered) faces
     float hi[3];
-    int32_t count;
+    int32_t count;                 // 0: internal node
+    int32_t skip, pad0, pad1, pad2;  // the node after this subtree (relative to the mesh's first)
 };
 
 struct alignas(16) DMat {
@@ -415,14 +417,17 @@ RTX_HD RayInv ray_inv(f3 o, f3 d) {
     r.pad_rel = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
     return r;
 }
-RTX_HD bool leaf_maybe_hit(const DLeaf& L, f3 o, const RayInv& ri, float cmax) {
+// tcap: the ray's current best t (closest hit) -- a face beyond it cannot win; the
+// padded box's entry precedes every face hit inside it.
+template <class L_>
+RTX_HD bool leaf_maybe_hit(const L_& L, f3 o, const RayInv& ri, float cmax, float tcap = INFINITY) {
     const float pad = 0x1p-16f * (ri.pad_rel + cmax);
     const float tx1 = (L.lo[0] - pad - o.x) * ri.inv.x, tx2 = (L.hi[0] + pad - o.x) * ri.inv.x;
     const float ty1 = (L.lo[1] - pad - o.y) * ri.inv.y, ty2 = (L.hi[1] + pad - o.y) * ri.inv.y;
     const float tz1 = (L.lo[2] - pad - o.z) * ri.inv.z, tz2 = (L.hi[2] + pad - o.z) * ri.inv.z;
     const float tn = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
     const float tf = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
-    return tf >= tn && tf >= 0.0f;
+    return tf >= tn && tf >= 0.0f && tn <= tcap;
 }
 
 // Exact fp64 t of a candidate, recomputed from the object exactly as during its test
@@ -1068,10 +1073,11 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
             const DObj ob = S.objs[oi];
             if (!mesh_bv(ob, o, d)) continue;  // the reference's bounding volume, quirks included
             const RayInv ri = ray_inv(o, d);
-            for (int li = 0; li < ob.leaf_count; ++li) {
-                const DLeaf L = S.leaves[ob.leaf_begin + li];
-                const bool maybe = leaf_maybe_hit(L, o, ri, ob.cmax);
-                if (!RTX_ANY(maybe)) continue;
+            for (int li = 0; li < ob.leaf_count;) {  // stackless wave-uniform BVH walk
+                cref<DLeaf> L = S.leaves[ob.leaf_begin + li];
+                const bool maybe = leaf_maybe_hit(L, o, ri, ob.cmax, h.t32);
+                if (!RTX_ANY(maybe)) { li = L.skip; continue; }
+                ++li;
                 for (int f = L.first; f < L.first + L.count; ++f) {
                     const DTri T = S.tris[ob.tri_begin + f];
                     tally_inc<COUNT>(tl, &Tally::tri);
@@ -1148,10 +1154,11 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
             const bool live = !occ && mesh_bv(ob, o, d);
             if (!RTX_ANY(live)) continue;
             const RayInv ri = ray_inv(o, d);
-            for (int li = 0; li < ob.leaf_count; ++li) {
-              const DLeaf L = S.leaves[ob.leaf_begin + li];
+            for (int li = 0; li < ob.leaf_count;) {  // stackless wave-uniform BVH walk
+              cref<DLeaf> L = S.leaves[ob.leaf_begin + li];
               const bool maybe = live && !occ && leaf_maybe_hit(L, o, ri, ob.cmax);
-              if (!RTX_ANY(maybe)) continue;
+              if (!RTX_ANY(maybe)) { li = L.skip; continue; }
+              ++li;
               for (int f = L.first; f < L.first + L.count; ++f) {
                 const DTri T = S.tris[ob.tri_begin + f];
                 tally_inc<COUNT>(tl, &Tally::tri);

@@ -147,3 +147,66 @@ def random_hier_scene(seed, res=(48, 36), mesh=False):
     sc["objects"] = [objs[i] for i in order]
     # leaves without materials need a root that has some (else the reference raises)
     return sc
+
+
+def blob_obj(path, level=6, seed=0):
+    """A closed, bumpy triangle mesh (icosphere subdivided `level` times, 20 * 4^level
+    faces, radially displaced by a few smooth waves) written as OBJ: a stand-in of the
+    size of the reference's missing bunny.obj (scenes/TorusMesh.json) for the large-mesh
+    path. Deterministic in (level, seed)."""
+    rng = np.random.RandomState(seed)
+    t = (1.0 + 5 ** 0.5) / 2
+    V = [[-1, t, 0], [1, t, 0], [-1, -t, 0], [1, -t, 0], [0, -1, t], [0, 1, t], [0, -1, -t], [0, 1, -t],
+         [t, 0, -1], [t, 0, 1], [-t, 0, -1], [-t, 0, 1]]
+    Fc = [[0, 11, 5], [0, 5, 1], [0, 1, 7], [0, 7, 10], [0, 10, 11], [1, 5, 9], [5, 11, 4], [11, 10, 2],
+          [10, 7, 6], [7, 1, 8], [3, 9, 4], [3, 4, 2], [3, 2, 6], [3, 6, 8], [3, 8, 9], [4, 9, 5], [2, 4, 11],
+          [6, 2, 10], [8, 6, 7], [9, 8, 1]]
+    V = [list(np.array(v) / np.linalg.norm(v)) for v in V]
+    for _ in range(level):
+        cache = {}
+        nf = []
+
+        def mid(a, b):
+            key = (min(a, b), max(a, b))
+            if key not in cache:
+                m = (np.array(V[a]) + np.array(V[b])) / 2
+                V.append(list(m / np.linalg.norm(m)))
+                cache[key] = len(V) - 1
+            return cache[key]
+        for a, b, c in Fc:
+            ab, bc, ca = mid(a, b), mid(b, c), mid(c, a)
+            nf += [[a, ab, ca], [b, bc, ab], [c, ca, bc], [ab, bc, ca]]
+        Fc = nf
+    V = np.array(V)
+    k = rng.normal(size=(6, 3)) * 2.5
+    ph = rng.uniform(0, 6.28, 6)
+    r = 1.0 + sum(0.06 * np.sin(V @ k[i] + ph[i]) for i in range(6))
+    V = V * r[:, None] * np.array([0.9, 0.8, 0.7])
+    with open(path, "w") as f:
+        for v in V:
+            f.write("v %.6f %.6f %.6f\n" % tuple(v))
+        for a, b, c in Fc:
+            f.write("f %d %d %d\n" % (a + 1, b + 1, c + 1))
+    return len(V), len(Fc)
+
+
+def blob_scene(obj_path, res=(64, 64), flat=False):
+    """The reference's scenes/TorusMesh.json (plane + one mesh, three point lights) with
+    the mesh file replaced by obj_path."""
+    return {"resolution": list(res), "AA": {"jitter": False, "samples": 1}, "ambient": [0.1, 0.1, 0.1],
+            "camera": {"position": [0.0, 4.0, 4.0], "lookAt": [0.0, 0.0, 0.0], "up": [0.0, 1.0, 0.0], "fov": 45.0},
+            "materials": [{"name": "white", "ID": 0, "diffuse": [0.9, 0.9, 0.9], "specular": [0.1, 0.1, 0.1],
+                           "hardness": 8},
+                          {"name": "grey", "ID": 1, "diffuse": [0.3, 0.3, 0.3], "specular": [0.1, 0.1, 0.1]},
+                          {"name": "clay", "ID": 2, "diffuse": [0.8, 0.5, 0.3], "specular": [0.6, 0.6, 0.6],
+                           "hardness": 32}],
+            "objects": [{"name": "plane", "type": "plane", "normal": [0.0, 1.0, 0.0], "position": [0.0, -1.0, 0.0],
+                         "materials": [1, 0]},
+                        {"name": "blob", "type": "mesh", "filepath": obj_path, "scale": 1.0,
+                         "position": [0.0, 0.0, 0.0], "materials": [2], "flat_shaded": bool(flat)}],
+            "lights": [{"name": "light1", "type": "point", "position": [-3.0, 10.0, 1.0], "colour": [1.0, 1.0, 1.0],
+                        "power": 0.5},
+                       {"name": "light2", "type": "point", "position": [3.0, 10.0, 1.0], "colour": [1.0, 1.0, 1.0],
+                        "power": 0.5},
+                       {"name": "light3", "type": "point", "position": [0.0, -5.0, 0.0], "colour": [1.0, 1.0, 1.0],
+                        "power": 10.0}]}

@@ -217,3 +217,15 @@ def test_hierarchy_geometry_kat():
         assert np.array_equal(got["normal"][hit], nn[hit]) and np.array_equal(got["position"][hit], pp[hit])
         for tmax in (1.0, np.inf):
             assert np.array_equal(sc.occluded(o, d, tmax, time), osc.shadow(time, o, d, tmax).astype(bool))
+
+
+@pytest.mark.parametrize("flat", [False, True])
+def test_large_mesh_bvh_matches_oracle(tmp_path, flat):
+    """81,920-face mesh (bunny-sized stand-in) through the device BVH."""
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import blob_obj, blob_scene
+    p = str(tmp_path / "blob6.obj")
+    blob_obj(p, level=6)
+    d = blob_scene(p, (64, 64), flat)
+    s = assert_parity(product_scene_dict(d).render(), oracle_render_dict(d), "blob")
+    assert s["frac_diff"] == 0.0, s

@@ -147,3 +147,42 @@ def test_hostemu_hierarchy_geometry_kat(seed):
         assert np.array_equal(got["position"][hit], pp[hit])
         for tmax in (1.0, np.inf):
             assert np.array_equal(hostemu.occluded(sc, o, d, tmax, time), osc.shadow(time, o, d, tmax).astype(bool))
+
+
+@pytest.fixture(scope="module")
+def blob5(tmp_path_factory):
+    from scenegen import blob_obj
+    p = str(tmp_path_factory.mktemp("mesh") / "blob5.obj")
+    blob_obj(p, level=5)  # 20,480 faces
+    return p
+
+
+@pytest.mark.parametrize("flat", [False, True])
+def test_hostemu_large_mesh_bvh(blob5, flat):
+    """Mesh BVH on a 20k-face mesh: bit-exact image and ray tallies."""
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import blob_scene
+    d = blob_scene(blob5, (40, 40), flat)
+    img, cnt = hostemu.render(product_scene_dict(d))
+    ref, tl = oracle_render_dict(d, tallies=True)
+    assert assert_parity(img, ref)["frac_diff"] == 0.0
+    assert list(cnt[:10]) == tl[:10] and cnt[10] == tl[11]
+
+
+def test_hostemu_large_mesh_kat(blob5):
+    from oracle import oracle as O
+    from common import product_scene_dict
+    from scenegen import blob_scene
+    import os
+    d = blob_scene(blob5)
+    rng = np.random.RandomState(9)
+    o, dd = _rays(rng, 1500, np.array([0, 0, 0]), spread=2.0)
+    sc = product_scene_dict(d)
+    osc = O.OracleScene(d, os.path.dirname(blob5))
+    got = hostemu.intersect(sc, o, dd, 0.0)
+    t, ob, _, m, nn, pp = osc.closest(0.0, o, dd)
+    hit = ob >= 0
+    assert np.array_equal(got["obj"], ob) and np.array_equal(got["t"][hit], t[hit])
+    assert np.array_equal(got["normal"][hit], nn[hit]) and np.array_equal(got["position"][hit], pp[hit])
+    for tmax in (1.0, np.inf):
+        assert np.array_equal(hostemu.occluded(sc, o, dd, tmax, 0.0), osc.shadow(0.0, o, dd, tmax).astype(bool))
