@@ -39,7 +39,9 @@
 #ifndef RTX_H
 #define RTX_H
 
+#if !defined(__HIPCC_RTC__)
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {

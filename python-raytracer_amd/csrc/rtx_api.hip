@@ -10,17 +10,23 @@
 //   k_occluded    shadow any-hit of SoA rays (Geometry.shadow_intersect, scene.py:160-164)
 //   k_to_rgb8     (v * 255.0) truncated to uint8 (main.py:327)
 #include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
 
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <fstream>
 #include <functional>
+#include <map>
+#include <mutex>
+#include <sstream>
 #include <string>
+#include <unistd.h>
 #include <vector>
 
 #include "../../include/rtx.h"
-#include "rtx_trace.h"
+#include "rtx_kernels.h"
 
 using namespace rtx;
 
@@ -39,211 +45,6 @@ int fail(int code, const std::string& msg) {
         if (e_ != hipSuccess)                                                             \
             return fail(RTX_ERR_HIP, std::string(#call ": ") + hipGetErrorString(e_));    \
     } while (0)
-
-struct KParams {
-    SceneView S;
-    // camera tables (device)
-    cptr<float> xs;
-    cptr<float> ys;
-    cptr<float> dof_o;   // [n_dof][3]
-    cptr<float> aa_o;    // [n_dof][n_aa][3]
-    cptr<float> times;   // [n_times] fp32
-    cptr<float> noise;   // replay jitter
-    float pos[4], u[4], v[4], dw[4];
-    float focal, divisor, jscale, inv_divisor;
-    int32_t div_pow2, pad0, pad1, pad2;
-    int32_t width, height, col0, ncols;
-    int32_t n_dof, n_aa, n_times, jitter;
-    uint32_t seed_lo, seed_hi;
-};
-
-template <bool COUNT>
-__device__ __forceinline__ void flush_tally(const Tally& tl, unsigned long long* counters, bool active) {
-    if (!COUNT || counters == nullptr) return;
-    uint32_t vals[RTX_COUNTERS] = {};
-#pragma unroll
-    for (int k = 0; k < kMaxDepth; ++k) vals[k] = active ? tl.cast[k] : 0u;
-    vals[RTX_CNT_SHADOW] = active ? tl.shadow : 0u;
-    vals[RTX_CNT_SHADE] = active ? tl.shade : 0u;
-    vals[RTX_CNT_TRI] = active ? tl.tri : 0u;
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int k = 0; k < RTX_COUNTERS; ++k) {
-        unsigned long long s = vals[k];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-        if (lane == 0 && s) atomicAdd(&counters[k], s);
-    }
-}
-
-// scene.py:47-79 for pixel p of the output block (host/device: the tests-only host
-// emulation runs the same body).
-template <bool MESH, bool SEC, bool X, bool COUNT, bool JIT>
-RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, int32_t cc, Tally& tl,
-                         const FrameStack& fs, const HStack& hs) {
-    const int64_t p = (int64_t)rr * P.ncols + cc;
-    const int j = P.height - 1 - (row0 + rr);  // reference row index (y grows upward)
-    const float fx = P.xs[cc];
-    const float fy = P.ys[j];
-    // base_ray_direction = normalize(x * u + y * v - d * w)  (scene.py:54)
-    const f3 bdir = normalize(sub(add(scale(ld3(P.u), fx), scale(ld3(P.v), fy)), ld3(P.dw)));
-    const f3 focal = add(ld3(P.pos), scale(bdir, P.focal));  // scene.py:55
-    f3 colour = mk(0.0f, 0.0f, 0.0f);
-    for (int kd = 0; kd < P.n_dof; ++kd) {
-        const f3 ddir = normalize(sub(focal, ld3(P.dof_o + 3 * kd)));  // scene.py:58
-        for (int ka = 0; ka < P.n_aa; ++ka) {
-            f3 o = ld3(P.aa_o + 3 * (kd * P.n_aa + ka));
-            if (JIT) {  // scene.py:63-65
-                f3 rnd;
-                if (P.jitter == RTX_JITTER_REPLAY) {
-                    const int64_t idx = (((int64_t)cc * P.height + j) * P.n_dof + kd) * P.n_aa + ka;
-                    rnd = ld3(P.noise + 3 * idx);
-                } else {
-                    uint32_t ctr[4] = {(uint32_t)(P.col0 + cc), (uint32_t)j, (uint32_t)(kd * P.n_aa + ka), 0u};
-                    philox4x32(ctr, P.seed_lo, P.seed_hi);
-                    rnd = mk((float)(ctr[0] >> 8) * 0x1p-24f, (float)(ctr[1] >> 8) * 0x1p-24f,
-                             (float)(ctr[2] >> 8) * 0x1p-24f);
-                }
-                o = add(o, scale(normalize(rnd), P.jscale));
-            }
-            for (int kt = 0; kt < P.n_times; ++kt)
-                colour = add(colour, cast_ray<MESH, SEC, X, COUNT>(P.S, o, ddir, P.times[kt], tl, fs, hs));
-        }
-    }
-    // colour / (samples * dof_samples * len(motion_times)) (scene.py:73); for a power of
-    // two the exact reciprocal multiply gives the identical correctly rounded result.
-    if (P.div_pow2) colour = scale(colour, P.inv_divisor);
-    else colour = divs(colour, P.divisor);
-    float* out = fb + 3 * p;
-    out[0] = colour.x;
-    out[1] = colour.y;
-    out[2] = colour.z;
-}
-
-// The per-frame parameters live in device memory (uploaded by rtx_camera_set) and are
-// read with scalar loads; only the per-call output block is passed by value.
-struct Launch {
-    float* fb;
-    unsigned long long* counters;
-    int32_t row0, nrows;
-};
-
-// Occupancy request (waves per SIMD) by kernel variant: mesh kernels without secondary
-// rays fit 128 VGPRs without scratch and gain from 4 waves/SIMD; the others spill if
-// forced below their natural allocation (measured, tools/ablate.sh).
-#ifndef RTX_LB_WAVES
-#define RTX_LB_WAVES(MESH, SEC) ((MESH) && !(SEC) ? 4 : 1)
-#endif
-#ifndef RTX_TILE
-#define RTX_TILE 1
-#endif
-// Pixels per lane: each wave renders RTX_PPL 8x8 tiles in sequence (amortises the
-// per-wave setup chain: parameters, tables, scene records).
-#ifndef RTX_PPL
-#define RTX_PPL 1
-#endif
-
-// Output pixel (row, column within the block) of this work-item. RTX_TILE=1 maps each
-// 64-lane wave to an 8x8 pixel tile (coherent rays per wave); 0 maps waves to 64
-// consecutive pixels of a row. The wave's tile is wave-uniform, so its coordinates are
-// scalar 32-bit arithmetic.
-struct PixelRC {
-    int32_t r, c;
-};
-__device__ __forceinline__ PixelRC pixel_rc(int32_t ncols, int sub) {
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(
-        (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RTX_PPL + sub));
-    if (RTX_TILE == 0) {
-        const int64_t p = (int64_t)wave * 64 + lane;
-        const int32_t r = (int32_t)(p / ncols);
-        return PixelRC{r, (int32_t)(p - (int64_t)r * ncols)};
-    }
-    const int tiles_x = (ncols + 7) >> 3;
-    const int ty = wave / tiles_x, tx = wave - ty * tiles_x;
-    return PixelRC{ty * 8 + (lane >> 3), tx * 8 + (lane & 7)};
-}
-
-__host__ __device__ inline int64_t launch_items(int32_t nrows, int32_t ncols) {
-    const int64_t waves = RTX_TILE == 0 ? ((int64_t)nrows * ncols + 63) / 64
-                                        : (int64_t)((ncols + 7) >> 3) * ((nrows + 7) >> 3);
-    return (waves + RTX_PPL - 1) / RTX_PPL * 64;
-}
-
-// Block size: 256 threads, or one wave for the hierarchy/texture (X) variants, whose
-// per-thread ray/point stacks (9 words per hierarchy level) share the CU's LDS.
-template <bool X>
-constexpr int kBlock = X ? 64 : 256;
-
-template <bool MESH, bool SEC, bool X, bool COUNT, bool JIT>
-__global__ __launch_bounds__(kBlock<X>, X ? 1 : RTX_LB_WAVES(MESH, SEC)) void k_render(const KParams* __restrict__ Pp,
-                                                                                  const Launch L) {
-    constexpr int B = kBlock<X>;
-    const int32_t ncols = Pp->ncols;
-    Tally tl = {};
-    // secondary-ray frames: [frame][word][thread] in LDS (40 KB per 256-thread block)
-    __shared__ float frames[SEC ? kMaxDepth * 4 * B : 1];
-    extern __shared__ float hstack[];  // X: [level][9][thread] (dynamic size)
-    const FrameStack fs{frames + threadIdx.x, B};
-    const HStack hs{hstack + threadIdx.x, B};
-    bool any_active = false;
-    for (int sub = 0; sub < RTX_PPL; ++sub) {
-        const PixelRC px = pixel_rc(ncols, sub);
-        const bool active = px.r < L.nrows && px.c < ncols;
-        any_active = any_active || active;
-        if (active) render_pixel<MESH, SEC, X, COUNT, JIT>(*Pp, L.fb, L.row0, px.r, px.c, tl, fs, hs);
-    }
-    flush_tally<COUNT>(tl, L.counters, any_active);
-}
-
-template <bool MESH, bool X>
-__global__ __launch_bounds__(256) void k_intersect(SceneView S, int64_t n, const float* __restrict__ ro,
-                                                   const float* __restrict__ rd, float time, double* t_out,
-                                                   int32_t* obj_out, int32_t* mat_out, float* n_out, float* p_out) {
-    extern __shared__ float hstack[];
-    const HStack hs{hstack + threadIdx.x, (int)blockDim.x};
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const f3 o = mk(ro[i], ro[n + i], ro[2 * n + i]);
-    const f3 d = mk(rd[i], rd[n + i], rd[2 * n + i]);
-    Tally tl = {};
-    HHit hh;
-    const Hit h = closest_hit<MESH, X, false>(S, o, d, time, tl, hs, hh);
-    int32_t mat = -1;
-    f3 nn = mk(0.0f, 0.0f, 0.0f), pp = mk(0.0f, 0.0f, 0.0f);
-    const bool hit = h.obj != -1;
-    if (hit) {
-        const Surface sf = resolve_hit<MESH, X>(S, h, hh, o, d, time);
-        mat = sf.mat;
-        nn = sf.normal;
-        pp = sf.position;
-    }
-    if (t_out) t_out[i] = !hit ? (double)INFINITY : h.obj == kHierHit ? hh.t64 : hit_t64(S, h.obj, h.sub, o, d, time);
-    if (obj_out) obj_out[i] = !hit ? -1 : h.obj == kHierHit ? h.sub : S.objs[h.obj].oid;
-    if (mat_out) mat_out[i] = mat;
-    if (n_out) { n_out[i] = nn.x; n_out[n + i] = nn.y; n_out[2 * n + i] = nn.z; }
-    if (p_out) { p_out[i] = pp.x; p_out[n + i] = pp.y; p_out[2 * n + i] = pp.z; }
-}
-
-template <bool MESH, bool X>
-__global__ __launch_bounds__(256) void k_occluded(SceneView S, int64_t n, const float* __restrict__ ro,
-                                                  const float* __restrict__ rd, const double* __restrict__ tmax,
-                                                  float time, uint8_t* occ) {
-    extern __shared__ float hstack[];
-    const HStack hs{hstack + threadIdx.x, (int)blockDim.x};
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const f3 o = mk(ro[i], ro[n + i], ro[2 * n + i]);
-    const f3 d = mk(rd[i], rd[n + i], rd[2 * n + i]);
-    Tally tl = {};
-    occ[i] = occluded<MESH, X, false>(S, o, d, tmax[i], time, tl, hs) ? 1 : 0;
-}
-
-__global__ __launch_bounds__(256) void k_to_rgb8(const float* __restrict__ fb, uint8_t* __restrict__ out, int64_t n) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    out[i] = (uint8_t)(int)((double)fb[i] * 255.0);
-}
 
 }  // namespace
 
@@ -880,6 +681,116 @@ int convert_camera(const rtx_camera_desc* c, KParams& k) {
 
 }  // namespace
 
+// ------------------------------------------------------------------ scene-specialized kernels
+// k_render loops over the scene's planes, spheres, boxes, meshes and lights with counts
+// read at run time; with the counts as compile-time constants the loops unroll and every
+// scene record is loaded up front (TSP 1080p: 57.9 -> 39.7 us/frame). rtx_render
+// therefore compiles, once per process and scene shape, render_body with those counts
+// pinned (hiprtc, same flags as the library; the code object is also cached on disk,
+// $RTX_JIT_CACHE or /tmp/rtx_jit_<uid>). Results are identical: only loop bounds become
+// constants. RTX_JIT=0 keeps the generic kernels.
+#include "rtx_jit_sources.inc"
+
+namespace {
+
+struct JitEntry {
+    hipModule_t mod = nullptr;
+    hipFunction_t fn = nullptr;
+};
+std::mutex g_jit_mu;
+std::map<std::string, JitEntry> g_jit;
+
+bool jit_enabled() {
+    const char* e = getenv("RTX_JIT");
+    return !(e && e[0] == '0');
+}
+
+std::string jit_cache_dir() {
+    const char* e = getenv("RTX_JIT_CACHE");
+    if (e && *e) return e;
+    return "/tmp/rtx_jit_" + std::to_string((long)getuid());
+}
+
+// Returns the specialized kernel, or nullptr (the caller then launches the generic one).
+hipFunction_t jit_render_kernel(const SceneView& v, bool mesh, bool sec, bool ext, bool cnt, bool jit) {
+    if (!jit_enabled()) return nullptr;
+    if (v.n_plane + v.n_sphere + v.n_box + v.n_mesh > 32 || v.n_lights > 8) return nullptr;  // code size
+    // CSG/texture kernels: the unrolled loops raise their (already high) register
+    // pressure and the specialized kernel measured slower (NovelScene1 105 -> 134 ms)
+    if (ext) return nullptr;
+    int device = 0;
+    if (hipGetDevice(&device) != hipSuccess) return nullptr;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return nullptr;
+    std::string arch = prop.gcnArchName;
+    arch = arch.substr(0, arch.find(':'));
+    std::vector<std::string> opts = {"--offload-arch=" + arch, "-O3", "-std=c++17", "-ffp-contract=off",
+                                     "-DRTX_FIXED_COUNTS",
+                                     "-DRTX_FIXED_NP=" + std::to_string(v.n_plane),
+                                     "-DRTX_FIXED_NS=" + std::to_string(v.n_sphere),
+                                     "-DRTX_FIXED_NB=" + std::to_string(v.n_box),
+                                     "-DRTX_FIXED_NM=" + std::to_string(v.n_mesh),
+                                     "-DRTX_FIXED_NL=" + std::to_string(v.n_lights)};
+    auto b = [](bool x) { return x ? "true" : "false"; };
+    const std::string src = std::string("#include \"rtx_kernels.h\"\nextern \"C\" __global__ RTX_RENDER_BOUNDS(") +
+                            b(mesh) + ", " + b(sec) + ", " + b(ext) + ") void rtx_jit_render(const rtx::KParams* "
+                            "__restrict__ P, const rtx::Launch L) {\n  rtx::render_body<" + b(mesh) + ", " + b(sec) +
+                            ", " + b(ext) + ", " + b(cnt) + ", " + b(jit) + ">(P, L);\n}\n";
+    std::string key = src;
+    for (const auto& o : opts) key += "\n" + o;
+    std::lock_guard<std::mutex> lock(g_jit_mu);
+    auto it = g_jit.find(key);
+    if (it != g_jit.end()) return it->second.fn;
+    std::string all = key;
+    for (int h = 0; h < kJitNumHeaders; ++h) all += kJitHeaderSrcs[h];
+    char hash[32];
+    snprintf(hash, sizeof(hash), "%016zx", std::hash<std::string>{}(all));
+    const std::string dir = jit_cache_dir(), path = dir + "/rtx_" + hash + ".co";
+    std::string code;
+    {
+        std::ifstream f(path, std::ios::binary);
+        if (f) { std::stringstream ss; ss << f.rdbuf(); code = ss.str(); }
+    }
+    if (code.empty()) {
+        hiprtcProgram prog;
+        if (hiprtcCreateProgram(&prog, src.c_str(), "rtx_jit_render.hip", kJitNumHeaders, kJitHeaderSrcs,
+                                kJitHeaderNames) != HIPRTC_SUCCESS)
+            return nullptr;
+        std::vector<const char*> copts;
+        for (const auto& o : opts) copts.push_back(o.c_str());
+        const hiprtcResult rc = hiprtcCompileProgram(prog, (int)copts.size(), copts.data());
+        if (rc != HIPRTC_SUCCESS) {
+            size_t n = 0;
+            hiprtcGetProgramLogSize(prog, &n);
+            std::string log(n, '\0');
+            hiprtcGetProgramLog(prog, &log[0]);
+            fprintf(stderr, "librtx: scene-specialized kernel failed to compile, using the generic one:\n%s\n",
+                    log.c_str());
+            hiprtcDestroyProgram(&prog);
+            return nullptr;
+        }
+        size_t n = 0;
+        hiprtcGetCodeSize(prog, &n);
+        code.resize(n);
+        hiprtcGetCode(prog, &code[0]);
+        hiprtcDestroyProgram(&prog);
+        (void)system(("mkdir -p '" + dir + "' 2>/dev/null").c_str());
+        const std::string tmp = path + "." + std::to_string((long)getpid());
+        std::ofstream f(tmp, std::ios::binary);
+        if (f.write(code.data(), (std::streamsize)code.size())) {
+            f.close();
+            (void)rename(tmp.c_str(), path.c_str());
+        }
+    }
+    JitEntry e;
+    if (hipModuleLoadData(&e.mod, code.data()) != hipSuccess) return nullptr;
+    if (hipModuleGetFunction(&e.fn, e.mod, "rtx_jit_render") != hipSuccess) return nullptr;
+    g_jit[key] = e;
+    return e.fn;
+}
+
+}  // namespace
+
 // ------------------------------------------------------------------ scene object
 struct rtx_scene {
     int device = 0;
@@ -1062,6 +973,13 @@ int rtx_render(rtx_scene* s, int32_t row0, int32_t nrows, float* fb_dev, uint64_
     const int sel = (s->has_mesh ? 16 : 0) | (s->has_secondary ? 8 : 0) | (s->has_ext ? 4 : 0) | (cnt ? 2 : 0) | (jit ? 1 : 0);
     const KParams* kp = s->d_kp;
     const size_t hbytes = (size_t)s->hlevels * 9 * sizeof(float);
+    if (hipFunction_t fn = jit_render_kernel(s->view, s->has_mesh, s->has_secondary, s->has_ext, cnt, jit)) {
+        const int blk = s->has_ext ? kBlock<true> : kBlock<false>;
+        void* args[] = {(void*)&kp, (void*)&L};
+        RTX_HIP(hipModuleLaunchKernel(fn, (unsigned)((items + blk - 1) / blk), 1, 1, blk, 1, 1,
+                                      s->has_ext ? (unsigned)(hbytes * blk) : 0u, st, args, nullptr));
+        return RTX_OK;
+    }
 #define RTX_LAUNCH(M, S, X, C, J)                                                                              \
     hipLaunchKernelGGL((k_render<M, S, X, C, J>), dim3((unsigned)((items + kBlock<X> - 1) / kBlock<X>)),   \
                        dim3(kBlock<X>), X ? hbytes * kBlock<X> : 0, st, kp, L)

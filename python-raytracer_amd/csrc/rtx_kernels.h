@@ -1,0 +1,231 @@
+// rtx_kernels.h — device side of the render path: per-frame parameters, the per-pixel
+// sample loops (scene.py:47-79) and the kernels of librtx.so. Compiled into librtx.so
+// (rtx_api.hip) and, for scene-specialized kernels, at run time by hiprtc (rtx_jit.cpp),
+// which only needs render_body.
+#pragma once
+
+#include "rtx_trace.h"
+#if defined(__HIPCC_RTC__)
+#include "rtx.h"  // handed to hiprtc by name
+#else
+#include "../../include/rtx.h"
+#endif
+
+namespace rtx {
+
+struct KParams {
+    SceneView S;
+    // camera tables (device)
+    cptr<float> xs;
+    cptr<float> ys;
+    cptr<float> dof_o;   // [n_dof][3]
+    cptr<float> aa_o;    // [n_dof][n_aa][3]
+    cptr<float> times;   // [n_times] fp32
+    cptr<float> noise;   // replay jitter
+    float pos[4], u[4], v[4], dw[4];
+    float focal, divisor, jscale, inv_divisor;
+    int32_t div_pow2, pad0, pad1, pad2;
+    int32_t width, height, col0, ncols;
+    int32_t n_dof, n_aa, n_times, jitter;
+    uint32_t seed_lo, seed_hi;
+};
+
+template <bool COUNT>
+__device__ __forceinline__ void flush_tally(const Tally& tl, unsigned long long* counters, bool active) {
+    if (!COUNT || counters == nullptr) return;
+    uint32_t vals[RTX_COUNTERS] = {};
+#pragma unroll
+    for (int k = 0; k < kMaxDepth; ++k) vals[k] = active ? tl.cast[k] : 0u;
+    vals[RTX_CNT_SHADOW] = active ? tl.shadow : 0u;
+    vals[RTX_CNT_SHADE] = active ? tl.shade : 0u;
+    vals[RTX_CNT_TRI] = active ? tl.tri : 0u;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < RTX_COUNTERS; ++k) {
+        unsigned long long s = vals[k];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+        if (lane == 0 && s) atomicAdd(&counters[k], s);
+    }
+}
+
+// scene.py:47-79 for pixel p of the output block (host/device: the tests-only host
+// emulation runs the same body).
+template <bool MESH, bool SEC, bool X, bool COUNT, bool JIT>
+RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, int32_t cc, Tally& tl,
+                         const FrameStack& fs, const HStack& hs) {
+    const int64_t p = (int64_t)rr * P.ncols + cc;
+    const int j = P.height - 1 - (row0 + rr);  // reference row index (y grows upward)
+    const float fx = P.xs[cc];
+    const float fy = P.ys[j];
+    // base_ray_direction = normalize(x * u + y * v - d * w)  (scene.py:54)
+    const f3 bdir = normalize(sub(add(scale(ld3(P.u), fx), scale(ld3(P.v), fy)), ld3(P.dw)));
+    const f3 focal = add(ld3(P.pos), scale(bdir, P.focal));  // scene.py:55
+    f3 colour = mk(0.0f, 0.0f, 0.0f);
+    for (int kd = 0; kd < P.n_dof; ++kd) {
+        const f3 ddir = normalize(sub(focal, ld3(P.dof_o + 3 * kd)));  // scene.py:58
+        for (int ka = 0; ka < P.n_aa; ++ka) {
+            f3 o = ld3(P.aa_o + 3 * (kd * P.n_aa + ka));
+            if (JIT) {  // scene.py:63-65
+                f3 rnd;
+                if (P.jitter == RTX_JITTER_REPLAY) {
+                    const int64_t idx = (((int64_t)cc * P.height + j) * P.n_dof + kd) * P.n_aa + ka;
+                    rnd = ld3(P.noise + 3 * idx);
+                } else {
+                    uint32_t ctr[4] = {(uint32_t)(P.col0 + cc), (uint32_t)j, (uint32_t)(kd * P.n_aa + ka), 0u};
+                    philox4x32(ctr, P.seed_lo, P.seed_hi);
+                    rnd = mk((float)(ctr[0] >> 8) * 0x1p-24f, (float)(ctr[1] >> 8) * 0x1p-24f,
+                             (float)(ctr[2] >> 8) * 0x1p-24f);
+                }
+                o = add(o, scale(normalize(rnd), P.jscale));
+            }
+            for (int kt = 0; kt < P.n_times; ++kt)
+                colour = add(colour, cast_ray<MESH, SEC, X, COUNT>(P.S, o, ddir, P.times[kt], tl, fs, hs));
+        }
+    }
+    // colour / (samples * dof_samples * len(motion_times)) (scene.py:73); for a power of
+    // two the exact reciprocal multiply gives the identical correctly rounded result.
+    if (P.div_pow2) colour = scale(colour, P.inv_divisor);
+    else colour = divs(colour, P.divisor);
+    float* out = fb + 3 * p;
+    out[0] = colour.x;
+    out[1] = colour.y;
+    out[2] = colour.z;
+}
+
+// The per-frame parameters live in device memory (uploaded by rtx_camera_set) and are
+// read with scalar loads; only the per-call output block is passed by value.
+struct Launch {
+    float* fb;
+    unsigned long long* counters;
+    int32_t row0, nrows;
+};
+
+// Occupancy request (waves per SIMD) by kernel variant: mesh kernels without secondary
+// rays fit 128 VGPRs without scratch and gain from 4 waves/SIMD; the others spill if
+// forced below their natural allocation (measured, tools/ablate.sh).
+#ifndef RTX_LB_WAVES
+#define RTX_LB_WAVES(MESH, SEC) ((MESH) && !(SEC) ? 4 : 1)
+#endif
+#ifndef RTX_TILE
+#define RTX_TILE 1
+#endif
+// Pixels per lane: each wave renders RTX_PPL 8x8 tiles in sequence (amortises the
+// per-wave setup chain: parameters, tables, scene records).
+#ifndef RTX_PPL
+#define RTX_PPL 1
+#endif
+
+// Output pixel (row, column within the block) of this work-item. RTX_TILE=1 maps each
+// 64-lane wave to an 8x8 pixel tile (coherent rays per wave); 0 maps waves to 64
+// consecutive pixels of a row. The wave's tile is wave-uniform, so its coordinates are
+// scalar 32-bit arithmetic.
+struct PixelRC {
+    int32_t r, c;
+};
+__device__ __forceinline__ PixelRC pixel_rc(int32_t ncols, int sub) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(
+        (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RTX_PPL + sub));
+    if (RTX_TILE == 0) {
+        const int64_t p = (int64_t)wave * 64 + lane;
+        const int32_t r = (int32_t)(p / ncols);
+        return PixelRC{r, (int32_t)(p - (int64_t)r * ncols)};
+    }
+    const int tiles_x = (ncols + 7) >> 3;
+    const int ty = wave / tiles_x, tx = wave - ty * tiles_x;
+    return PixelRC{ty * 8 + (lane >> 3), tx * 8 + (lane & 7)};
+}
+
+__host__ __device__ inline int64_t launch_items(int32_t nrows, int32_t ncols) {
+    const int64_t waves = RTX_TILE == 0 ? ((int64_t)nrows * ncols + 63) / 64
+                                        : (int64_t)((ncols + 7) >> 3) * ((nrows + 7) >> 3);
+    return (waves + RTX_PPL - 1) / RTX_PPL * 64;
+}
+
+// Block size: 256 threads, or one wave for the hierarchy/texture (X) variants, whose
+// per-thread ray/point stacks (9 words per hierarchy level) share the CU's LDS.
+template <bool X>
+constexpr int kBlock = X ? 64 : 256;
+
+// The body of k_render, shared with the scene-specialized kernels compiled at run time
+// (rtx_jit.cpp), which pin the scene's object and light counts.
+template <bool MESH, bool SEC, bool X, bool COUNT, bool JIT>
+__device__ __forceinline__ void render_body(const KParams* __restrict__ Pp, const Launch L) {
+    constexpr int B = kBlock<X>;
+    const int32_t ncols = Pp->ncols;
+    Tally tl = {};
+    // secondary-ray frames: [frame][word][thread] in LDS (40 KB per 256-thread block)
+    __shared__ float frames[SEC ? kMaxDepth * 4 * B : 1];
+    extern __shared__ float hstack[];  // X: [level][9][thread] (dynamic size)
+    const FrameStack fs{frames + threadIdx.x, B};
+    const HStack hs{hstack + threadIdx.x, B};
+    bool any_active = false;
+    for (int sub = 0; sub < RTX_PPL; ++sub) {
+        const PixelRC px = pixel_rc(ncols, sub);
+        const bool active = px.r < L.nrows && px.c < ncols;
+        any_active = any_active || active;
+        if (active) render_pixel<MESH, SEC, X, COUNT, JIT>(*Pp, L.fb, L.row0, px.r, px.c, tl, fs, hs);
+    }
+    flush_tally<COUNT>(tl, L.counters, any_active);
+}
+
+#define RTX_RENDER_BOUNDS(MESH, SEC, X) __launch_bounds__(rtx::kBlock<X>, (X) ? 1 : RTX_LB_WAVES(MESH, SEC))
+
+#if !defined(__HIPCC_RTC__)
+template <bool MESH, bool SEC, bool X, bool COUNT, bool JIT>
+__global__ RTX_RENDER_BOUNDS(MESH, SEC, X) void k_render(const KParams* __restrict__ Pp, const Launch L) {
+    render_body<MESH, SEC, X, COUNT, JIT>(Pp, L);
+}
+
+template <bool MESH, bool X>
+__global__ __launch_bounds__(256) void k_intersect(SceneView S, int64_t n, const float* __restrict__ ro,
+                                                   const float* __restrict__ rd, float time, double* t_out,
+                                                   int32_t* obj_out, int32_t* mat_out, float* n_out, float* p_out) {
+    extern __shared__ float hstack[];
+    const HStack hs{hstack + threadIdx.x, (int)blockDim.x};
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const f3 o = mk(ro[i], ro[n + i], ro[2 * n + i]);
+    const f3 d = mk(rd[i], rd[n + i], rd[2 * n + i]);
+    Tally tl = {};
+    HHit hh;
+    const Hit h = closest_hit<MESH, X, false>(S, o, d, time, tl, hs, hh);
+    int32_t mat = -1;
+    f3 nn = mk(0.0f, 0.0f, 0.0f), pp = mk(0.0f, 0.0f, 0.0f);
+    const bool hit = h.obj != -1;
+    if (hit) {
+        const Surface sf = resolve_hit<MESH, X>(S, h, hh, o, d, time);
+        mat = sf.mat;
+        nn = sf.normal;
+        pp = sf.position;
+    }
+    if (t_out) t_out[i] = !hit ? (double)INFINITY : h.obj == kHierHit ? hh.t64 : hit_t64(S, h.obj, h.sub, o, d, time);
+    if (obj_out) obj_out[i] = !hit ? -1 : h.obj == kHierHit ? h.sub : S.objs[h.obj].oid;
+    if (mat_out) mat_out[i] = mat;
+    if (n_out) { n_out[i] = nn.x; n_out[n + i] = nn.y; n_out[2 * n + i] = nn.z; }
+    if (p_out) { p_out[i] = pp.x; p_out[n + i] = pp.y; p_out[2 * n + i] = pp.z; }
+}
+
+template <bool MESH, bool X>
+__global__ __launch_bounds__(256) void k_occluded(SceneView S, int64_t n, const float* __restrict__ ro,
+                                                  const float* __restrict__ rd, const double* __restrict__ tmax,
+                                                  float time, uint8_t* occ) {
+    extern __shared__ float hstack[];
+    const HStack hs{hstack + threadIdx.x, (int)blockDim.x};
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const f3 o = mk(ro[i], ro[n + i], ro[2 * n + i]);
+    const f3 d = mk(rd[i], rd[n + i], rd[2 * n + i]);
+    Tally tl = {};
+    occ[i] = occluded<MESH, X, false>(S, o, d, tmax[i], time, tl, hs) ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void k_to_rgb8(const float* __restrict__ fb, uint8_t* __restrict__ out, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = (uint8_t)(int)((double)fb[i] * 255.0);
+}
+#endif  // !__HIPCC_RTC__
+
+}  // namespace rtx

@@ -7,8 +7,19 @@
 // SpacewaIker/python-raytracer @ 2025-02-14.
 #pragma once
 
+#if !defined(__HIPCC_RTC__)  // hiprtc (scene-specialized kernels) brings its own runtime header
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#else
+using __hip_internal::int32_t;
+using __hip_internal::int64_t;
+using __hip_internal::uint8_t;
+using __hip_internal::uint32_t;
+using __hip_internal::uint64_t;
+#ifndef INFINITY
+#define INFINITY __builtin_inff()
+#endif
+#endif
 
 #define RTX_HD __host__ __device__ __forceinline__
 
@@ -1027,12 +1038,27 @@ RTX_HY void hier_closest(const SceneView& S, const HStack& hs, f3 o, f3 d, float
     }
 }
 
+// Object/light counts (an experiment can pin them at compile time: -DRTX_FIXED_COUNTS=...)
+#ifdef RTX_FIXED_COUNTS
+#define RTX_NPLANE(S) RTX_FIXED_NP
+#define RTX_NSPHERE(S) RTX_FIXED_NS
+#define RTX_NBOX(S) RTX_FIXED_NB
+#define RTX_NMESH(S) RTX_FIXED_NM
+#define RTX_NLIGHTS(S) RTX_FIXED_NL
+#else
+#define RTX_NPLANE(S) (S).n_plane
+#define RTX_NSPHERE(S) (S).n_sphere
+#define RTX_NBOX(S) (S).n_box
+#define RTX_NMESH(S) (S).n_mesh
+#define RTX_NLIGHTS(S) (S).n_lights
+#endif
+
 // ------------------------------------------------------------------ closest hit
 template <bool MESH, bool X, bool COUNT>
 RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const HStack& hs, HHit& hh) {
     Hit h{INFINITY, -1, 0};
     int oi = 0;
-    for (int k = 0; k < S.n_plane; ++k, ++oi) {  // simple_geometry.py:105-120
+    for (int k = 0; k < RTX_NPLANE(S); ++k, ++oi) {  // simple_geometry.py:105-120
         const DObj ob = S.objs[oi];
         const f3 n = ld3(ob.b);
         const float denom = dot(d, n);
@@ -1042,7 +1068,7 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
         const bool valid = fabsf(denom) >= kEps4Up && quot_nonneg(t32, num, denom);
         offer(S, h, valid, t32, oi, 0, o, d, time);
     }
-    for (int k = 0; k < S.n_sphere; ++k, ++oi) {  // simple_geometry.py:20-46
+    for (int k = 0; k < RTX_NSPHERE(S); ++k, ++oi) {  // simple_geometry.py:20-46
         if (RTX_ABLATE == 7) continue;  // cost probe: no spheres in the primary test
         const DObj ob = S.objs[oi];
         const f3 ctr = moved(ob, ob.a, time);
@@ -1060,7 +1086,7 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
         }
         offer(S, h, valid, t32, oi, root, o, d, time);
     }
-    for (int k = 0; k < S.n_box; ++k, ++oi) {  // simple_geometry.py:188-249 (entry precedes exit)
+    for (int k = 0; k < RTX_NBOX(S); ++k, ++oi) {  // simple_geometry.py:188-249 (entry precedes exit)
         const DObj ob = S.objs[oi];
         double start = 0.0, end = 0.0;
         int label = 0;
@@ -1069,7 +1095,7 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
         offer(S, h, valid, (float)start, oi, label, o, d, time);
     }
     if (MESH) {
-        for (int k = 0; k < S.n_mesh; ++k, ++oi) {  // mesh.py:72-119, faces in order
+        for (int k = 0; k < RTX_NMESH(S); ++k, ++oi) {  // mesh.py:72-119, faces in order
             const DObj ob = S.objs[oi];
             if (!mesh_bv(ob, o, d)) continue;  // the reference's bounding volume, quirks included
             const RayInv ri = ray_inv(o, d);
@@ -1110,7 +1136,7 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
     const float tmax32 = (float)t_max;
     bool occ = false;
     int oi = 0;
-    for (int k = 0; k < S.n_plane; ++k, ++oi) {  // simple_geometry.py:122-131
+    for (int k = 0; k < RTX_NPLANE(S); ++k, ++oi) {  // simple_geometry.py:122-131
         const DObj ob = S.objs[oi];
         const f3 n = ld3(ob.b);
         const float denom = dot(d, n);
@@ -1121,7 +1147,7 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
         occ = occ || hit;
     }
     if (RTX_ALL(occ)) return true;
-    for (int k = 0; k < S.n_sphere; ++k, ++oi) {  // simple_geometry.py:48-72 (shadow_epsilon 1e-3)
+    for (int k = 0; k < RTX_NSPHERE(S); ++k, ++oi) {  // simple_geometry.py:48-72 (shadow_epsilon 1e-3)
         const DObj ob = S.objs[oi];
         const f3 ctr = moved(ob, ob.a, time);
         if (!occ && sphere_disc_sign(o, d, ctr, (float)ob.r2) >= 0) {
@@ -1138,7 +1164,7 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
         }
     }
     if (RTX_ALL(occ)) return true;
-    for (int k = 0; k < S.n_box; ++k, ++oi) {  // simple_geometry.py:251-294
+    for (int k = 0; k < RTX_NBOX(S); ++k, ++oi) {  // simple_geometry.py:251-294
         const DObj ob = S.objs[oi];
         if (!occ) {
             double start, end;
@@ -1148,7 +1174,7 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
         }
     }
     if (MESH) {
-        for (int k = 0; k < S.n_mesh; ++k, ++oi) {  // mesh.py:121-153 (no t_max test)
+        for (int k = 0; k < RTX_NMESH(S); ++k, ++oi) {  // mesh.py:121-153 (no t_max test)
             const DObj ob = S.objs[oi];
             if (RTX_ALL(occ)) break;
             const bool live = !occ && mesh_bv(ob, o, d);
@@ -1261,7 +1287,7 @@ RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const 
                            Tally& tl, const HStack& hs) {
     f3 colour = mk(0.0f, 0.0f, 0.0f);
     tally_inc<COUNT>(tl, &Tally::shade);
-    for (int li = 0; li < S.n_lights; ++li) {
+    for (int li = 0; li < RTX_NLIGHTS(S); ++li) {
         const DLight L = S.lights[li];
         f3 sdir;
         double t_max;

@@ -10,13 +10,15 @@ SRC = os.path.join(HERE, "native", "rtx_hostemu.hip")
 LIB = os.path.join(HERE, "native", "librtx_hostemu.so")
 DEPS = [SRC, os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_api.hip"),
         os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_trace.h"),
+        os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_kernels.h"),
+        os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_jit_sources.inc"),
         os.path.join(HERE, "..", "include", "rtx.h")]
 
 
 def build():
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(p) for p in DEPS):
         subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-O2", "-std=c++17", "-ffp-contract=off", "-fopenmp",
-                               "-fPIC", "-shared", "-o", LIB, SRC])
+                               "-fPIC", "-shared", "-o", LIB, SRC, "-lhiprtc"])
     return LIB
 
 

@@ -229,3 +229,20 @@ def test_large_mesh_bvh_matches_oracle(tmp_path, flat):
     d = blob_scene(p, (64, 64), flat)
     s = assert_parity(product_scene_dict(d).render(), oracle_render_dict(d), "blob")
     assert s["frac_diff"] == 0.0, s
+
+
+@pytest.mark.parametrize("name,res,edits", [
+    ("TwoSpheresPlane", (160, 90), {}), ("MirrorRefraction", (160, 90), {}), ("TorusMesh", (96, 96), {}),
+    ("DepthOfField", (64, 48), {"AA": {"jitter": True, "samples": 2}}),
+    ("NovelScene1", (128, 64), {"AA": {"jitter": True, "samples": 2}}),
+])
+def test_scene_specialized_kernel_equals_generic(name, res, edits, monkeypatch):
+    """rtx_render's hiprtc kernel (object/light counts pinned) vs the precompiled generic
+    kernel: identical framebuffers and counters."""
+    sc = product_scene(name, res, **edits)
+    cnt_a = torch.zeros(16, dtype=torch.int64, device="cuda")
+    a = sc.render_device(counters=cnt_a).clone()
+    monkeypatch.setenv("RTX_JIT", "0")
+    cnt_b = torch.zeros(16, dtype=torch.int64, device="cuda")
+    b = sc.render_device(counters=cnt_b).clone()
+    assert torch.equal(a, b) and torch.equal(cnt_a, cnt_b)

@@ -10,7 +10,7 @@ mkdir -p "$OUT" /tmp/rtx_ablate
 for n in ${VARIANTS:-0 1 2 3}; do
   fl_var="FLAGS_$n"; fl="${!fl_var:--DRTX_ABLATE=$n}"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared $fl \
-    -o /tmp/rtx_ablate/librtx_$n.so python-raytracer_amd/csrc/rtx_api.hip || exit 1
+    -o /tmp/rtx_ablate/librtx_$n.so python-raytracer_amd/csrc/rtx_api.hip -lhiprtc || exit 1
 done
 for n in ${VARIANTS:-0 1 2 3}; do
   for c in ${CONFIGS:-tsp1080}; do
