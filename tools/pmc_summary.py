@@ -16,7 +16,7 @@ acc = {}
 kname = None
 for f in sorted(glob.glob(os.path.join(d, "p*", "*counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
-        if "k_render" not in r["Kernel_Name"]:
+        if "k_render" not in r["Kernel_Name"] and "rtx_jit_render" not in r["Kernel_Name"]:
             continue
         kname = r["Kernel_Name"]
         acc.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
