@@ -732,8 +732,11 @@ hipFunction_t jit_render_kernel(const SceneView& v, bool mesh, bool sec, bool ex
                                      "-DRTX_FIXED_NM=" + std::to_string(v.n_mesh),
                                      "-DRTX_FIXED_NL=" + std::to_string(v.n_lights)};
     auto b = [](bool x) { return x ? "true" : "false"; };
+    // kernel name: rtx_jit_render_<mesh><sec><ext><count><jitter> (tells profiles apart)
+    std::string name = "rtx_jit_render_";
+    for (bool f : {mesh, sec, ext, cnt, jit}) name += f ? '1' : '0';
     const std::string src = std::string("#include \"rtx_kernels.h\"\nextern \"C\" __global__ RTX_RENDER_BOUNDS(") +
-                            b(mesh) + ", " + b(sec) + ", " + b(ext) + ") void rtx_jit_render(const rtx::KParams* "
+                            b(mesh) + ", " + b(sec) + ", " + b(ext) + ") void " + name + "(const rtx::KParams* "
                             "__restrict__ P, const rtx::Launch L) {\n  rtx::render_body<" + b(mesh) + ", " + b(sec) +
                             ", " + b(ext) + ", " + b(cnt) + ", " + b(jit) + ">(P, L);\n}\n";
     std::string key = src;
@@ -784,7 +787,7 @@ hipFunction_t jit_render_kernel(const SceneView& v, bool mesh, bool sec, bool ex
     }
     JitEntry e;
     if (hipModuleLoadData(&e.mod, code.data()) != hipSuccess) return nullptr;
-    if (hipModuleGetFunction(&e.fn, e.mod, "rtx_jit_render") != hipSuccess) return nullptr;
+    if (hipModuleGetFunction(&e.fn, e.mod, name.c_str()) != hipSuccess) return nullptr;
     g_jit[key] = e;
     return e.fn;
 }
