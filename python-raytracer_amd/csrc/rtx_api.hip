@@ -731,6 +731,10 @@ hipFunction_t jit_render_kernel(const SceneView& v, bool mesh, bool sec, bool ex
                                      "-DRTX_FIXED_NB=" + std::to_string(v.n_box),
                                      "-DRTX_FIXED_NM=" + std::to_string(v.n_mesh),
                                      "-DRTX_FIXED_NL=" + std::to_string(v.n_lights)};
+    if (const char* extra = getenv("RTX_JIT_FLAGS")) {  // experiments (tools/ablate.sh); part of the cache key
+        std::istringstream is(extra);
+        for (std::string o; is >> o;) opts.push_back(o);
+    }
     auto b = [](bool x) { return x ? "true" : "false"; };
     // kernel name: rtx_jit_render_<mesh><sec><ext><count><jitter> (tells profiles apart)
     std::string name = "rtx_jit_render_";
