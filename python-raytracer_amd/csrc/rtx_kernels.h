@@ -87,6 +87,16 @@ RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, 
     // two the exact reciprocal multiply gives the identical correctly rounded result.
     if (P.div_pow2) colour = scale(colour, P.inv_divisor);
     else colour = divs(colour, P.divisor);
+#if RTX_ABLATE == 11 && defined(__HIP_DEVICE_COMPILE__)
+    {  // cost probe only: RTX_PAD extra VALU instructions per pixel in 4 independent chains
+        float c0 = colour.x, c1 = colour.y, c2 = colour.z, c3 = fx;
+#pragma unroll
+        for (int k = 0; k < RTX_PAD / 4; ++k)
+            asm volatile("v_add_f32 %0, %4, %0\n v_add_f32 %1, %4, %1\n v_add_f32 %2, %4, %2\n v_add_f32 %3, %4, %3"
+                         : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3) : "v"(fy));
+        colour = mk(c0, c1, c2 + c3 * 0.0f);
+    }
+#endif
     float* out = fb + 3 * p;
     out[0] = colour.x;
     out[1] = colour.y;

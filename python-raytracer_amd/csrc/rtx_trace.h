@@ -102,7 +102,8 @@ struct alignas(16) DObj {
     int32_t type, nmat, mat0, mat1;
     int32_t has_speed, tri_begin, tri_count, bv_type;
     int32_t flat, oid, leaf_begin, leaf_count;   // mesh: BVH nodes (DLeaf range, preorder)
-    float cmax, pad3, pad4, pad5;                // mesh: max |vertex coordinate|
+    float cmax;                                  // mesh: max |vertex coordinate|
+    int32_t face_cull, pad4, pad5;               // mesh: test each face's box before its exact test
     float a[4];       // sphere centre | plane point | box minpos
     float b[4];       // plane normal | box maxpos
     float c[4];       // plane width axis
@@ -122,6 +123,12 @@ struct alignas(16) DTri {
     float e01[3], e12[3], e20[3];  // v1 - v0, v2 - v1, v0 - v2 (mesh.py:99-101)
     float n[3];                    // normalize(cross(v1 - v0, v2 - v0)) (mesh.py:86)
     float nu[3];                   // cross(v1 - v0, v2 - v0) (mesh.py:134)
+};
+
+// A face's bounds, for the conservative per-face skip of small meshes (DObj::face_cull).
+struct alignas(16) DFaceBox {
+    float lo[3], pad0;
+    float hi[3], pad1;
 };
 
 struct alignas(16) DTriN {
@@ -194,6 +201,7 @@ struct SceneView {
     cptr<DObj> objs;   // [planes | spheres | boxes | meshes]
     cptr<DTri> tris;
     cptr<DTriN> trins;
+    cptr<DFaceBox> fboxes;           // per stored face (meshes with face_cull)
     cptr<DMat> mats;
     cptr<DLight> lights;
     cptr<DLeaf> leaves;
@@ -439,6 +447,16 @@ RTX_HD bool leaf_maybe_hit(const L_& L, f3 o, const RayInv& ri, float cmax, floa
     const float tn = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
     const float tf = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
     return tf >= tn && tf >= 0.0f && tn <= tcap;
+}
+
+// Per-face skip of a mesh: DObj::face_cull, or a constant when every mesh of the scene
+// agrees (scene-specialized kernels: RTX_FACE_CULL_MODE 0 = never, 1 = always).
+#ifndef RTX_FACE_CULL_MODE
+#define RTX_FACE_CULL_MODE 2
+#endif
+template <class O>
+RTX_HD bool face_cull(const O& ob) {
+    return RTX_FACE_CULL_MODE == 2 ? ob.face_cull != 0 : RTX_FACE_CULL_MODE == 1;
 }
 
 // Exact fp64 t of a candidate, recomputed from the object exactly as during its test
@@ -1105,6 +1123,11 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
                 if (!RTX_ANY(maybe)) { li = L.skip; continue; }
                 ++li;
                 for (int f = L.first; f < L.first + L.count; ++f) {
+                    bool fmaybe = maybe;
+                    if (face_cull(ob)) {  // the face's own padded box (the cluster's bound)
+                        fmaybe = maybe && leaf_maybe_hit(S.fboxes[ob.tri_begin + f], o, ri, ob.cmax, h.t32);
+                        if (!RTX_ANY(fmaybe)) continue;  // no lane's ray can pass its exact test
+                    }
                     const DTri T = S.tris[ob.tri_begin + f];
                     tally_inc<COUNT>(tl, &Tally::tri);
                     const f3 n = ld3(T.n);
@@ -1113,7 +1136,7 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
                     const float num = dot(sub(v0, o), n);
                     const float t32 = num / denom;
                     // abs(denom) < epsilon -> skip; time < 0 -> skip
-                    bool valid = maybe && !(fabsf(denom) < kEps4Up) && !quot_neg(t32, num, denom);
+                    bool valid = fmaybe && !(fabsf(denom) < kEps4Up) && !quot_neg(t32, num, denom);
                     const f3 p = add(o, scale(d, t32));  // getPoint(time)
                     const float b0 = dot(cross(ld3(T.e01), sub(p, v0)), n);
                     const float b1 = dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n);
@@ -1186,6 +1209,11 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
               if (!RTX_ANY(maybe)) { li = L.skip; continue; }
               ++li;
               for (int f = L.first; f < L.first + L.count; ++f) {
+                bool fmaybe = maybe;
+                if (face_cull(ob)) {
+                    fmaybe = maybe && leaf_maybe_hit(S.fboxes[ob.tri_begin + f], o, ri, ob.cmax);
+                    if (!RTX_ANY(fmaybe)) continue;
+                }
                 const DTri T = S.tris[ob.tri_begin + f];
                 tally_inc<COUNT>(tl, &Tally::tri);
                 const f3 n = ld3(T.nu);
@@ -1199,7 +1227,7 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
                 hit = hit && dot(cross(ld3(T.e01), sub(p, v0)), n) >= 0.0f &&
                       dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n) >= 0.0f &&
                       dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n) >= 0.0f;
-                occ = occ || (maybe && hit);
+                occ = occ || (fmaybe && hit);
               }
             }
         }

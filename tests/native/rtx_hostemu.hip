@@ -11,6 +11,7 @@ void bind_view(const HostScene& H, SceneView& v) {
     v.objs = (cptr<DObj>)H.objs.data();
     v.tris = (cptr<DTri>)H.tris.data();
     v.trins = (cptr<DTriN>)H.trins.data();
+    v.fboxes = (cptr<DFaceBox>)H.fboxes.data();
     v.mats = (cptr<DMat>)H.mats.data();
     v.lights = (cptr<DLight>)H.lights.data();
     v.leaves = (cptr<DLeaf>)H.leaves.data();
