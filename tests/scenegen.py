@@ -210,3 +210,48 @@ def blob_scene(obj_path, res=(64, 64), flat=False):
                         "power": 0.5},
                        {"name": "light3", "type": "point", "position": [0.0, -5.0, 0.0], "colour": [1.0, 1.0, 1.0],
                         "power": 10.0}]}
+
+
+def bv_stress_rays(lo, hi, n, seed=0):
+    """Rays that stress a mesh's AABB bounding volume (bounding_volumes.py:49-83):
+    origins inside, outside and exactly on the faces of the box [lo, hi], directions with
+    exact zero components, and rays aimed at the box's edges and corners (start == end up
+    to rounding). Returns float32 (n, 3) origins and directions."""
+    rng = np.random.RandomState(seed)
+    lo = np.asarray(lo, np.float64)
+    hi = np.asarray(hi, np.float64)
+    span = hi - lo
+    k = n // 4
+    # 1: origins in the box grown by half its size, random directions, some axes zeroed
+    o1 = lo - 0.5 * span + rng.uniform(0, 2, (k, 3)) * span
+    d1 = rng.normal(size=(k, 3))
+    z = rng.rand(k, 3) < 0.15
+    d1[z] = 0.0
+    d1[np.all(d1 == 0, axis=1), 1] = 1.0
+    # 2: origins exactly on a face of the box
+    o2 = lo + rng.uniform(0, 1, (k, 3)) * span
+    ax = rng.randint(0, 3, k)
+    side = rng.rand(k) < 0.5
+    o2[np.arange(k), ax] = np.where(side, lo[ax], hi[ax])
+    d2 = rng.normal(size=(k, 3))
+    # 3: aimed at points on the box's edges and corners from outside
+    m = n - 3 * k
+    tgt = lo + rng.uniform(0, 1, (m, 3)) * span
+    for i in range(m):
+        for a in rng.choice(3, rng.randint(2, 4), replace=False):
+            tgt[i, a] = lo[a] if rng.rand() < 0.5 else hi[a]
+    d3 = rng.normal(size=(m, 3))
+    o3 = tgt - d3 * rng.uniform(1, 6, (m, 1))
+    # 4: like 1 with directions of very different magnitudes (unnormalised shadow rays)
+    o4 = lo - span + rng.uniform(0, 3, (k, 3)) * span
+    d4 = rng.normal(size=(k, 3)) * (10.0 ** rng.uniform(-3, 2, (k, 1)))
+    o = np.concatenate([o1, o2, o3, o4]).astype(np.float32)
+    d = np.concatenate([d1, d2, d3, d4]).astype(np.float32)
+    return o, d
+
+
+def obj_bounds(path):
+    """Vertex bounds (float32) of an OBJ file, as Mesh.__init__ computes them for scale 1
+    and no translation (mesh.py:31-36)."""
+    v = np.array([[float(x) for x in l.split()[1:4]] for l in open(path) if l.startswith("v ")], np.float32)
+    return v.min(axis=0), v.max(axis=0)

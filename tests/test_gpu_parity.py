@@ -130,6 +130,27 @@ def test_geometry_kat(name):
             assert (sc.occluded(o, d, tmax, time) == osc.shadow(time, o, d, tmax).astype(bool)).mean() > 0.9999
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_mesh_bv_stress_matches_oracle(seed):
+    """Rays inside / on / grazing the torus's bounding box vs the oracle, exactly (the
+    fp32 decision of BoundingAABB.intersect and its fp64 fallback)."""
+    import os
+    from oracle import oracle as O
+    from scenegen import bv_stress_rays, obj_bounds
+    lo, hi = obj_bounds(os.path.join(os.path.dirname(__file__), "..", "assets", "torus_mesh.obj"))
+    o, d = bv_stress_rays(lo, hi, 20000, seed)
+    sc = product_scene("TorusMesh", (8, 8))
+    dd, base = O.load_bundle("TorusMesh")
+    osc = O.OracleScene(dd, base)
+    got = sc.intersect(o, d, 0.0)
+    t, ob, _, m, nn, pp = osc.closest(0.0, o, d)
+    assert np.array_equal(got["obj"], ob)
+    hit = ob >= 0
+    assert np.array_equal(got["t"][hit], t[hit])
+    for tmax in (1.0, np.inf):
+        assert np.array_equal(sc.occluded(o, d, tmax, 0.0), osc.shadow(0.0, o, d, tmax).astype(bool))
+
+
 def test_full_size_dof_4k_properties():
     """DepthOfField 3840x2160, AA 2 x DOF 32 (config 5): a 64-row block. Values in [0, 1],
     deterministic, and identical when split into sub-blocks (partition invariance)."""

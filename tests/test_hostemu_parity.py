@@ -80,6 +80,27 @@ def test_hostemu_geometry_kat(name):
             assert np.array_equal(hostemu.occluded(sc, o, d, tmax, time), osc.shadow(time, o, d, tmax).astype(bool))
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_hostemu_mesh_bv_stress(seed):
+    """Rays inside / on / grazing the torus's bounding box (its fp32 decision and fp64
+    fallback) vs the oracle, exactly."""
+    import os
+    from oracle import oracle as O
+    from scenegen import bv_stress_rays, obj_bounds
+    lo, hi = obj_bounds(os.path.join(os.path.dirname(__file__), "..", "assets", "torus_mesh.obj"))
+    o, d = bv_stress_rays(lo, hi, 4000, seed)
+    sc = product_scene("TorusMesh", (8, 8))
+    dd, base = O.load_bundle("TorusMesh")
+    osc = O.OracleScene(dd, base)
+    got = hostemu.intersect(sc, o, d, 0.0)
+    t, ob, _, m, nn, pp = osc.closest(0.0, o, d)
+    assert np.array_equal(got["obj"], ob)
+    hit = ob >= 0
+    assert np.array_equal(got["t"][hit], t[hit])
+    for tmax in (1.0, np.inf):
+        assert np.array_equal(hostemu.occluded(sc, o, d, tmax, 0.0), osc.shadow(0.0, o, d, tmax).astype(bool))
+
+
 @pytest.mark.parametrize("seed", range(12))
 def test_hostemu_random_scenes(seed):
     from common import oracle_render_dict, product_scene_dict
