@@ -55,6 +55,10 @@ template <bool MESH, bool SEC, bool X, bool COUNT, bool JIT>
 RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, int32_t cc, Tally& tl,
                          const FrameStack& fs, const HStack& hs) {
     const int64_t p = (int64_t)rr * P.ncols + cc;
+    if (RTX_ABLATE == 14) {  // cost probe only: store a constant (launch + framebuffer write)
+        fb[3 * p] = 0.5f; fb[3 * p + 1] = 0.25f; fb[3 * p + 2] = 0.125f;
+        return;
+    }
     const int j = P.height - 1 - (row0 + rr);  // reference row index (y grows upward)
     const float fx = P.xs[cc];
     const float fy = P.ys[j];
@@ -71,6 +75,8 @@ RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, 
                 if (P.jitter == RTX_JITTER_REPLAY) {
                     const int64_t idx = (((int64_t)cc * P.height + j) * P.n_dof + kd) * P.n_aa + ka;
                     rnd = ld3(P.noise + 3 * idx);
+                } else if (RTX_ABLATE == 15) {  // cost probe only: no RNG
+                    rnd = mk(0.25f + 0.001f * (float)ka, 0.5f, 0.75f + 0.001f * (float)kd);
                 } else {
                     uint32_t ctr[4] = {(uint32_t)(P.col0 + cc), (uint32_t)j, (uint32_t)(kd * P.n_aa + ka), 0u};
                     philox4x32(ctr, P.seed_lo, P.seed_hi);

@@ -459,6 +459,21 @@ RTX_HD bool face_cull(const O& ob) {
     return RTX_FACE_CULL_MODE == 2 ? ob.face_cull != 0 : RTX_FACE_CULL_MODE == 1;
 }
 
+// A box's conservative pre-test (same bound as the clusters'): false only when no exact
+// slab test of the ray against [mn, mx] can pass with start <= tcap.
+struct Box3 {
+    float lo[3], hi[3];
+};
+RTX_HD bool box_maybe_hit(f3 mn, f3 mx, f3 o, const RayInv& ri, float tcap) {
+    // the slabs are symmetric in (min, max): a box given with min > max on an axis
+    // (NovelScene2's trails) spans [max, min] there
+    const Box3 B{{fminf(mn.x, mx.x), fminf(mn.y, mx.y), fminf(mn.z, mx.z)},
+                 {fmaxf(mn.x, mx.x), fmaxf(mn.y, mx.y), fmaxf(mn.z, mx.z)}};
+    const float cm = fmaxf(fmaxf(fmaxf(fabsf(mn.x), fabsf(mn.y)), fmaxf(fabsf(mn.z), fabsf(mx.x))),
+                           fmaxf(fabsf(mx.y), fabsf(mx.z)));
+    return leaf_maybe_hit(B, o, ri, cm, tcap);
+}
+
 // Exact fp64 t of a candidate, recomputed from the object exactly as during its test
 // (used only when two fp32 proxies tie; out of line to keep the hot loop's registers low).
 __host__ __device__ __attribute__((noinline)) inline double hit_t64(const SceneView& S, int32_t obj, int32_t sb, f3 o, f3 d, float time) {
@@ -1104,11 +1119,17 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
         }
         offer(S, h, valid, t32, oi, root, o, d, time);
     }
+    RayInv ri{};
+    if (RTX_NBOX(S) > 0 || (MESH && RTX_NMESH(S) > 0)) ri = ray_inv(o, d);
     for (int k = 0; k < RTX_NBOX(S); ++k, ++oi) {  // simple_geometry.py:188-249 (entry precedes exit)
         const DObj ob = S.objs[oi];
+        const f3 mn = moved(ob, ob.a, time), mx = moved(ob, ob.b, time);
+        // the fp64 slabs only where some lane's ray may hit the box before its best t
+        const bool maybe = box_maybe_hit(mn, mx, o, ri, h.t32);
+        if (!RTX_ANY(maybe)) continue;
         double start = 0.0, end = 0.0;
         int label = 0;
-        bool valid = box_slabs(o, d, moved(ob, ob.a, time), moved(ob, ob.b, time), start, label, end);
+        bool valid = maybe && box_slabs(o, d, mn, mx, start, label, end);
         valid = valid && !(start > end || start < 0.0);
         offer(S, h, valid, (float)start, oi, label, o, d, time);
     }
@@ -1116,7 +1137,6 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
         for (int k = 0; k < RTX_NMESH(S); ++k, ++oi) {  // mesh.py:72-119, faces in order
             const DObj ob = S.objs[oi];
             if (!mesh_bv(ob, o, d)) continue;  // the reference's bounding volume, quirks included
-            const RayInv ri = ray_inv(o, d);
             for (int li = 0; li < ob.leaf_count;) {  // stackless wave-uniform BVH walk
                 cref<DLeaf> L = S.leaves[ob.leaf_begin + li];
                 const bool maybe = leaf_maybe_hit(L, o, ri, ob.cmax, h.t32);
@@ -1187,12 +1207,17 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
         }
     }
     if (RTX_ALL(occ)) return true;
+    RayInv ri{};
+    if (RTX_NBOX(S) > 0 || (MESH && RTX_NMESH(S) > 0)) ri = ray_inv(o, d);
     for (int k = 0; k < RTX_NBOX(S); ++k, ++oi) {  // simple_geometry.py:251-294
         const DObj ob = S.objs[oi];
-        if (!occ) {
+        const f3 mn = moved(ob, ob.a, time), mx = moved(ob, ob.b, time);
+        const bool maybe = !occ && box_maybe_hit(mn, mx, o, ri, INFINITY);
+        if (!RTX_ANY(maybe)) continue;
+        if (maybe) {
             double start, end;
             int label;
-            if (box_slabs(o, d, moved(ob, ob.a, time), moved(ob, ob.b, time), start, label, end))
+            if (box_slabs(o, d, mn, mx, start, label, end))
                 occ = !(start > end) && 1e-4 < start && start < t_max;
         }
     }
@@ -1202,7 +1227,6 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
             if (RTX_ALL(occ)) break;
             const bool live = !occ && mesh_bv(ob, o, d);
             if (!RTX_ANY(live)) continue;
-            const RayInv ri = ray_inv(o, d);
             for (int li = 0; li < ob.leaf_count;) {  // stackless wave-uniform BVH walk
               cref<DLeaf> L = S.leaves[ob.leaf_begin + li];
               const bool maybe = live && !occ && leaf_maybe_hit(L, o, ri, ob.cmax);

@@ -31,6 +31,12 @@ def random_scene(seed, res=(48, 36), mesh=False):
     for k in range(rng.randint(0, 3)):
         o = {"name": "b%d" % k, "type": "box", "position": r(-2, 2, 3), "size": r(0.3, 1.5, 3),
              "materials": [int(rng.choice(ids))]}
+        if rng.rand() < 0.4:  # given by corners, some axes with min > max (NovelScene2's trails)
+            c, sz = np.array(o.pop("position")), np.array(o.pop("size"))
+            mn, mx = c - sz / 2, c + sz / 2
+            sw = rng.rand(3) < 0.4
+            mn[sw], mx[sw] = mx[sw].copy(), mn[sw].copy()
+            o["min"], o["max"] = np.round(mn, 3).tolist(), np.round(mx, 3).tolist()
         if rng.rand() < 0.3:
             o["speed"] = r(-0.5, 0.5, 3)
         objs.append(o)
