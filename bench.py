@@ -66,8 +66,8 @@ def scene_dict(cfg):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--config", default="tsp1080", choices=sorted(CONFIGS))
     p.add_argument("--rowblock", action="store_true", help="also time row-block + RCCL gather of one frame")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
@@ -179,9 +179,11 @@ def main():
         sc.render_device(out=fb, stream=stream)
     e1.record(stream)
     torch.cuda.synchronize()
+    # each rank's clock stops when its own K frames are done; the closing barrier keeps
+    # every rank inside the bracket and the max over ranks below is the job's time
+    t1 = time.perf_counter()
     if use_dist:
         dist.barrier()
-    t1 = time.perf_counter()
     wall = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
     kern = torch.tensor([e0.elapsed_time(e1) / a.steps], dtype=torch.float64, device="cuda")
     if use_dist:

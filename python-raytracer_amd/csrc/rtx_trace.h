@@ -406,13 +406,126 @@ RTX_HD bool box_slabs(f3 o, f3 d, f3 mn, f3 mx, double& start, int& label, doubl
     return true;
 }
 
+// The same slabs decided in fp32, with box_slabs as the fallback. Each reference quotient
+// t = fl64((bound - o) / d) is estimated as q = fl32(bound - o) * rcp(d): three fp32
+// roundings and v_rcp_f32's 1 ulp give |q - t| <= 2^-22 |q|, so q +- (2^-20 |q| + 2^-100)
+// holds t. Start and end are then known to lie in [s_lo, s_hi] and [e_lo, e_hi], and the
+// entry label is known when the first maximal start is separated from the other axes'.
+// Slabs with 0 < |d| < 2^-20 or a quotient beyond 2^100 (or NaN) leave the lane undecided
+// (so a flushed subnormal numerator, <= 2^-126 * 2^20, stays inside the 2^-100 term).
+struct SlabIv {
+    float s_lo, s_hi, e_lo, e_hi;
+    int label;
+    bool reject;  // certain: a d == 0 slab does not contain the origin (exact comparison)
+    bool sure;    // the intervals and the label hold
+};
+RTX_HD float rcp_approx(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(x);
+#else
+    return 1.0f / x;
+#endif
+}
+RTX_HD SlabIv box_slabs_iv(f3 o, f3 d, f3 mn, f3 mx) {
+    const float ro[3] = {o.x, o.y, o.z};
+    const float rd[3] = {d.x, d.y, d.z};
+    const float lo[3] = {mn.x, mn.y, mn.z};
+    const float hi[3] = {mx.x, mx.y, mx.z};
+    float sc[3], ec[3], w[3];
+    SlabIv r;
+    r.reject = false;
+    r.sure = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        if (rd[k] == 0.0f) {
+            r.reject = r.reject || !(lo[k] < ro[k] && ro[k] < hi[k]);
+            sc[k] = -INFINITY;
+            ec[k] = INFINITY;
+            w[k] = 0.0f;
+        } else {
+            const float rc = rcp_approx(rd[k]);
+            const float q1 = (lo[k] - ro[k]) * rc, q2 = (hi[k] - ro[k]) * rc;
+            sc[k] = fminf(q1, q2);
+            ec[k] = fmaxf(q1, q2);
+            const float m = fmaxf(fabsf(q1), fabsf(q2));
+            w[k] = m * 0x1p-20f + 0x1p-100f;
+            r.sure = r.sure && fabsf(rd[k]) >= 0x1p-20f && m < 0x1p100f;  // false for NaN
+        }
+    }
+    int l = 0;  // max(..., key=start) keeps the first maximum
+    if (sc[1] > sc[l]) l = 1;
+    if (sc[2] > sc[l]) l = 2;
+    r.label = l;
+    r.s_lo = sc[l] - w[l];
+    r.s_hi = sc[l] + w[l];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        if (k != l) r.sure = r.sure && sc[k] + w[k] < r.s_lo;  // false if every d is 0
+    r.e_lo = fminf(fminf(ec[0] - w[0], ec[1] - w[1]), ec[2] - w[2]);
+    r.e_hi = fminf(fminf(ec[0] + w[0], ec[1] + w[1]), ec[2] + w[2]);
+    return r;
+}
+// The reference's start for entry axis k: min(t1, t2) of that axis, i.e. the bound the
+// ray meets first (fl64 division is monotone, so the exact order decides).
+RTX_HD double slab_start64(f3 o, f3 d, f3 mn, f3 mx, int k) {
+    const float ok = k == 0 ? o.x : (k == 1 ? o.y : o.z);
+    const float dk = k == 0 ? d.x : (k == 1 ? d.y : d.z);
+    const float lk = k == 0 ? mn.x : (k == 1 ? mn.y : mn.z);
+    const float hk = k == 0 ? mx.x : (k == 1 ? mx.y : mx.z);
+    const float b = ((hk > lk) == (dk > 0.0f)) ? lk : hk;
+    return ((double)b - (double)ok) / (double)dk;
+}
+// Box entry as the closest-hit test needs it (simple_geometry.py:188-226: valid iff no
+// zero-direction slab rejects, start <= end and start >= 0): fp32 decision, one fp64
+// division for the entry t, the full fp64 slabs for undecided lanes.
+RTX_HD bool box_entry(f3 o, f3 d, f3 mn, f3 mx, bool live, double& start, int& label) {
+    const SlabIv iv = box_slabs_iv(o, d, mn, mx);
+    const bool yes = live && iv.sure && !iv.reject && iv.s_hi < iv.e_lo && iv.s_lo > 0.0f;
+    const bool no = !live || iv.reject || (iv.sure && (iv.s_lo > iv.e_hi || iv.s_hi < 0.0f));
+    label = iv.label;
+    start = 0.0;
+    if (yes) start = slab_start64(o, d, mn, mx, iv.label);
+    bool valid = yes;
+    const bool und = !yes && !no;
+    if (RTX_ANY(und)) {
+        if (und) {
+            double e = 0.0;
+            valid = box_slabs(o, d, mn, mx, start, label, e) && !(start > e || start < 0.0);
+        }
+    }
+    return valid;
+}
+// Box shadow test (simple_geometry.py:251-294): 1e-4 < start < t_max and start <= end.
+RTX_HD bool box_shadow(f3 o, f3 d, f3 mn, f3 mx, double t_max) {
+    const SlabIv iv = box_slabs_iv(o, d, mn, mx);
+    const bool yes = iv.sure && !iv.reject && iv.s_hi < iv.e_lo && iv.s_lo >= kEps4Up && (double)iv.s_hi < t_max;
+    const bool no = iv.reject ||
+                    (iv.sure && (iv.s_lo > iv.e_hi || iv.s_hi < kEps4Up || (double)iv.s_lo >= t_max));
+    bool occ = yes;
+    const bool und = !yes && !no;
+    if (RTX_ANY(und)) {
+        if (und) {
+            double start, end;
+            int label;
+            occ = box_slabs(o, d, mn, mx, start, label, end) && !(start > end) && 1e-4 < start && start < t_max;
+        }
+    }
+    return occ;
+}
+
 // Mesh bounding volume (bounding_volumes.py:18-37 sphere, :49-83 AABB).
 template <class O>
 RTX_HD bool mesh_bv(const O& ob, f3 o, f3 d) {
     if (ob.bv_type == BV_AABB) {
+        // valid iff start <= end and start >= 0 (the fp64 slabs only for undecided lanes)
+        const f3 mn = ld3(ob.bv_a), mx = ld3(ob.bv_b);
+        const SlabIv iv = box_slabs_iv(o, d, mn, mx);
+        const bool yes = iv.sure && !iv.reject && iv.s_hi < iv.e_lo && iv.s_lo > 0.0f;
+        const bool no = iv.reject || (iv.sure && (iv.s_lo > iv.e_hi || iv.s_hi < 0.0f));
+        if (yes || no) return yes;
         double start, end;
         int label;
-        if (!box_slabs(o, d, ld3(ob.bv_a), ld3(ob.bv_b), start, label, end)) return false;
+        if (!box_slabs(o, d, mn, mx, start, label, end)) return false;
         return !(start > end || start < 0.0);
     }
     double b, s, two_a;
@@ -432,7 +545,8 @@ struct RayInv {
 RTX_HD RayInv ray_inv(f3 o, f3 d) {
     auto safe = [](float v) { return fabsf(v) < 1e-30f ? copysignf(1e-30f, v) : v; };
     RayInv r;
-    r.inv = f3{1.0f / safe(d.x), 1.0f / safe(d.y), 1.0f / safe(d.z)};
+    // v_rcp_f32 (1 ulp): its error moves a slab by <= 2^-23 |bound - o|, far inside the pad
+    r.inv = f3{rcp_approx(safe(d.x)), rcp_approx(safe(d.y)), rcp_approx(safe(d.z))};
     r.pad_rel = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
     return r;
 }
@@ -709,13 +823,7 @@ RTX_HD bool leaf_shadow(const SceneView& S, const O& ob, f3 o, f3 d, double t_ma
         const double t = (double)dot(sub(moved(ob, ob.a, time), o), n) / (double)den;
         return 1e-4 < t && t < t_max;
     }
-    if (ob.type == OBJ_BOX) {
-        double start, end;
-        int label;
-        if (!box_slabs(o, d, moved(ob, ob.a, time), moved(ob, ob.b, time), start, label, end)) return false;
-        if (start > end) return false;
-        return 1e-4 < start && start < t_max;
-    }
+    if (ob.type == OBJ_BOX) return box_shadow(o, d, moved(ob, ob.a, time), moved(ob, ob.b, time), t_max);
     if (MESH && ob.type == OBJ_MESH) {
         if (!mesh_bv(ob, o, d)) return false;
         for (int f = 0; f < ob.tri_count; ++f) {
@@ -1127,10 +1235,9 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
         // the fp64 slabs only where some lane's ray may hit the box before its best t
         const bool maybe = box_maybe_hit(mn, mx, o, ri, h.t32);
         if (!RTX_ANY(maybe)) continue;
-        double start = 0.0, end = 0.0;
+        double start = 0.0;
         int label = 0;
-        bool valid = maybe && box_slabs(o, d, mn, mx, start, label, end);
-        valid = valid && !(start > end || start < 0.0);
+        const bool valid = box_entry(o, d, mn, mx, maybe, start, label);
         offer(S, h, valid, (float)start, oi, label, o, d, time);
     }
     if (MESH) {
@@ -1208,18 +1315,13 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
     }
     if (RTX_ALL(occ)) return true;
     RayInv ri{};
-    if (RTX_NBOX(S) > 0 || (MESH && RTX_NMESH(S) > 0)) ri = ray_inv(o, d);
+    if (RTX_NBOX(S) > 0) ri = ray_inv(o, d);  // meshes: only once a lane passes a bounding volume
     for (int k = 0; k < RTX_NBOX(S); ++k, ++oi) {  // simple_geometry.py:251-294
         const DObj ob = S.objs[oi];
         const f3 mn = moved(ob, ob.a, time), mx = moved(ob, ob.b, time);
         const bool maybe = !occ && box_maybe_hit(mn, mx, o, ri, INFINITY);
         if (!RTX_ANY(maybe)) continue;
-        if (maybe) {
-            double start, end;
-            int label;
-            if (box_slabs(o, d, mn, mx, start, label, end))
-                occ = !(start > end) && 1e-4 < start && start < t_max;
-        }
+        if (maybe) occ = box_shadow(o, d, mn, mx, t_max);
     }
     if (MESH) {
         for (int k = 0; k < RTX_NMESH(S); ++k, ++oi) {  // mesh.py:121-153 (no t_max test)
@@ -1227,6 +1329,7 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
             if (RTX_ALL(occ)) break;
             const bool live = !occ && mesh_bv(ob, o, d);
             if (!RTX_ANY(live)) continue;
+            if (RTX_NBOX(S) == 0) ri = ray_inv(o, d);
             for (int li = 0; li < ob.leaf_count;) {  // stackless wave-uniform BVH walk
               cref<DLeaf> L = S.leaves[ob.leaf_begin + li];
               const bool maybe = live && !occ && leaf_maybe_hit(L, o, ri, ob.cmax);

@@ -256,6 +256,18 @@ def bv_stress_rays(lo, hi, n, seed=0):
     return o, d
 
 
+def scene_box_stress_rays(scene_dict, n_per_box, seed=0):
+    """bv_stress_rays around every top-level box of a scene dict (corners as AABB.__init__
+    computes them in fp32: center -+ size / 2, simple_geometry.py:180-185)."""
+    os_, ds_ = [], []
+    for k, b in enumerate(x for x in scene_dict["objects"] if x["type"] == "box"):
+        c, s = np.float32(b["position"]), np.float32(b["size"])
+        o, d = bv_stress_rays(c - s / np.float32(2), c + s / np.float32(2), n_per_box, seed * 7 + k)
+        os_.append(o)
+        ds_.append(d)
+    return np.concatenate(os_), np.concatenate(ds_)
+
+
 def obj_bounds(path):
     """Vertex bounds (float32) of an OBJ file, as Mesh.__init__ computes them for scale 1
     and no translation (mesh.py:31-36)."""

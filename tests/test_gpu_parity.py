@@ -151,6 +151,28 @@ def test_mesh_bv_stress_matches_oracle(seed):
         assert np.array_equal(sc.occluded(o, d, tmax, 0.0), osc.shadow(0.0, o, d, tmax).astype(bool))
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_box_stress_matches_oracle(seed):
+    """Rays inside / on / grazing / aimed at the edges and corners of DepthOfField's two
+    boxes vs the oracle, exactly: the fp32 slab decision (box_slabs_iv), the single fp64
+    entry division and the full fp64 fallback of AABB.intersect / shadow_intersect
+    (simple_geometry.py:188-294), for closest hits and shadows with t_max 1 and inf."""
+    from oracle import oracle as O
+    from scenegen import scene_box_stress_rays
+    dd, base = O.load_bundle("DepthOfField")
+    o, d = scene_box_stress_rays(dd, 10000, seed)
+    sc = product_scene("DepthOfField", (8, 8))
+    osc = O.OracleScene(dd, base)
+    got = sc.intersect(o, d, 0.0)
+    t, ob, _, m, nn, pp = osc.closest(0.0, o, d)
+    assert np.array_equal(got["obj"], ob)
+    hit = ob >= 0
+    assert np.array_equal(got["t"][hit], t[hit])
+    assert np.array_equal(got["normal"][hit], nn[hit])
+    for tmax in (1.0, np.inf):
+        assert np.array_equal(sc.occluded(o, d, tmax, 0.0), osc.shadow(0.0, o, d, tmax).astype(bool))
+
+
 def test_full_size_dof_4k_properties():
     """DepthOfField 3840x2160, AA 2 x DOF 32 (config 5): a 64-row block. Values in [0, 1],
     deterministic, and identical when split into sub-blocks (partition invariance)."""

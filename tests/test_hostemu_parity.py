@@ -101,6 +101,26 @@ def test_hostemu_mesh_bv_stress(seed):
         assert np.array_equal(hostemu.occluded(sc, o, d, tmax, 0.0), osc.shadow(0.0, o, d, tmax).astype(bool))
 
 
+@pytest.mark.parametrize("seed", range(2))
+def test_hostemu_box_stress(seed):
+    """Rays inside / on / grazing / aimed at the edges and corners of DepthOfField's boxes
+    (the fp32 slab decision and its fp64 fallback) vs the oracle, exactly."""
+    from oracle import oracle as O
+    from scenegen import scene_box_stress_rays
+    dd, base = O.load_bundle("DepthOfField")
+    o, d = scene_box_stress_rays(dd, 3000, seed)
+    sc = product_scene("DepthOfField", (8, 8))
+    osc = O.OracleScene(dd, base)
+    got = hostemu.intersect(sc, o, d, 0.0)
+    t, ob, _, m, nn, pp = osc.closest(0.0, o, d)
+    assert np.array_equal(got["obj"], ob)
+    hit = ob >= 0
+    assert np.array_equal(got["t"][hit], t[hit])
+    assert np.array_equal(got["normal"][hit], nn[hit])
+    for tmax in (1.0, np.inf):
+        assert np.array_equal(hostemu.occluded(sc, o, d, tmax, 0.0), osc.shadow(0.0, o, d, tmax).astype(bool))
+
+
 @pytest.mark.parametrize("seed", range(12))
 def test_hostemu_random_scenes(seed):
     from common import oracle_render_dict, product_scene_dict
