@@ -98,39 +98,62 @@ def make_scene(cfg):
     return rtx.load_scene(d, verbose=False)
 
 
-def cpu_baseline(cfg, budget_s):
-    """The oracle (C restatement of the reference, one core) on the same workload:
-    full frames, repeated until the budget is used (whole frames only)."""
+def cpu_threads():
+    """Host threads for the CPU baseline: the GPU box's CPU share (16 per GPU), or fewer
+    cores when the machine has them; RTX_CPU_THREADS overrides."""
+    n = os.environ.get("RTX_CPU_THREADS")
+    if n:
+        return max(1, int(n))
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return max(1, min(16, avail))
+
+
+def cpu_baseline(cfg, budget_s, threads=None):
+    """The oracle (C restatement of the reference) on the same workload, as the reference
+    parallelises it: column strips (scene.py:35-37 `np.array_split`, render.nu's tasks),
+    one strip per host thread (ctypes releases the GIL; every oracle_render call builds
+    its own scene). Whole frames (or the config's fixed sub-sample) repeated until the
+    budget is used."""
+    from concurrent.futures import ThreadPoolExecutor
     from oracle import oracle as O
     name, res, spp, _ = CONFIGS[cfg]
     d, base = scene_dict(cfg)
     osc = O.OracleScene(d, base)
     W, H = res
-    rows = H
+    P = threads or cpu_threads()
+    frac = CPU_STRIPS.get(cfg, 1)  # render the first 1/frac of the columns
+    tasks = P * frac
+    strips = [len(c) for c in np.array_split(np.arange(W), tasks)[:P]]
+    noises = [None] * P
+    if osc.jitter:
+        rs = np.random.RandomState(0)
+        noises = [rs.rand(nc * H * osc.spp_rays * 3) for nc in strips]
+    ncol = sum(strips)
+
+    def one(k):
+        osc.render(k, tasks, noise=noises[k])
+
     nsamp = 0
     frames = 0
-    t0 = time.perf_counter()
-    noise = None
-    while True:
-        if cfg in CPU_STRIPS:
-            # the first of N column strips (tasks=N, subimage 0)
-            ns = CPU_STRIPS[cfg]
-            ncol = len(np.array_split(np.arange(W), ns)[0])
-            if osc.jitter:
-                noise = np.random.RandomState(0).rand(ncol * H * osc.spp_rays * 3)
-            osc.render(0, ns, noise=noise)
+    with ThreadPoolExecutor(P) as ex:
+        t0 = time.perf_counter()
+        while True:
+            list(ex.map(one, range(P)))
             nsamp += ncol * H * osc.n_samples
-            sample = "columns 0..%d of %dx%d (1/%d of the frame) per repeat" % (ncol - 1, W, H, ns)
-        else:
-            osc.render()
-            nsamp += W * rows * osc.n_samples
-            sample = "full %dx%d frame(s)" % (W, H)
-        frames += 1
-        if time.perf_counter() - t0 >= budget_s:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": nsamp / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
-            "sample": "%s x %d repeats in %.1f s (oracle/rtx_oracle.c, gcc -O2, 1 thread)" % (sample, frames, dt)}
+            frames += 1
+            if time.perf_counter() - t0 >= budget_s:
+                break
+        dt = time.perf_counter() - t0
+    if frac == 1:
+        sample = "full %dx%d frame(s)" % (W, H)
+    else:
+        sample = "columns 0..%d of %dx%d (1/%d of the frame)" % (ncol - 1, W, H, frac)
+    return {"value": nsamp / dt / 1e6, "unit": "Mrays/s", "cores": P, "kind": "port",
+            "sample": "%s x %d repeats in %.1f s; %d column strips (np.array_split, as render.nu) on %d host "
+                      "threads (oracle/rtx_oracle.c, gcc -O2)" % (sample, frames, dt, P, P)}
 
 
 def main():
