@@ -23,6 +23,8 @@ using __hip_internal::uint64_t;
 
 #define RTX_HD __host__ __device__ __forceinline__
 
+#include "rtx_fastmath.h"
+
 // Read-only scene and camera tables are addressed as the AMDGPU constant address space in
 // device code: wave-uniform reads of them become scalar (s_load) reads through the
 // constant cache. The host-emulation build (tests only) sees plain pointers.
@@ -67,10 +69,17 @@ RTX_HD f3 cross(f3 a, f3 b) {
 }
 // glm::normalize = v * inversesqrt(dot(v, v)), inversesqrt(x) = 1 / sqrt(x)
 RTX_HD f3 normalize(f3 v) {
+    const float q = dot(v, v);
 #if RTX_ABLATE == 6 && defined(__HIP_DEVICE_COMPILE__)
-    float inv = __builtin_amdgcn_rsqf(dot(v, v));  // cost probe only
+    float inv = __builtin_amdgcn_rsqf(q);  // cost probe only
 #else
-    float inv = 1.0f / sqrtf(dot(v, v));
+#if defined(__HIP_DEVICE_COMPILE__)
+    // the same IEEE results from the hardware approximations (rtx_fastmath.h) when every
+    // active lane's dot is in range -- the common case; the compiler's sequence otherwise
+    const bool fast = q >= fm::kLo && q < fm::kHi;  // false for NaN
+    if (__all((int)fast)) return scale(v, fm::rcp_rn(fm::sqrt_rn(q)));
+#endif
+    float inv = 1.0f / sqrtf(q);
 #endif
     return scale(v, inv);
 }

@@ -11,6 +11,7 @@ LIB = os.path.join(HERE, "native", "librtx_hostemu.so")
 DEPS = [SRC, os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_api.hip"),
         os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_trace.h"),
         os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_kernels.h"),
+        os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_fastmath.h"),
         os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_jit_sources.inc"),
         os.path.join(HERE, "..", "include", "rtx.h")]
 
