@@ -723,6 +723,23 @@ struct JitEntry {
 std::mutex g_jit_mu;
 std::map<std::string, JitEntry> g_jit;
 
+// Sample-parallel mapping (render_body_spp) for the hierarchy/texture kernels when a
+// pixel has >= RTX_SPP_MIN samples (default 16): a wave then traces one pixel's nearly
+// identical AA/time samples, so the wave-uniform subtree culling stays effective
+// (NovelScene1 108 -> 30 ms, NovelScene2 741 -> 161 ms). The flat-scene kernels keep
+// the 8x8-tile mapping, whose waves are already coherent (same lens sample across a
+// tile; DepthOfField 4K: 11.1 ms tiles vs 19.3 ms sample-parallel). RTX_SPP=0 never
+// uses it, RTX_SPP=1 always (tests compare both mappings).
+bool use_spp_mode(int spp, bool ext) {
+    if (spp < 1 || spp >= (1 << 20)) return false;  // udiv_small's range
+    const char* e = getenv("RTX_SPP");
+    if (e && e[0] == '0') return false;
+    if (e && e[0] == '1') return true;
+    const char* m = getenv("RTX_SPP_MIN");
+    const int lo = (m && *m) ? atoi(m) : 16;
+    return ext && spp >= lo;
+}
+
 bool jit_enabled() {
     const char* e = getenv("RTX_JIT");
     return !(e && e[0] == '0');
@@ -735,7 +752,8 @@ std::string jit_cache_dir() {
 }
 
 // Returns the specialized kernel, or nullptr (the caller then launches the generic one).
-hipFunction_t jit_render_kernel(const SceneView& v, int fc_mode, bool mesh, bool sec, bool ext, bool cnt, bool jit) {
+hipFunction_t jit_render_kernel(const SceneView& v, int fc_mode, bool mesh, bool sec, bool ext, bool cnt, bool jit,
+                                bool spp) {
     if (!jit_enabled()) return nullptr;
     if (v.n_plane + v.n_sphere + v.n_box + v.n_mesh > 32 || v.n_lights > 8) return nullptr;  // code size
     // CSG/texture kernels: the unrolled loops raise their (already high) register
@@ -763,9 +781,11 @@ hipFunction_t jit_render_kernel(const SceneView& v, int fc_mode, bool mesh, bool
     // kernel name: rtx_jit_render_<mesh><sec><ext><count><jitter> (tells profiles apart)
     std::string name = "rtx_jit_render_";
     for (bool f : {mesh, sec, ext, cnt, jit}) name += f ? '1' : '0';
+    if (spp) name += "_spp";
     const std::string src = std::string("#include \"rtx_kernels.h\"\nextern \"C\" __global__ RTX_RENDER_BOUNDS(") +
                             b(mesh) + ", " + b(sec) + ", " + b(ext) + ") void " + name + "(const rtx::KParams* "
-                            "__restrict__ P, const rtx::Launch L) {\n  rtx::render_body<" + b(mesh) + ", " + b(sec) +
+                            "__restrict__ P, const rtx::Launch L) {\n  rtx::" + (spp ? "render_body_spp<" : "render_body<") +
+                            b(mesh) + ", " + b(sec) +
                             ", " + b(ext) + ", " + b(cnt) + ", " + b(jit) + ">(P, L);\n}\n";
     std::string key = src;
     for (const auto& o : opts) key += "\n" + o;
@@ -1007,23 +1027,35 @@ int rtx_render(rtx_scene* s, int32_t row0, int32_t nrows, float* fb_dev, uint64_
     L.row0 = row0;
     L.nrows = nrows;
     L.counters = reinterpret_cast<unsigned long long*>(counters_dev);
-    const int64_t items = launch_items(nrows, s->kp.ncols);
     hipStream_t st = (hipStream_t)stream;
     const bool cnt = counters_dev != nullptr;
     const bool jit = s->kp.jitter != RTX_JITTER_OFF;
     const int sel = (s->has_mesh ? 16 : 0) | (s->has_secondary ? 8 : 0) | (s->has_ext ? 4 : 0) | (cnt ? 2 : 0) | (jit ? 1 : 0);
     const KParams* kp = s->d_kp;
     const size_t hbytes = (size_t)s->hlevels * 9 * sizeof(float);
-    if (hipFunction_t fn = jit_render_kernel(s->view, s->fc_mode, s->has_mesh, s->has_secondary, s->has_ext, cnt, jit)) {
-        const int blk = s->has_ext ? kBlock<true> : kBlock<false>;
+    const int blk = s->has_ext ? kBlock<true> : kBlock<false>;
+    const int spp = s->kp.n_dof * s->kp.n_aa * s->kp.n_times;
+    const bool spp_mode = use_spp_mode(spp, s->has_ext);
+    // pixel mapping: one lane per pixel (8x8 tiles per wave); sample-parallel: blocks of
+    // spp_pixels_per_block pixels (rtx_kernels.h render_body_spp)
+    const int64_t nblocks = spp_mode ? ((int64_t)nrows * s->kp.ncols + spp_pixels_per_block(spp, blk) - 1) /
+                                           spp_pixels_per_block(spp, blk)
+                                     : (launch_items(nrows, s->kp.ncols) + blk - 1) / blk;
+    if (nblocks > 0x7fffffff) return fail(RTX_ERR_INVALID, "rtx_render: launch too large");
+    if (hipFunction_t fn = jit_render_kernel(s->view, s->fc_mode, s->has_mesh, s->has_secondary, s->has_ext, cnt, jit,
+                                             spp_mode)) {
         void* args[] = {(void*)&kp, (void*)&L};
-        RTX_HIP(hipModuleLaunchKernel(fn, (unsigned)((items + blk - 1) / blk), 1, 1, blk, 1, 1,
+        RTX_HIP(hipModuleLaunchKernel(fn, (unsigned)nblocks, 1, 1, blk, 1, 1,
                                       s->has_ext ? (unsigned)(hbytes * blk) : 0u, st, args, nullptr));
         return RTX_OK;
     }
 #define RTX_LAUNCH(M, S, X, C, J)                                                                              \
-    hipLaunchKernelGGL((k_render<M, S, X, C, J>), dim3((unsigned)((items + kBlock<X> - 1) / kBlock<X>)),   \
-                       dim3(kBlock<X>), X ? hbytes * kBlock<X> : 0, st, kp, L)
+    if (spp_mode)                                                                                              \
+        hipLaunchKernelGGL((k_render_spp<M, S, X, C, J>), dim3((unsigned)nblocks), dim3(kBlock<X>),          \
+                           X ? hbytes * kBlock<X> : 0, st, kp, L);                                            \
+    else                                                                                                       \
+        hipLaunchKernelGGL((k_render<M, S, X, C, J>), dim3((unsigned)nblocks), dim3(kBlock<X>),              \
+                           X ? hbytes * kBlock<X> : 0, st, kp, L)
 #define RTX_CASE(n) \
     case n: RTX_LAUNCH(((n) & 16) != 0, ((n) & 8) != 0, ((n) & 4) != 0, ((n) & 2) != 0, ((n) & 1) != 0); break
     switch (sel) {

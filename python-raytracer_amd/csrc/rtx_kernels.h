@@ -49,6 +49,41 @@ __device__ __forceinline__ void flush_tally(const Tally& tl, unsigned long long*
     }
 }
 
+// scene.py:54-55: base_ray_direction and focal_point of pixel (column cc, reference row j).
+RTX_HD f3 pixel_focal(const KParams& P, int32_t cc, int j) {
+    const float fx = P.xs[cc];
+    const float fy = P.ys[j];
+    // base_ray_direction = normalize(x * u + y * v - d * w)  (scene.py:54)
+    const f3 bdir = normalize(sub(add(scale(ld3(P.u), fx), scale(ld3(P.v), fy)), ld3(P.dw)));
+    return add(ld3(P.pos), scale(bdir, P.focal));  // scene.py:55
+}
+
+// scene.py:60-65: the origin of AA sample ka of DOF sample kd, jittered (JIT).
+template <bool JIT>
+RTX_HD f3 sample_origin(const KParams& P, int32_t cc, int j, int kd, int ka) {
+    f3 o = ld3(P.aa_o + 3 * (kd * P.n_aa + ka));
+    if (JIT) {  // scene.py:63-65
+        f3 rnd;
+        if (P.jitter == RTX_JITTER_REPLAY) {
+            const int64_t idx = (((int64_t)cc * P.height + j) * P.n_dof + kd) * P.n_aa + ka;
+            rnd = ld3(P.noise + 3 * idx);
+        } else if (RTX_ABLATE == 15) {  // cost probe only: no RNG
+            rnd = mk(0.25f + 0.001f * (float)ka, 0.5f, 0.75f + 0.001f * (float)kd);
+        } else {
+            uint32_t ctr[4] = {(uint32_t)(P.col0 + cc), (uint32_t)j, (uint32_t)(kd * P.n_aa + ka), 0u};
+            philox4x32(ctr, P.seed_lo, P.seed_hi);
+            rnd = mk((float)(ctr[0] >> 8) * 0x1p-24f, (float)(ctr[1] >> 8) * 0x1p-24f,
+                     (float)(ctr[2] >> 8) * 0x1p-24f);
+        }
+        o = add(o, scale(normalize(rnd), P.jscale));
+    }
+    return o;
+}
+
+// colour / (samples * dof_samples * len(motion_times)) (scene.py:73); for a power of two
+// the exact reciprocal multiply gives the identical correctly rounded result.
+RTX_HD float sample_mean(const KParams& P, float c) { return P.div_pow2 ? c * P.inv_divisor : c / P.divisor; }
+
 // scene.py:47-79 for pixel p of the output block (host/device: the tests-only host
 // emulation runs the same body).
 template <bool MESH, bool SEC, bool X, bool COUNT, bool JIT>
@@ -60,46 +95,24 @@ RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, 
         return;
     }
     const int j = P.height - 1 - (row0 + rr);  // reference row index (y grows upward)
-    const float fx = P.xs[cc];
-    const float fy = P.ys[j];
-    // base_ray_direction = normalize(x * u + y * v - d * w)  (scene.py:54)
-    const f3 bdir = normalize(sub(add(scale(ld3(P.u), fx), scale(ld3(P.v), fy)), ld3(P.dw)));
-    const f3 focal = add(ld3(P.pos), scale(bdir, P.focal));  // scene.py:55
+    const f3 focal = pixel_focal(P, cc, j);
     f3 colour = mk(0.0f, 0.0f, 0.0f);
     for (int kd = 0; kd < P.n_dof; ++kd) {
         const f3 ddir = normalize(sub(focal, ld3(P.dof_o + 3 * kd)));  // scene.py:58
         for (int ka = 0; ka < P.n_aa; ++ka) {
-            f3 o = ld3(P.aa_o + 3 * (kd * P.n_aa + ka));
-            if (JIT) {  // scene.py:63-65
-                f3 rnd;
-                if (P.jitter == RTX_JITTER_REPLAY) {
-                    const int64_t idx = (((int64_t)cc * P.height + j) * P.n_dof + kd) * P.n_aa + ka;
-                    rnd = ld3(P.noise + 3 * idx);
-                } else if (RTX_ABLATE == 15) {  // cost probe only: no RNG
-                    rnd = mk(0.25f + 0.001f * (float)ka, 0.5f, 0.75f + 0.001f * (float)kd);
-                } else {
-                    uint32_t ctr[4] = {(uint32_t)(P.col0 + cc), (uint32_t)j, (uint32_t)(kd * P.n_aa + ka), 0u};
-                    philox4x32(ctr, P.seed_lo, P.seed_hi);
-                    rnd = mk((float)(ctr[0] >> 8) * 0x1p-24f, (float)(ctr[1] >> 8) * 0x1p-24f,
-                             (float)(ctr[2] >> 8) * 0x1p-24f);
-                }
-                o = add(o, scale(normalize(rnd), P.jscale));
-            }
+            const f3 o = sample_origin<JIT>(P, cc, j, kd, ka);
             for (int kt = 0; kt < P.n_times; ++kt)
                 colour = add(colour, cast_ray<MESH, SEC, X, COUNT>(P.S, o, ddir, P.times[kt], tl, fs, hs));
         }
     }
-    // colour / (samples * dof_samples * len(motion_times)) (scene.py:73); for a power of
-    // two the exact reciprocal multiply gives the identical correctly rounded result.
-    if (P.div_pow2) colour = scale(colour, P.inv_divisor);
-    else colour = divs(colour, P.divisor);
+    colour = mk(sample_mean(P, colour.x), sample_mean(P, colour.y), sample_mean(P, colour.z));
 #if RTX_ABLATE == 11 && defined(__HIP_DEVICE_COMPILE__)
     {  // cost probe only: RTX_PAD extra VALU instructions per pixel in 4 independent chains
-        float c0 = colour.x, c1 = colour.y, c2 = colour.z, c3 = fx;
+        float c0 = colour.x, c1 = colour.y, c2 = colour.z, c3 = focal.x;
 #pragma unroll
         for (int k = 0; k < RTX_PAD / 4; ++k)
             asm volatile("v_add_f32 %0, %4, %0\n v_add_f32 %1, %4, %1\n v_add_f32 %2, %4, %2\n v_add_f32 %3, %4, %3"
-                         : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3) : "v"(fy));
+                         : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3) : "v"(focal.y));
         colour = mk(c0, c1, c2 + c3 * 0.0f);
     }
 #endif
@@ -186,12 +199,104 @@ __device__ __forceinline__ void render_body(const KParams* __restrict__ Pp, cons
     flush_tally<COUNT>(tl, L.counters, any_active);
 }
 
+// n / d and n % d for 0 <= n < 2^22, d >= 1 (rd = fl32(1 / d)): the fp32 quotient is
+// off by at most one, which the remainder test corrects. Full-rate 24-bit multiplies.
+__device__ __forceinline__ int udiv_small(int n, int d, float rd, int& rem) {
+    int q = (int)((float)n * rd);
+    int r = n - (int)__umul24((unsigned)q, (unsigned)d);
+    if (r >= d) { ++q; r -= d; }
+    if (r < 0) { --q; r += d; }
+    rem = r;
+    return q;
+}
+
+// Pixels per block of the sample-parallel mapping (host and device agree on it).
+__host__ __device__ inline int spp_pixels_per_block(int spp, int block) { return spp >= block ? 1 : block / spp; }
+
+// Sample-parallel mapping for high sample counts (rtx_render picks it for the hierarchy /
+// texture kernels when a pixel has >= RTX_SPP_MIN samples): the B lanes of a block trace the samples of P = B / spp
+// consecutive pixels (row-major within the output block), or the samples of one pixel
+// in ceil(spp / B) rounds, so a wave's rays start from one pixel (coherent) and a wave
+// lasts one sample instead of all of them. Each lane puts its sample's colour in LDS;
+// per (pixel, channel) one owner lane then adds them in the reference's order
+// (dof, aa, time; scene.py:57-70) starting from +0 -- the same fp32 sums as
+// render_pixel -- and writes the mean. Samples s map to (kd, ka, kt) with kt fastest.
+template <bool MESH, bool SEC, bool X, bool COUNT, bool JIT>
+__device__ __forceinline__ void render_body_spp(const KParams* __restrict__ Pp, const Launch L) {
+    constexpr int B = kBlock<X>;
+    const KParams& P = *Pp;
+    const int32_t ncols = P.ncols;
+    const int nt = P.n_times, na = P.n_aa;
+    const int S = P.n_dof * na * nt;
+    const int PPB = spp_pixels_per_block(S, B);
+    const int rounds = (PPB * S + B - 1) / B;
+    const float rS = 1.0f / (float)S, rT = 1.0f / (float)nt, rA = 1.0f / (float)na;
+    Tally tl = {};
+    __shared__ float frames[SEC ? kMaxDepth * 4 * B : 1];
+    __shared__ float sbuf[3 * B];
+    extern __shared__ float hstack[];  // X: [level][9][thread] (dynamic size)
+    const FrameStack fs{frames + threadIdx.x, B};
+    const HStack hs{hstack + threadIdx.x, B};
+    const int64_t npix = (int64_t)L.nrows * ncols;
+    const int64_t pix0 = (int64_t)blockIdx.x * PPB;
+    const int tid = threadIdx.x;
+    float acc = 0.0f;  // rounds > 1 (one pixel per block): lane ch < 3 sums channel ch
+    bool any_active = false;
+    for (int rd = 0; rd < rounds; ++rd) {
+        const int flat = rd * B + tid;  // the block's sample index
+        int s;
+        const int lp = udiv_small(flat, S, rS, s);
+        const int64_t p = pix0 + lp;
+        const bool active = lp < PPB && p < npix;
+        f3 c = mk(0.0f, 0.0f, 0.0f);
+        if (active) {
+            any_active = true;
+            const int32_t rr = (int32_t)(p / ncols), cc = (int32_t)(p - (int64_t)rr * ncols);
+            const int j = P.height - 1 - (L.row0 + rr);
+            int kt, ka;
+            const int da = udiv_small(s, nt, rT, kt);
+            const int kd = udiv_small(da, na, rA, ka);
+            const f3 focal = pixel_focal(P, cc, j);
+            const f3 ddir = normalize(sub(focal, ld3(P.dof_o + 3 * kd)));  // scene.py:58
+            const f3 o = sample_origin<JIT>(P, cc, j, kd, ka);
+            c = cast_ray<MESH, SEC, X, COUNT>(P.S, o, ddir, P.times[kt], tl, fs, hs);
+        }
+        sbuf[tid] = c.x;
+        sbuf[B + tid] = c.y;
+        sbuf[2 * B + tid] = c.z;
+        __syncthreads();
+        if (rounds == 1) {  // (pixel, channel) pairs, each summed in order by one lane
+            for (int q = tid; q < 3 * PPB; q += B) {
+                const int pp = q / 3, ch = q - 3 * (q / 3);
+                if (pix0 + pp < npix) {
+                    const float* src = sbuf + ch * B + pp * S;
+                    float a = 0.0f;
+                    for (int k = 0; k < S; ++k) a += src[k];
+                    L.fb[3 * (pix0 + pp) + ch] = sample_mean(P, a);
+                }
+            }
+        } else if (tid < 3) {  // this round's samples of the block's pixel
+            const int hi = min(S - rd * B, B);
+            const float* src = sbuf + tid * B;
+            for (int k = 0; k < hi; ++k) acc += src[k];
+        }
+        if (rounds > 1) __syncthreads();  // sbuf is reused by the next round
+    }
+    if (rounds > 1 && tid < 3 && pix0 < npix) L.fb[3 * pix0 + tid] = sample_mean(P, acc);
+    flush_tally<COUNT>(tl, L.counters, any_active);
+}
+
 #define RTX_RENDER_BOUNDS(MESH, SEC, X) __launch_bounds__(rtx::kBlock<X>, (X) ? 1 : RTX_LB_WAVES(MESH, SEC))
 
 #if !defined(__HIPCC_RTC__)
 template <bool MESH, bool SEC, bool X, bool COUNT, bool JIT>
 __global__ RTX_RENDER_BOUNDS(MESH, SEC, X) void k_render(const KParams* __restrict__ Pp, const Launch L) {
     render_body<MESH, SEC, X, COUNT, JIT>(Pp, L);
+}
+
+template <bool MESH, bool SEC, bool X, bool COUNT, bool JIT>
+__global__ RTX_RENDER_BOUNDS(MESH, SEC, X) void k_render_spp(const KParams* __restrict__ Pp, const Launch L) {
+    render_body_spp<MESH, SEC, X, COUNT, JIT>(Pp, L);
 }
 
 template <bool MESH, bool X>

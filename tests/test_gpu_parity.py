@@ -289,3 +289,47 @@ def test_scene_specialized_kernel_equals_generic(name, res, edits, monkeypatch):
     cnt_b = torch.zeros(16, dtype=torch.int64, device="cuda")
     b = sc.render_device(counters=cnt_b).clone()
     assert torch.equal(a, b) and torch.equal(cnt_a, cnt_b)
+
+
+SPP_CASES = CASES + [
+    ("NovelScene1", (96, 48), {"AA": {"jitter": False, "samples": 2}}),
+    ("NovelScene2", (64, 32), {"AA": {"jitter": False, "samples": 1}}),
+]
+
+
+@pytest.mark.parametrize("name,res,edits", SPP_CASES)
+def test_sample_parallel_mapping_matches_oracle(name, res, edits, monkeypatch):
+    """The sample-parallel mapping (render_body_spp, forced for every sample count, 1 to
+    NovelScene2's 240) vs the oracle: exact, i.e. the owner lanes' in-order LDS sums equal
+    the reference's per-pixel accumulation."""
+    monkeypatch.setenv("RTX_SPP", "1")
+    sc = product_scene(name, res, **edits)
+    W, H = res
+    fb = torch.full((H, W, 3), float("nan"), dtype=torch.float32, device="cuda")  # every pixel must be written
+    sc.render_device(out=fb)
+    img = np.ascontiguousarray(np.transpose(fb.cpu().numpy()[::-1], (1, 0, 2))).astype(np.float64)
+    assert np.isfinite(img).all(), "pixels left unwritten"
+    s = assert_parity(img, oracle_render(name, res, **edits), name)
+    assert s["frac_diff"] == 0.0, s
+
+
+@pytest.mark.parametrize("name,res,edits,rows", [
+    ("DepthOfField", (3840, 2160), {"AA": {"jitter": True, "samples": 2}}, (1000, 40)),
+    ("DepthOfField", (97, 61), {"AA": {"jitter": True, "samples": 3}}, (0, 61)),
+    ("MotionBlur", (75, 64), {}, (0, 64)),
+    ("NovelScene1", (256, 128), {"AA": {"jitter": True, "samples": 2}}, (0, 128)),
+    ("NovelScene2", (128, 64), {}, (17, 20)),
+    ("TwoSpheresPlane", (160, 90), {"AA": {"jitter": True, "samples": 5}}, (3, 80)),
+])
+def test_sample_parallel_equals_pixel_mapping(name, res, edits, rows, monkeypatch):
+    """Both mappings on the production (Philox) jitter: identical framebuffers (bitwise)
+    and ray counters, on row blocks that start mid-frame."""
+    sc = product_scene(name, res, **edits)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("RTX_SPP", mode)
+        cnt = torch.zeros(16, dtype=torch.int64, device="cuda")
+        fb = torch.full((rows[1], res[0], 3), float("nan"), dtype=torch.float32, device="cuda")
+        out[mode] = (sc.render_device(row0=rows[0], nrows=rows[1], out=fb, counters=cnt), cnt)
+    assert torch.equal(out["0"][0], out["1"][0])
+    assert torch.equal(out["0"][1], out["1"][1])
