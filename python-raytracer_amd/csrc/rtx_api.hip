@@ -27,6 +27,7 @@
 
 #include "../../include/rtx.h"
 #include "rtx_kernels.h"
+#include "rtx_launch.h"
 
 // faces per mesh BVH leaf (cluster); meshes of at most kFaceCullMaxFaces faces also
 // test each face's box before its exact test (DObj::face_cull)
@@ -1038,10 +1039,12 @@ int rtx_render(rtx_scene* s, int32_t row0, int32_t nrows, float* fb_dev, uint64_
     const bool spp_mode = use_spp_mode(spp, s->has_ext);
     // pixel mapping: one lane per pixel (8x8 tiles per wave); sample-parallel: blocks of
     // spp_pixels_per_block pixels (rtx_kernels.h render_body_spp)
-    const int64_t nblocks = spp_mode ? ((int64_t)nrows * s->kp.ncols + spp_pixels_per_block(spp, blk) - 1) /
-                                           spp_pixels_per_block(spp, blk)
-                                     : (launch_items(nrows, s->kp.ncols) + blk - 1) / blk;
-    if (nblocks > 0x7fffffff) return fail(RTX_ERR_INVALID, "rtx_render: launch too large");
+    auto blocks = [&](bool sm) {
+        return sm ? ((int64_t)nrows * s->kp.ncols + spp_pixels_per_block(spp, blk) - 1) / spp_pixels_per_block(spp, blk)
+                  : (launch_items(nrows, s->kp.ncols) + blk - 1) / blk;
+    };
+    int64_t nblocks = blocks(spp_mode);
+    if (nblocks > 0x7fffffff || blocks(false) > 0x7fffffff) return fail(RTX_ERR_INVALID, "rtx_render: launch too large");
     if (hipFunction_t fn = jit_render_kernel(s->view, s->fc_mode, s->has_mesh, s->has_secondary, s->has_ext, cnt, jit,
                                              spp_mode)) {
         void* args[] = {(void*)&kp, (void*)&L};
@@ -1049,20 +1052,23 @@ int rtx_render(rtx_scene* s, int32_t row0, int32_t nrows, float* fb_dev, uint64_
                                       s->has_ext ? (unsigned)(hbytes * blk) : 0u, st, args, nullptr));
         return RTX_OK;
     }
-#define RTX_LAUNCH(M, S, X, C, J)                                                                              \
-    if (spp_mode)                                                                                              \
-        hipLaunchKernelGGL((k_render_spp<M, S, X, C, J>), dim3((unsigned)nblocks), dim3(kBlock<X>),          \
-                           X ? hbytes * kBlock<X> : 0, st, kp, L);                                            \
-    else                                                                                                       \
-        hipLaunchKernelGGL((k_render<M, S, X, C, J>), dim3((unsigned)nblocks), dim3(kBlock<X>),              \
-                           X ? hbytes * kBlock<X> : 0, st, kp, L)
+    if (s->has_ext) {  // precompiled in rtx_kern_ext_m{0,1}.hip
+        const RenderLaunch rl{kp, (unsigned)nblocks, hbytes * kBlock<true>, st, spp_mode};
+        RTX_HIP(s->has_mesh ? launch_render_ext_m1(sel, rl, L) : launch_render_ext_m0(sel, rl, L));
+        return RTX_OK;
+    }
+    // the flat-scene kernels use the tile mapping here (their sample-parallel variants
+    // are reached through the scene-specialized kernels only)
+    if (spp_mode) nblocks = blocks(false);
+#define RTX_LAUNCH(M, S, C, J) \
+    hipLaunchKernelGGL((k_render<M, S, false, C, J>), dim3((unsigned)nblocks), dim3(kBlock<false>), 0, st, kp, L)
 #define RTX_CASE(n) \
-    case n: RTX_LAUNCH(((n) & 16) != 0, ((n) & 8) != 0, ((n) & 4) != 0, ((n) & 2) != 0, ((n) & 1) != 0); break
+    case n: RTX_LAUNCH(((n) & 16) != 0, ((n) & 8) != 0, ((n) & 2) != 0, ((n) & 1) != 0); break
     switch (sel) {
-        RTX_CASE(0); RTX_CASE(1); RTX_CASE(2); RTX_CASE(3); RTX_CASE(4); RTX_CASE(5); RTX_CASE(6); RTX_CASE(7);
-        RTX_CASE(8); RTX_CASE(9); RTX_CASE(10); RTX_CASE(11); RTX_CASE(12); RTX_CASE(13); RTX_CASE(14); RTX_CASE(15);
-        RTX_CASE(16); RTX_CASE(17); RTX_CASE(18); RTX_CASE(19); RTX_CASE(20); RTX_CASE(21); RTX_CASE(22); RTX_CASE(23);
-        RTX_CASE(24); RTX_CASE(25); RTX_CASE(26); RTX_CASE(27); RTX_CASE(28); RTX_CASE(29); RTX_CASE(30); RTX_CASE(31);
+        RTX_CASE(0); RTX_CASE(1); RTX_CASE(2); RTX_CASE(3);
+        RTX_CASE(8); RTX_CASE(9); RTX_CASE(10); RTX_CASE(11);
+        RTX_CASE(16); RTX_CASE(17); RTX_CASE(18); RTX_CASE(19);
+        RTX_CASE(24); RTX_CASE(25); RTX_CASE(26); RTX_CASE(27);
     }
 #undef RTX_CASE
 #undef RTX_LAUNCH

@@ -1,0 +1,31 @@
+// Hierarchy/texture render kernels with MESH = false (tile and sample-parallel mappings):
+// a translation unit of their own so they compile in parallel with the rest of librtx.so.
+#include <hip/hip_runtime.h>
+
+#define RTX_EXT_TU 1
+#include "rtx_kernels.h"
+#include "rtx_launch.h"
+
+namespace rtx {
+
+hipError_t launch_render_ext_m0(int sel, const RenderLaunch& r, const Launch& L) {
+    constexpr int B = kBlock<true>;
+#define RTX_EXT_LAUNCH(S, C, J)                                                                          \
+    if (r.spp)                                                                                           \
+        hipLaunchKernelGGL((k_render_spp<false, S, true, C, J>), dim3(r.nblocks), dim3(B), r.lds_bytes,  \
+                           r.stream, r.kp, L);                                                           \
+    else                                                                                                 \
+        hipLaunchKernelGGL((k_render<false, S, true, C, J>), dim3(r.nblocks), dim3(B), r.lds_bytes,      \
+                           r.stream, r.kp, L)
+#define RTX_EXT_CASE(n) \
+    case n: RTX_EXT_LAUNCH(((n) & 8) != 0, ((n) & 2) != 0, ((n) & 1) != 0); break
+    switch (sel & 11) {
+        RTX_EXT_CASE(0); RTX_EXT_CASE(1); RTX_EXT_CASE(2); RTX_EXT_CASE(3);
+        RTX_EXT_CASE(8); RTX_EXT_CASE(9); RTX_EXT_CASE(10); RTX_EXT_CASE(11);
+    }
+#undef RTX_EXT_CASE
+#undef RTX_EXT_LAUNCH
+    return hipGetLastError();
+}
+
+}  // namespace rtx

@@ -342,11 +342,13 @@ __global__ __launch_bounds__(256) void k_occluded(SceneView S, int64_t n, const 
     occ[i] = occluded<MESH, X, false>(S, o, d, tmax[i], time, tl, hs) ? 1 : 0;
 }
 
+#if !defined(RTX_EXT_TU)  // defined once, in rtx_api.hip
 __global__ __launch_bounds__(256) void k_to_rgb8(const float* __restrict__ fb, uint8_t* __restrict__ out, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     out[i] = (uint8_t)(int)((double)fb[i] * 255.0);
 }
+#endif
 #endif  // !__HIPCC_RTC__
 
 }  // namespace rtx

@@ -1,0 +1,23 @@
+// rtx_launch.h — launchers of the precompiled hierarchy/texture (X) render kernels, which
+// live in their own translation units (rtx_kern_ext_m0.hip / _m1.hip, by MESH) so the
+// library's largest kernels compile in parallel.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace rtx {
+struct KParams;
+struct Launch;
+
+struct RenderLaunch {
+    const KParams* kp;
+    unsigned nblocks;
+    size_t lds_bytes;  // dynamic LDS (hierarchy stacks)
+    hipStream_t stream;
+    bool spp;          // sample-parallel mapping (render_body_spp)
+};
+
+// sel: (SEC ? 8 : 0) | (COUNT ? 2 : 0) | (JITTER ? 1 : 0); returns hipGetLastError().
+hipError_t launch_render_ext_m0(int sel, const RenderLaunch& r, const Launch& L);
+hipError_t launch_render_ext_m1(int sel, const RenderLaunch& r, const Launch& L);
+}  // namespace rtx

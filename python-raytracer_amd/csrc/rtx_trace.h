@@ -932,7 +932,7 @@ RTX_HD bool pt_in(const float RTX_CONST* lo, const float RTX_CONST* hi, f3 p) {
 #if RTX_HIER_INLINE >= 2
 #define RTX_HX RTX_HD
 #else
-#define RTX_HX __host__ __device__ __attribute__((noinline))
+#define RTX_HX __host__ __device__ __attribute__((noinline)) inline
 #endif
 
 // is_inside(x, p) for p in the frame of x's parent's children (hierarchy.py:111-129).

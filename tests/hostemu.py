@@ -12,6 +12,7 @@ DEPS = [SRC, os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_api.h
         os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_trace.h"),
         os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_kernels.h"),
         os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_fastmath.h"),
+        os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_launch.h"),
         os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_jit_sources.inc"),
         os.path.join(HERE, "..", "include", "rtx.h")]
 

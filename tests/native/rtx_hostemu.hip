@@ -4,6 +4,13 @@
 // (python-raytracer_amd/rtx) never loads this library, and it has no HIP calls.
 #include "../../python-raytracer_amd/csrc/rtx_api.hip"
 
+// the hierarchy/texture kernels live in their own translation units; the host emulation
+// never launches a kernel
+namespace rtx {
+hipError_t launch_render_ext_m0(int, const RenderLaunch&, const Launch&) { return hipErrorNotSupported; }
+hipError_t launch_render_ext_m1(int, const RenderLaunch&, const Launch&) { return hipErrorNotSupported; }
+}  // namespace rtx
+
 #include <omp.h>
 
 namespace {

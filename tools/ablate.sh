@@ -17,7 +17,7 @@ for n in ${VARIANTS:-0 1 2 3}; do
   if [ "$fl" = "none" ]; then cp python-raytracer_amd/rtx/_lib/librtx.so "$ABL_DIR/librtx_$n.so"; continue; fi
   if [ -n "${PREBUILT:-}" ] && [ -f "$ABL_DIR/librtx_$n.so" ]; then continue; fi
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared $fl \
-    -o "$ABL_DIR/librtx_$n.so" python-raytracer_amd/csrc/rtx_api.hip -lhiprtc || exit 1
+    -o "$ABL_DIR/librtx_$n.so" python-raytracer_amd/csrc/rtx_api.hip python-raytracer_amd/csrc/rtx_kern_ext_m0.hip python-raytracer_amd/csrc/rtx_kern_ext_m1.hip -lhiprtc || exit 1
 done
 for n in ${VARIANTS:-0 1 2 3}; do
   for c in ${CONFIGS:-tsp1080}; do

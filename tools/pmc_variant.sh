@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 for n in ${VARIANTS:-0}; do
   fl_var="FLAGS_$n"; fl="${!fl_var:--DRTX_ABLATE=$n}"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared $fl \
-    -o /tmp/rtx_ablate/librtx_$n.so python-raytracer_amd/csrc/rtx_api.hip -lhiprtc || exit 1
+    -o /tmp/rtx_ablate/librtx_$n.so python-raytracer_amd/csrc/rtx_api.hip python-raytracer_amd/csrc/rtx_kern_ext_m0.hip python-raytracer_amd/csrc/rtx_kern_ext_m1.hip -lhiprtc || exit 1
   RTX_LIB_OVERRIDE=/tmp/rtx_ablate/librtx_$n.so timeout -k 10 240 rocprofv3 --kernel-trace \
     --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SMEM \
     -d "$OUT/$n" -o pmc --output-format csv -- python3 tools/prof_driver.py --config ${CFG:-tsp1080} --iters 5 > "$OUT/$n.log" 2>&1 || exit 1
