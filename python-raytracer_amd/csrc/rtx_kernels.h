@@ -131,10 +131,12 @@ struct Launch {
 };
 
 // Occupancy request (waves per SIMD) by kernel variant: mesh kernels without secondary
-// rays fit 128 VGPRs without scratch and gain from 4 waves/SIMD; the others spill if
-// forced below their natural allocation (measured, tools/ablate.sh).
+// rays fit 128 VGPRs without scratch and gain from 4 waves/SIMD; the flat primary+shadow
+// kernels from 5 (DepthOfField 4K 11.2 -> 10.2 ms; TwoSpheresPlane already fits); the
+// secondary-ray kernels lose if forced below their natural allocation (measured,
+// tools/ablate.sh: 6 and 8 waves are slower everywhere).
 #ifndef RTX_LB_WAVES
-#define RTX_LB_WAVES(MESH, SEC) ((MESH) && !(SEC) ? 4 : 1)
+#define RTX_LB_WAVES(MESH, SEC) ((SEC) ? 1 : ((MESH) ? 4 : 5))
 #endif
 #ifndef RTX_TILE
 #define RTX_TILE 1
