@@ -753,8 +753,8 @@ std::string jit_cache_dir() {
 }
 
 // Returns the specialized kernel, or nullptr (the caller then launches the generic one).
-hipFunction_t jit_render_kernel(const SceneView& v, int fc_mode, bool mesh, bool sec, bool ext, bool cnt, bool jit,
-                                bool spp) {
+hipFunction_t jit_render_kernel(const SceneView& v, const KParams& kp, int fc_mode, bool mesh, bool sec, bool ext,
+                                bool cnt, bool jit, bool spp) {
     if (!jit_enabled()) return nullptr;
     if (v.n_plane + v.n_sphere + v.n_box + v.n_mesh > 32 || v.n_lights > 8) return nullptr;  // code size
     // CSG/texture kernels: the unrolled loops raise their (already high) register
@@ -773,7 +773,12 @@ hipFunction_t jit_render_kernel(const SceneView& v, int fc_mode, bool mesh, bool
                                      "-DRTX_FIXED_NB=" + std::to_string(v.n_box),
                                      "-DRTX_FIXED_NM=" + std::to_string(v.n_mesh),
                                      "-DRTX_FIXED_NL=" + std::to_string(v.n_lights),
-                                     "-DRTX_FACE_CULL_MODE=" + std::to_string(fc_mode)};
+                                     "-DRTX_FACE_CULL_MODE=" + std::to_string(fc_mode),
+                                     // the camera's sample counts (the 1-spp loops vanish)
+                                     "-DRTX_FIXED_SAMPLES",
+                                     "-DRTX_FIXED_NDOF=" + std::to_string(kp.n_dof),
+                                     "-DRTX_FIXED_NAA=" + std::to_string(kp.n_aa),
+                                     "-DRTX_FIXED_NTIMES=" + std::to_string(kp.n_times)};
     if (const char* extra = getenv("RTX_JIT_FLAGS")) {  // experiments (tools/ablate.sh); part of the cache key
         std::istringstream is(extra);
         for (std::string o; is >> o;) opts.push_back(o);
@@ -1045,8 +1050,8 @@ int rtx_render(rtx_scene* s, int32_t row0, int32_t nrows, float* fb_dev, uint64_
     };
     int64_t nblocks = blocks(spp_mode);
     if (nblocks > 0x7fffffff || blocks(false) > 0x7fffffff) return fail(RTX_ERR_INVALID, "rtx_render: launch too large");
-    if (hipFunction_t fn = jit_render_kernel(s->view, s->fc_mode, s->has_mesh, s->has_secondary, s->has_ext, cnt, jit,
-                                             spp_mode)) {
+    if (hipFunction_t fn = jit_render_kernel(s->view, s->kp, s->fc_mode, s->has_mesh, s->has_secondary, s->has_ext, cnt,
+                                             jit, spp_mode)) {
         void* args[] = {(void*)&kp, (void*)&L};
         RTX_HIP(hipModuleLaunchKernel(fn, (unsigned)nblocks, 1, 1, blk, 1, 1,
                                       s->has_ext ? (unsigned)(hbytes * blk) : 0u, st, args, nullptr));

@@ -49,6 +49,18 @@ __device__ __forceinline__ void flush_tally(const Tally& tl, unsigned long long*
     }
 }
 
+// Sample counts per pixel; the scene-specialized kernels pin them (with the camera's
+// values) so the sample loops of the 1-spp configs disappear.
+#ifdef RTX_FIXED_SAMPLES
+#define RTX_NDOF(P) RTX_FIXED_NDOF
+#define RTX_NAA(P) RTX_FIXED_NAA
+#define RTX_NTIMES(P) RTX_FIXED_NTIMES
+#else
+#define RTX_NDOF(P) (P).n_dof
+#define RTX_NAA(P) (P).n_aa
+#define RTX_NTIMES(P) (P).n_times
+#endif
+
 // scene.py:54-55: base_ray_direction and focal_point of pixel (column cc, reference row j).
 RTX_HD f3 pixel_focal(const KParams& P, int32_t cc, int j) {
     const float fx = P.xs[cc];
@@ -61,16 +73,16 @@ RTX_HD f3 pixel_focal(const KParams& P, int32_t cc, int j) {
 // scene.py:60-65: the origin of AA sample ka of DOF sample kd, jittered (JIT).
 template <bool JIT>
 RTX_HD f3 sample_origin(const KParams& P, int32_t cc, int j, int kd, int ka) {
-    f3 o = ld3(P.aa_o + 3 * (kd * P.n_aa + ka));
+    f3 o = ld3(P.aa_o + 3 * (kd * RTX_NAA(P) + ka));
     if (JIT) {  // scene.py:63-65
         f3 rnd;
         if (P.jitter == RTX_JITTER_REPLAY) {
-            const int64_t idx = (((int64_t)cc * P.height + j) * P.n_dof + kd) * P.n_aa + ka;
+            const int64_t idx = (((int64_t)cc * P.height + j) * RTX_NDOF(P) + kd) * RTX_NAA(P) + ka;
             rnd = ld3(P.noise + 3 * idx);
         } else if (RTX_ABLATE == 15) {  // cost probe only: no RNG
             rnd = mk(0.25f + 0.001f * (float)ka, 0.5f, 0.75f + 0.001f * (float)kd);
         } else {
-            uint32_t ctr[4] = {(uint32_t)(P.col0 + cc), (uint32_t)j, (uint32_t)(kd * P.n_aa + ka), 0u};
+            uint32_t ctr[4] = {(uint32_t)(P.col0 + cc), (uint32_t)j, (uint32_t)(kd * RTX_NAA(P) + ka), 0u};
             philox4x32(ctr, P.seed_lo, P.seed_hi);
             rnd = mk((float)(ctr[0] >> 8) * 0x1p-24f, (float)(ctr[1] >> 8) * 0x1p-24f,
                      (float)(ctr[2] >> 8) * 0x1p-24f);
@@ -97,11 +109,15 @@ RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, 
     const int j = P.height - 1 - (row0 + rr);  // reference row index (y grows upward)
     const f3 focal = pixel_focal(P, cc, j);
     f3 colour = mk(0.0f, 0.0f, 0.0f);
-    for (int kd = 0; kd < P.n_dof; ++kd) {
+    // pinned counts must not unroll the loops (one cast_ray body per sample)
+#pragma unroll 1
+    for (int kd = 0; kd < RTX_NDOF(P); ++kd) {
         const f3 ddir = normalize(sub(focal, ld3(P.dof_o + 3 * kd)));  // scene.py:58
-        for (int ka = 0; ka < P.n_aa; ++ka) {
+#pragma unroll 1
+        for (int ka = 0; ka < RTX_NAA(P); ++ka) {
             const f3 o = sample_origin<JIT>(P, cc, j, kd, ka);
-            for (int kt = 0; kt < P.n_times; ++kt)
+#pragma unroll 1
+            for (int kt = 0; kt < RTX_NTIMES(P); ++kt)
                 colour = add(colour, cast_ray<MESH, SEC, X, COUNT>(P.S, o, ddir, P.times[kt], tl, fs, hs));
         }
     }
@@ -228,8 +244,8 @@ __device__ __forceinline__ void render_body_spp(const KParams* __restrict__ Pp, 
     constexpr int B = kBlock<X>;
     const KParams& P = *Pp;
     const int32_t ncols = P.ncols;
-    const int nt = P.n_times, na = P.n_aa;
-    const int S = P.n_dof * na * nt;
+    const int nt = RTX_NTIMES(P), na = RTX_NAA(P);
+    const int S = RTX_NDOF(P) * na * nt;
     const int PPB = spp_pixels_per_block(S, B);
     const int rounds = (PPB * S + B - 1) / B;
     const float rS = 1.0f / (float)S, rT = 1.0f / (float)nt, rA = 1.0f / (float)na;
@@ -288,7 +304,10 @@ __device__ __forceinline__ void render_body_spp(const KParams* __restrict__ Pp, 
     flush_tally<COUNT>(tl, L.counters, any_active);
 }
 
-#define RTX_RENDER_BOUNDS(MESH, SEC, X) __launch_bounds__(rtx::kBlock<X>, (X) ? 1 : RTX_LB_WAVES(MESH, SEC))
+#ifndef RTX_LB_XWAVES  // hierarchy/texture kernels: waves per SIMD requested (experiments)
+#define RTX_LB_XWAVES 1
+#endif
+#define RTX_RENDER_BOUNDS(MESH, SEC, X) __launch_bounds__(rtx::kBlock<X>, (X) ? RTX_LB_XWAVES : RTX_LB_WAVES(MESH, SEC))
 
 #if !defined(__HIPCC_RTC__)
 template <bool MESH, bool SEC, bool X, bool COUNT, bool JIT>
