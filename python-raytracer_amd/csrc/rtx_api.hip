@@ -759,7 +759,10 @@ hipFunction_t jit_render_kernel(const SceneView& v, const KParams& kp, int fc_mo
     if (v.n_plane + v.n_sphere + v.n_box + v.n_mesh > 32 || v.n_lights > 8) return nullptr;  // code size
     // CSG/texture kernels: the unrolled loops raise their (already high) register
     // pressure and the specialized kernel measured slower (NovelScene1 105 -> 134 ms)
-    if (ext) return nullptr;
+    if (ext) {
+        const char* e = getenv("RTX_JIT_EXT");  // experiment: specialize them anyway
+        if (!(e && e[0] == '1')) return nullptr;
+    }
     int device = 0;
     if (hipGetDevice(&device) != hipSuccess) return nullptr;
     hipDeviceProp_t prop;
