@@ -753,8 +753,8 @@ std::string jit_cache_dir() {
 }
 
 // Returns the specialized kernel, or nullptr (the caller then launches the generic one).
-hipFunction_t jit_render_kernel(const SceneView& v, const KParams& kp, int fc_mode, bool mesh, bool sec, bool ext,
-                                bool cnt, bool jit, bool spp) {
+hipFunction_t jit_render_kernel(const SceneView& v, const KParams& kp, int fc_mode, bool any_speed, uint32_t ldir,
+                                bool mesh, bool sec, bool ext, bool cnt, bool jit, bool spp) {
     if (!jit_enabled()) return nullptr;
     if (v.n_plane + v.n_sphere + v.n_box + v.n_mesh > 32 || v.n_lights > 8) return nullptr;  // code size
     // CSG/texture kernels: the unrolled loops raise their (already high) register
@@ -781,7 +781,12 @@ hipFunction_t jit_render_kernel(const SceneView& v, const KParams& kp, int fc_mo
                                      "-DRTX_FIXED_SAMPLES",
                                      "-DRTX_FIXED_NDOF=" + std::to_string(kp.n_dof),
                                      "-DRTX_FIXED_NAA=" + std::to_string(kp.n_aa),
-                                     "-DRTX_FIXED_NTIMES=" + std::to_string(kp.n_times)};
+                                     "-DRTX_FIXED_NTIMES=" + std::to_string(kp.n_times),
+                                     // static scene, light kinds, pow loop length, divisor kind
+                                     "-DRTX_FIXED_STATIC=" + std::to_string(any_speed ? 0 : 1),
+                                     "-DRTX_FIXED_LDIR=" + std::to_string(ldir) + "u",
+                                     "-DRTX_FIXED_POWBITS=" + std::to_string(v.pow_bits),
+                                     "-DRTX_FIXED_DIVPOW2=" + std::to_string(kp.div_pow2)};
     if (const char* extra = getenv("RTX_JIT_FLAGS")) {  // experiments (tools/ablate.sh); part of the cache key
         std::istringstream is(extra);
         for (std::string o; is >> o;) opts.push_back(o);
@@ -857,6 +862,8 @@ struct rtx_scene {
     SceneView view{};
     bool has_mesh = false, has_secondary = false, has_ext = false;
     int fc_mode = 0;  // RTX_FACE_CULL_MODE of the top-level meshes: 0 none, 1 all, 2 mixed
+    bool any_speed = false;  // some top-level object moves (else the JIT pins a static scene)
+    uint32_t light_dir_mask = 0;  // bit i: light i is directional (JIT, <= 8 lights)
     int32_t hlevels = 0;
     // host copies for the per-time-range hierarchy bounds
     std::vector<DNode> h_nodes;
@@ -949,6 +956,9 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
         for (const DObj& o : H.objs)
             if (o.type == RTX_MESH) { ++n_m; n_fc += o.face_cull ? 1 : 0; }
         s->fc_mode = n_fc == 0 ? 0 : n_fc == n_m ? 1 : 2;
+        for (const DObj& o : H.objs) s->any_speed = s->any_speed || o.has_speed;
+        for (size_t i = 0; i < H.lights.size() && i < 32; ++i)
+            if (H.lights[i].type == LIGHT_DIRECTIONAL) s->light_dir_mask |= 1u << i;
     }
     if (!H.nodes.empty()) {
         s->h_nodes = H.nodes;
@@ -1053,8 +1063,8 @@ int rtx_render(rtx_scene* s, int32_t row0, int32_t nrows, float* fb_dev, uint64_
     };
     int64_t nblocks = blocks(spp_mode);
     if (nblocks > 0x7fffffff || blocks(false) > 0x7fffffff) return fail(RTX_ERR_INVALID, "rtx_render: launch too large");
-    if (hipFunction_t fn = jit_render_kernel(s->view, s->kp, s->fc_mode, s->has_mesh, s->has_secondary, s->has_ext, cnt,
-                                             jit, spp_mode)) {
+    if (hipFunction_t fn = jit_render_kernel(s->view, s->kp, s->fc_mode, s->any_speed, s->light_dir_mask, s->has_mesh,
+                                             s->has_secondary, s->has_ext, cnt, jit, spp_mode)) {
         void* args[] = {(void*)&kp, (void*)&L};
         RTX_HIP(hipModuleLaunchKernel(fn, (unsigned)nblocks, 1, 1, blk, 1, 1,
                                       s->has_ext ? (unsigned)(hbytes * blk) : 0u, st, args, nullptr));

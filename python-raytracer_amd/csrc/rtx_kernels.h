@@ -94,7 +94,13 @@ RTX_HD f3 sample_origin(const KParams& P, int32_t cc, int j, int kd, int ka) {
 
 // colour / (samples * dof_samples * len(motion_times)) (scene.py:73); for a power of two
 // the exact reciprocal multiply gives the identical correctly rounded result.
-RTX_HD float sample_mean(const KParams& P, float c) { return P.div_pow2 ? c * P.inv_divisor : c / P.divisor; }
+RTX_HD float sample_mean(const KParams& P, float c) {
+#ifdef RTX_FIXED_DIVPOW2
+    return RTX_FIXED_DIVPOW2 ? c * P.inv_divisor : c / P.divisor;
+#else
+    return P.div_pow2 ? c * P.inv_divisor : c / P.divisor;
+#endif
+}
 
 // scene.py:47-79 for pixel p of the output block (host/device: the tests-only host
 // emulation runs the same body).

@@ -242,7 +242,12 @@ template <class O, class P>
 RTX_HD f3 moved(const O& o, P p, float time) {
     // `p + self.speed * self.scene.current_time` (simple_geometry.py:21-24, :106-109, :189-194)
     f3 q = ld3(p);
+#if defined(RTX_FIXED_STATIC) && RTX_FIXED_STATIC
+    (void)o;
+    (void)time;  // scene-specialized kernel of a scene without speeds
+#else
     if (o.has_speed) q = add(q, scale(ld3(o.speed), time));
+#endif
     return q;
 }
 
@@ -1453,9 +1458,14 @@ RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const 
     tally_inc<COUNT>(tl, &Tally::shade);
     for (int li = 0; li < RTX_NLIGHTS(S); ++li) {
         const DLight L = S.lights[li];
+#ifdef RTX_FIXED_LDIR  // scene-specialized: bit li set = directional
+        const bool point = ((RTX_FIXED_LDIR >> li) & 1u) == 0u;
+#else
+        const bool point = L.type == LIGHT_POINT;
+#endif
         f3 sdir;
         double t_max;
-        if (L.type == LIGHT_POINT) {
+        if (point) {
             sdir = sub(ld3(L.vec), pos);
             t_max = 1.0;
         } else {
@@ -1465,14 +1475,18 @@ RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const 
         tally_inc<COUNT>(tl, &Tally::shadow);
         if (RTX_ABLATE != 1 && occluded<MESH, X, COUNT>(S, pos, sdir, t_max, time, tl, hs)) continue;
         if (RTX_ABLATE == 3) { colour = add(colour, mul(ld3(L.cp), diffuse)); continue; }
-        f3 light_dir = L.type == LIGHT_POINT ? normalize(sdir) : ld3(L.ndir);
+        f3 light_dir = point ? normalize(sdir) : ld3(L.ndir);
         f3 lambert = scale(diffuse, pos_part(dot(normal, light_dir)));
         f3 ls = lambert;
         if (!m.spec_zero) {
             f3 half_vect = normalize(sub(light_dir, dir));
             float nh = dot(normal, half_vect);
             double base = nh > 0.0f ? (double)nh : 0.0;
+#ifdef RTX_FIXED_POWBITS
+            f3 specular = scale(ld3(m.specular), (float)spec_pow(base, m, RTX_FIXED_POWBITS));
+#else
             f3 specular = scale(ld3(m.specular), (float)spec_pow(base, m, S.pow_bits));
+#endif
             ls = add(lambert, specular);
         }
         // spec_zero: specular == +0 and diffuse >= +0, so lambert + specular == lambert exactly
