@@ -6,8 +6,8 @@ One step = one 1920x1080 1-spp frame of TwoSpheresPlane rendered by each rank (t
 primary sample is the reference's unit: its tqdm bar counts W*H*aa*dof*|times|,
 provided/scene.py:45,71). With N ranks the job renders N frames per step, one per GPU
 (frame-parallel weak scaling; no data-path collective). ``--rowblock`` additionally times
-the north-star strong-scaling form: one frame split into row blocks across ranks and
-gathered to rank 0 over RCCL.
+the north-star strong-scaling form: one frame split across ranks (interleaved 8-row groups,
+which balance sky and ground rows) and gathered to rank 0 over RCCL.
 
 Launch: python bench.py [--steps K --warmup W]          (N = 1)
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -169,7 +169,7 @@ def main():
     if use_dist:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import rtx  # noqa: F401
-    from rtx.scene import split_rows
+    from rtx.scene import group_rows
 
     sc = make_scene(a.config)
     W, H = sc.vc.width, sc.vc.height
@@ -222,21 +222,22 @@ def main():
     if a.rowblock and use_dist:
         from rtx.distributed import render_frame
         for _ in range(3):
-            render_frame(sc, rank, world, dtype=torch.uint8)
+            render_frame(sc, rank, world, dtype=torch.uint8, interleave=True)
         torch.cuda.synchronize()
         dist.barrier()
         r0 = time.perf_counter()
         nrb = max(5, a.steps // 2)
         for _ in range(nrb):
-            render_frame(sc, rank, world, dtype=torch.uint8)
+            render_frame(sc, rank, world, dtype=torch.uint8, interleave=True)
         torch.cuda.synchronize()
         dist.barrier()
         rb = torch.tensor([time.perf_counter() - r0], dtype=torch.float64, device="cuda")
         dist.all_reduce(rb, op=dist.ReduceOp.MAX)
         rb_ms = float(rb.item()) * 1e3 / nrb
         rowblock = {"ms_per_frame": rb_ms, "Mrays_s": W * H * spp / rb_ms / 1e3, "scaling": "strong",
-                    "gather": "uint8 row blocks to rank 0 (torch.distributed.gather, RCCL)",
-                    "rows_per_rank": split_rows(H, world, 0)[1]}
+                    "gather": "uint8 interleaved 8-row groups (rtx_render_groups) to rank 0 "
+                              "(torch.distributed.gather, RCCL)",
+                    "rows_per_rank": max(len(group_rows(H, world, r)) for r in range(world))}
 
     if rank == 0:
         achieved = b_alg / (kern_ms * 1e-3) / 1e9

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define RTX_ABI_VERSION 2
+#define RTX_ABI_VERSION 3
 
 typedef enum rtx_status {
     RTX_OK = 0,
@@ -185,6 +185,18 @@ int rtx_camera_set(rtx_scene* scene, const rtx_camera_desc* cam);
  * rotated by main.py's rot90. */
 int rtx_render(rtx_scene* scene, int32_t row0, int32_t nrows, float* fb_dev,
                uint64_t* counters_dev, void* hip_stream);
+
+/* Multi-GPU load balance (no reference counterpart: the reference splits columns across
+ * processes, provided/scene.py:36-37 + render.nu): renders the 8-row groups phase,
+ * phase + stride, phase + 2 stride, ... of the image (row 0 = top), packed in order into
+ * fb_dev: float32 [rtx_group_rows(height, phase, stride)][ncols][3]. Rank r of N calls
+ * it with (r, N), so every rank gets rows from the whole frame (sky and ground alike).
+ * Pixel values equal rtx_render's for the same rows. */
+int rtx_render_groups(rtx_scene* scene, int32_t phase, int32_t stride, float* fb_dev,
+                      uint64_t* counters_dev, void* hip_stream);
+
+/* Rows rtx_render_groups writes for an image of `height` rows (-1: bad arguments). */
+int32_t rtx_group_rows(int32_t height, int32_t phase, int32_t stride);
 
 /* Closest hit of n rays (SoA device arrays ray_o_dev/ray_d_dev = [3][n] fp32) at one
  * motion time. Outputs: t (fp64, +inf on miss), object index (-1), material index (-1),

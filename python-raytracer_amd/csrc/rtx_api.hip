@@ -1034,6 +1034,10 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     return RTX_OK;
 }
 
+namespace {
+int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream);
+}
+
 int rtx_render(rtx_scene* s, int32_t row0, int32_t nrows, float* fb_dev, uint64_t* counters_dev, void* stream) {
     if (!s) return fail(RTX_ERR_INVALID, "rtx_render: null scene");
     if (!s->cam_set) return fail(RTX_ERR_STATE, "rtx_render: rtx_camera_set was not called");
@@ -1045,6 +1049,41 @@ int rtx_render(rtx_scene* s, int32_t row0, int32_t nrows, float* fb_dev, uint64_
     L.fb = fb_dev;
     L.row0 = row0;
     L.nrows = nrows;
+    L.gphase = 0;
+    L.gstride = 0;
+    return render_launch(s, L, counters_dev, stream);
+}
+
+int32_t rtx_group_rows(int32_t height, int32_t phase, int32_t stride) {
+    if (height < 0 || stride < 1 || phase < 0 || phase >= stride) return -1;
+    const int32_t groups = (height + 7) / 8;
+    if (phase >= groups) return 0;
+    const int32_t mine = (groups - 1 - phase) / stride + 1;  // groups phase, phase + stride, ...
+    int32_t rows = mine * 8;
+    if ((groups - 1) % stride == phase) rows -= groups * 8 - height;  // the short last group
+    return rows;
+}
+
+int rtx_render_groups(rtx_scene* s, int32_t phase, int32_t stride, float* fb_dev, uint64_t* counters_dev,
+                      void* stream) {
+    if (!s) return fail(RTX_ERR_INVALID, "rtx_render_groups: null scene");
+    if (!s->cam_set) return fail(RTX_ERR_STATE, "rtx_render_groups: rtx_camera_set was not called");
+    const int32_t nrows = rtx_group_rows(s->kp.height, phase, stride);
+    if (nrows < 0) return fail(RTX_ERR_INVALID, "rtx_render_groups: need 0 <= phase < stride");
+    if (nrows == 0) return RTX_OK;
+    if (!fb_dev) return fail(RTX_ERR_INVALID, "rtx_render_groups: null framebuffer");
+    Launch L;
+    L.fb = fb_dev;
+    L.row0 = 0;
+    L.nrows = nrows;
+    L.gphase = phase;
+    L.gstride = stride;
+    return render_launch(s, L, counters_dev, stream);
+}
+
+namespace {
+int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream) {
+    const int32_t nrows = L.nrows;
     L.counters = reinterpret_cast<unsigned long long*>(counters_dev);
     hipStream_t st = (hipStream_t)stream;
     const bool cnt = counters_dev != nullptr;
@@ -1093,6 +1132,7 @@ int rtx_render(rtx_scene* s, int32_t row0, int32_t nrows, float* fb_dev, uint64_
     RTX_HIP(hipGetLastError());
     return RTX_OK;
 }
+}  // namespace
 
 namespace {
 // The scene view for one motion time (hierarchy bounds uploaded in stream order).

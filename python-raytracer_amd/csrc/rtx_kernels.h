@@ -150,7 +150,15 @@ struct Launch {
     float* fb;
     unsigned long long* counters;
     int32_t row0, nrows;
+    // gstride > 0 (rtx_render_groups): the block's rows are the 8-row groups gphase,
+    // gphase + gstride, ... of the image, packed in order
+    int32_t gphase, gstride;
 };
+
+// Image row (row 0 = top) of block row rr.
+__host__ __device__ inline int32_t image_row(const Launch& L, int32_t rr) {
+    return L.gstride > 0 ? ((rr >> 3) * L.gstride + L.gphase) * 8 + (rr & 7) : L.row0 + rr;
+}
 
 // Occupancy request (waves per SIMD) by kernel variant: mesh kernels without secondary
 // rays fit 128 VGPRs without scratch and gain from 4 waves/SIMD; the flat primary+shadow
@@ -218,7 +226,8 @@ __device__ __forceinline__ void render_body(const KParams* __restrict__ Pp, cons
         const PixelRC px = pixel_rc(ncols, sub);
         const bool active = px.r < L.nrows && px.c < ncols;
         any_active = any_active || active;
-        if (active) render_pixel<MESH, SEC, X, COUNT, JIT>(*Pp, L.fb, L.row0, px.r, px.c, tl, fs, hs);
+        // render_pixel's image row is row0 + rr: pass the image row of px.r as that sum
+        if (active) render_pixel<MESH, SEC, X, COUNT, JIT>(*Pp, L.fb, image_row(L, px.r) - px.r, px.r, px.c, tl, fs, hs);
     }
     flush_tally<COUNT>(tl, L.counters, any_active);
 }
@@ -276,7 +285,7 @@ __device__ __forceinline__ void render_body_spp(const KParams* __restrict__ Pp, 
         if (active) {
             any_active = true;
             const int32_t rr = (int32_t)(p / ncols), cc = (int32_t)(p - (int64_t)rr * ncols);
-            const int j = P.height - 1 - (L.row0 + rr);
+            const int j = P.height - 1 - image_row(L, rr);
             int kt, ka;
             const int da = udiv_small(s, nt, rT, kt);
             const int kd = udiv_small(da, na, rA, ka);

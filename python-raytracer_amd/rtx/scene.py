@@ -46,6 +46,14 @@ def split_rows(height, n, k):
     return k * base + min(k, extra), base + (1 if k < extra else 0)
 
 
+def group_rows(height, n, k):
+    """Image rows (row 0 = top) of rank k's interleaved 8-row groups k, k + n, ... (the
+    rows rtx_render_groups packs, in order), as an int64 array."""
+    g = np.arange(k, (height + 7) // 8, n)
+    rows = (g[:, None] * 8 + np.arange(8)[None, :]).ravel()
+    return rows[rows < height]
+
+
 class _NativeScene:
     """Owns an rtx_scene handle (device buffers live until destroy)."""
 
@@ -260,11 +268,18 @@ class Scene:
         return t
 
     # ------------------------------------------------------------------ rendering
-    def render_device(self, subimage=0, tasks=1, row0=0, nrows=None, out=None, counters=None, stream=None):
+    def render_device(self, subimage=0, tasks=1, row0=0, nrows=None, out=None, counters=None, stream=None,
+                      groups=None):
         """Render image rows [row0, row0 + nrows) (row 0 = top) of the strip into a float32
         CUDA tensor [nrows, strip_width, 3] (the rot90'd reference image). Asynchronous
-        on ``stream`` (default: torch's current stream)."""
+        on ``stream`` (default: torch's current stream). ``groups=(k, n)`` instead renders
+        the interleaved 8-row groups k, k + n, ... (rows ``group_rows(H, n, k)``, packed)."""
         t = self._set_camera(subimage, tasks)
+        if groups is not None:
+            k, n = groups
+            nrows = int(N.load().rtx_group_rows(self.vc.height, int(k), int(n)))
+            if nrows < 0:
+                raise ValueError("groups=(k, n) needs 0 <= k < n")
         if nrows is None:
             nrows = self.vc.height - row0
         if out is None:
@@ -276,8 +291,13 @@ class Scene:
                                      or not counters.is_cuda):
             raise ValueError("counters must be an int64 CUDA tensor with >= %d entries" % N.RTX_COUNTERS)
         st = stream if stream is not None else torch.cuda.current_stream()
-        N.call("rtx_render", self._native.h, int(row0), int(nrows), C.c_void_p(out.data_ptr()),
-               C.c_void_p(counters.data_ptr() if counters is not None else 0), C.c_void_p(st.cuda_stream))
+        cnt = C.c_void_p(counters.data_ptr() if counters is not None else 0)
+        if groups is not None:
+            N.call("rtx_render_groups", self._native.h, int(groups[0]), int(groups[1]), C.c_void_p(out.data_ptr()),
+                   cnt, C.c_void_p(st.cuda_stream))
+        else:
+            N.call("rtx_render", self._native.h, int(row0), int(nrows), C.c_void_p(out.data_ptr()), cnt,
+                   C.c_void_p(st.cuda_stream))
         return out
 
     def render(self, subimage: int = 0, tasks: int = 1) -> np.ndarray:

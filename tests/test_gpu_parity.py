@@ -333,3 +333,24 @@ def test_sample_parallel_equals_pixel_mapping(name, res, edits, rows, monkeypatc
         out[mode] = (sc.render_device(row0=rows[0], nrows=rows[1], out=fb, counters=cnt), cnt)
     assert torch.equal(out["0"][0], out["1"][0])
     assert torch.equal(out["0"][1], out["1"][1])
+
+
+@pytest.mark.parametrize("name,res,edits", [
+    ("MirrorRefraction", (160, 181), {}),
+    ("DepthOfField", (96, 77), {"AA": {"jitter": True, "samples": 2}}),
+    ("NovelScene1", (64, 45), {"AA": {"jitter": True, "samples": 2}}),
+    ("TorusMesh", (64, 64), {}),
+])
+def test_interleaved_row_groups_equal_full_frame(name, res, edits):
+    """rtx_render_groups (multi-GPU load balance): each rank's packed 8-row groups are
+    exactly the full frame's rows group_rows(H, n, k), for tile and sample-parallel kernels."""
+    from rtx.scene import group_rows
+    sc = product_scene(name, res, **edits)
+    full = sc.render_device().clone()
+    H = res[1]
+    for n in (2, 3, 8):
+        for k in range(n):
+            rows = group_rows(H, n, k)
+            fb = torch.full((len(rows), res[0], 3), float("nan"), dtype=torch.float32, device="cuda")
+            got = sc.render_device(groups=(k, n), out=fb)
+            assert torch.equal(got, full[torch.as_tensor(rows, device="cuda")]), (n, k)

@@ -18,7 +18,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def test_library_exports_every_header_symbol():
     hdr = open(os.path.join(REPO, "include", "rtx.h")).read()
-    decl = set(re.findall(r"^(?:int|const char\*)\s+(rtx_\w+)\s*\(", hdr, re.M))
+    decl = set(re.findall(r"^(?:int|int32_t|const char\*)\s+(rtx_\w+)\s*\(", hdr, re.M))
     assert decl == set(N.EXPORTS)
     lib = N.load()
     for sym in decl:

@@ -36,10 +36,18 @@ def _worker(rank, world, port, name, res, out_q):
         fb = np.ascontiguousarray(np.transpose(img, (1, 0, 2))[::-1]).astype(np.float32)
         return torch.from_numpy(fb[row0:row0 + nrows].copy())
 
+    def group(rws):  # interleaved 8-row groups: the given image rows
+        img, _ = hostemu.render(sc, threads=2)
+        fb = np.ascontiguousarray(np.transpose(img, (1, 0, 2))[::-1]).astype(np.float32)
+        return torch.from_numpy(fb[rws].copy())
+
     for dtype in (torch.float32, torch.uint8):
         frame = render_frame(sc, rank, world, render_rows=rows, dtype=dtype)
         if rank == 0:
             out_q.put((str(dtype), frame.numpy()))
+        frame = render_frame(sc, rank, world, render_rows=group, dtype=dtype, interleave=True)
+        if rank == 0:
+            out_q.put(("interleaved " + str(dtype), frame.numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -54,7 +62,7 @@ def test_gather_row_blocks(world, res):
     procs = [ctx.Process(target=_worker, args=(r, world, port, "MirrorRefraction", res, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = dict(q.get(timeout=120) for _ in range(2))
+    got = dict(q.get(timeout=120) for _ in range(4))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -62,6 +70,24 @@ def test_gather_row_blocks(world, res):
     fb_ref = np.transpose(ref, (1, 0, 2))[::-1].astype(np.float32)
     assert np.array_equal(got["torch.float32"], fb_ref)
     assert np.array_equal(got["torch.uint8"], O.to_png_array(ref))
+    assert np.array_equal(got["interleaved torch.float32"], fb_ref)
+    assert np.array_equal(got["interleaved torch.uint8"], O.to_png_array(ref))
+
+
+@pytest.mark.parametrize("height", [1, 7, 8, 9, 23, 64, 181, 1080, 2160])
+def test_interleaved_groups_partition_the_rows(height):
+    """group_rows (Python) and rtx_group_rows (C ABI, host-only) agree, and the ranks'
+    8-row groups partition the image rows."""
+    from rtx import _native as N
+    from rtx.scene import group_rows
+    lib = N.load()
+    for n in (1, 2, 3, 4, 5, 8):
+        parts = [group_rows(height, n, k) for k in range(n)]
+        assert np.array_equal(np.sort(np.concatenate(parts)), np.arange(height))
+        for k in range(n):
+            assert lib.rtx_group_rows(height, k, n) == len(parts[k])
+            assert np.all(np.diff(parts[k]) > 0)
+    assert lib.rtx_group_rows(height, 3, 3) == -1 and lib.rtx_group_rows(height, -1, 2) == -1
 
 
 def test_glue_reassembles_strips(tmp_path):
