@@ -333,6 +333,7 @@ struct HostScene {
     int32_t n_objs = 0, n_lights = 0;
     int32_t n_plane = 0, n_sphere = 0, n_box = 0, n_mesh = 0;
     int32_t pow_bits = 0;
+    int32_t uniform_hard = -2;  // -2: no specular lobe; -1: mixed or non-integer
     float ambient[4] = {0, 0, 0, 0};
 };
 
@@ -376,6 +377,10 @@ int convert_scene(const rtx_scene_desc* desc, HostScene& H) {
                       m.hardness >= 0.0 && m.hardness <= 1e6;  // pow(base <= 1 + eps, h) stays finite
         for (int b = 0; b < 31; ++b)
             if ((d.hard_int >> b) && H.pow_bits < b + 1) H.pow_bits = b + 1;
+        if (!d.spec_zero) {  // the one integer hardness of every specular lobe, or -1
+            const int h = d.hard_is_int ? d.hard_int : -1;
+            H.uniform_hard = H.uniform_hard == -2 ? h : (H.uniform_hard == h ? h : -1);
+        }
     }
     for (int i = 0; i < desc->n_lights; ++i) {
         const rtx_light& l = desc->lights[i];
@@ -754,7 +759,7 @@ std::string jit_cache_dir() {
 
 // Returns the specialized kernel, or nullptr (the caller then launches the generic one).
 hipFunction_t jit_render_kernel(const SceneView& v, const KParams& kp, int fc_mode, bool any_speed, uint32_t ldir,
-                                bool mesh, bool sec, bool ext, bool cnt, bool jit, bool spp) {
+                                int uniform_hard, bool mesh, bool sec, bool ext, bool cnt, bool jit, bool spp) {
     if (!jit_enabled()) return nullptr;
     if (v.n_plane + v.n_sphere + v.n_box + v.n_mesh > 32 || v.n_lights > 8) return nullptr;  // code size
     // CSG/texture kernels: the unrolled loops raise their (already high) register
@@ -787,6 +792,7 @@ hipFunction_t jit_render_kernel(const SceneView& v, const KParams& kp, int fc_mo
                                      "-DRTX_FIXED_LDIR=" + std::to_string(ldir) + "u",
                                      "-DRTX_FIXED_POWBITS=" + std::to_string(v.pow_bits),
                                      "-DRTX_FIXED_DIVPOW2=" + std::to_string(kp.div_pow2)};
+    if (uniform_hard >= 0) opts.push_back("-DRTX_FIXED_HARD=" + std::to_string(uniform_hard));
     if (const char* extra = getenv("RTX_JIT_FLAGS")) {  // experiments (tools/ablate.sh); part of the cache key
         std::istringstream is(extra);
         for (std::string o; is >> o;) opts.push_back(o);
@@ -864,6 +870,7 @@ struct rtx_scene {
     int fc_mode = 0;  // RTX_FACE_CULL_MODE of the top-level meshes: 0 none, 1 all, 2 mixed
     bool any_speed = false;  // some top-level object moves (else the JIT pins a static scene)
     uint32_t light_dir_mask = 0;  // bit i: light i is directional (JIT, <= 8 lights)
+    int32_t uniform_hard = -1;    // >= 0: every specular lobe's integer hardness (JIT)
     int32_t hlevels = 0;
     // host copies for the per-time-range hierarchy bounds
     std::vector<DNode> h_nodes;
@@ -957,6 +964,7 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
             if (o.type == RTX_MESH) { ++n_m; n_fc += o.face_cull ? 1 : 0; }
         s->fc_mode = n_fc == 0 ? 0 : n_fc == n_m ? 1 : 2;
         for (const DObj& o : H.objs) s->any_speed = s->any_speed || o.has_speed;
+        s->uniform_hard = H.uniform_hard >= 0 ? H.uniform_hard : -1;
         for (size_t i = 0; i < H.lights.size() && i < 32; ++i)
             if (H.lights[i].type == LIGHT_DIRECTIONAL) s->light_dir_mask |= 1u << i;
     }
@@ -1102,8 +1110,9 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream) 
     };
     int64_t nblocks = blocks(spp_mode);
     if (nblocks > 0x7fffffff || blocks(false) > 0x7fffffff) return fail(RTX_ERR_INVALID, "rtx_render: launch too large");
-    if (hipFunction_t fn = jit_render_kernel(s->view, s->kp, s->fc_mode, s->any_speed, s->light_dir_mask, s->has_mesh,
-                                             s->has_secondary, s->has_ext, cnt, jit, spp_mode)) {
+    if (hipFunction_t fn = jit_render_kernel(s->view, s->kp, s->fc_mode, s->any_speed, s->light_dir_mask,
+                                             s->uniform_hard, s->has_mesh, s->has_secondary, s->has_ext, cnt, jit,
+                                             spp_mode)) {
         void* args[] = {(void*)&kp, (void*)&L};
         RTX_HIP(hipModuleLaunchKernel(fn, (unsigned)nblocks, 1, 1, blk, 1, 1,
                                       s->has_ext ? (unsigned)(hbytes * blk) : 0u, st, args, nullptr));

@@ -1434,8 +1434,13 @@ __host__ __device__ __attribute__((noinline)) inline double pow_general(double x
 // multiplications of `while (n) { if (n & 1) r *= b; b *= b; n >>= 1; }`.
 RTX_HD double spec_pow(double x, const DMat& m, int pow_bits) {
     if (RTX_ABLATE == 5) return (double)__builtin_powf((float)x, (float)m.hardness);  // cost probe only
+#ifdef RTX_FIXED_HARD  // scene-specialized: every specular lobe has this integer hardness
+    if (true) {
+        const int n = RTX_FIXED_HARD;
+#else
     if (m.hard_is_int) {
         const int n = m.hard_int;
+#endif
         double r = 1.0, b = x;
         for (int k = 0; k < pow_bits; ++k) {
 #if defined(__HIP_DEVICE_COMPILE__)
