@@ -89,6 +89,21 @@ def pmc_traffic(path):
         return None, None
 
 
+# VALU issue ceiling: 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction
+# (MI355X_MICROARCH.md: a SIMD issues a wave64 v_fma_f32 over 2 cycles).
+VALU_PEAK_GINST_S = 1024 * 2.4 / 2.0
+
+
+def pmc_valu(path):
+    """VALU wave-instructions per launch from the same PMC summary (SQ_INSTS_VALU)."""
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d["counters_per_dispatch"]["SQ_INSTS_VALU"]
+    except (OSError, ValueError, KeyError, TypeError):
+        return None
+
+
 def make_scene(cfg):
     import rtx
     d, base = scene_dict(cfg)
@@ -260,6 +275,14 @@ def main():
                          "model": "B_alg = 32 B x ray segments + 12 B x pixels per frame (SURVEY.md 8d) / kernel time",
                          "bytes_alg_per_frame": b_alg},
         }
+        valu = pmc_valu(os.path.join(REPO, traffic_src)) if traffic_src else None
+        if valu:
+            ach = valu / (kern_ms * 1e-3) / 1e9
+            # the kernel's second bound: VALU issue (the path computes, the HBM model
+            # above charges algorithmic ray traffic that stays in registers)
+            out["valu"] = {"insts_per_launch": int(valu), "achieved": round(ach, 1), "peak": VALU_PEAK_GINST_S,
+                           "unit": "G wave64-instructions/s", "frac": round(ach / VALU_PEAK_GINST_S, 4),
+                           "source": traffic_src}
         if rowblock:
             out["rowblock"] = rowblock
         if world == 1 and not a.no_cpu_baseline and a.cpu_seconds > 0:
