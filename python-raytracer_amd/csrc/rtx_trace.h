@@ -346,6 +346,17 @@ RTX_HD bool quot_neg(float t32, float num, float den) {
 }
 
 // Sphere quadratic (simple_geometry.py:29-39); returns false when disc < 0.
+// The same with oc = o - c and q = dot(oc, oc) given (shared by a shading point's lights).
+RTX_HD bool sphere_roots_oc(f3 d, f3 oc, float q, double r2, double& b, double& s, double& two_a) {
+    double a = (double)dot(d, d);
+    b = 2.0 * (double)dot(d, oc);
+    double cc = (double)q - r2;
+    double disc = b * b - 4.0 * a * cc;
+    if (disc < 0.0) return false;
+    s = sqrt(disc);
+    two_a = 2.0 * a;
+    return true;
+}
 RTX_HD bool sphere_roots(f3 o, f3 d, f3 c, double r2, double& b, double& s, double& two_a) {
     if (RTX_ABLATE == 4) {  // cost probe only: fp32 quadratic (not parity-correct)
         float a = dot(d, d);
@@ -357,15 +368,8 @@ RTX_HD bool sphere_roots(f3 o, f3 d, f3 c, double r2, double& b, double& s, doub
         b = bf; s = sqrtf(disc); two_a = 2.0f * a;
         return true;
     }
-    double a = (double)dot(d, d);
-    f3 oc = sub(o, c);
-    b = 2.0 * (double)dot(d, oc);
-    double cc = (double)dot(oc, oc) - r2;
-    double disc = b * b - 4.0 * a * cc;
-    if (disc < 0.0) return false;
-    s = sqrt(disc);
-    two_a = 2.0 * a;
-    return true;
+    const f3 oc = sub(o, c);
+    return sphere_roots_oc(d, oc, dot(oc, oc), r2, b, s, two_a);
 }
 
 // fp32 filter for the sign of the reference's fp64 discriminant (simple_geometry.py:29-34):
@@ -373,15 +377,18 @@ RTX_HD bool sphere_roots(f3 o, f3 d, f3 c, double r2, double& b, double& s, doub
 // With h = dot(d, o - c) (b = 2h exactly), a = dot(d, d), q = dot(o - c, o - c), the
 // quarter discriminant h^2 - a (q - r^2) is evaluated in fp32; its error is below
 // 2^-21 (h^2 + a (q + r^2) + |D|), which also covers the reference's own fp64 rounding.
-RTX_HD int sphere_disc_sign(f3 o, f3 d, f3 c, float r2f) {
-    const f3 oc = sub(o, c);
-    const float a = dot(d, d), h = dot(d, oc), q = dot(oc, oc);
+RTX_HD int sphere_disc_sign_oc(f3 d, f3 oc, float q, float r2f) {
+    const float a = dot(d, d), h = dot(d, oc);
     const float hh = h * h;
     const float D = hh - a * (q - r2f);
     const float E = 0x1p-21f * (hh + a * (q + r2f) + fabsf(D));
     if (D < -E) return -1;
     if (D > E) return 1;
     return 0;  // also NaN/inf inputs: the exact path reproduces the reference
+}
+RTX_HD int sphere_disc_sign(f3 o, f3 d, f3 c, float r2f) {
+    const f3 oc = sub(o, c);
+    return sphere_disc_sign_oc(d, oc, dot(oc, oc), r2f);
 }
 
 // AABB slabs (simple_geometry.py:196-226; bounding_volumes.py:61-91). Returns false if
@@ -1293,10 +1300,39 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
 }
 
 // ------------------------------------------------------------------ shadow any-hit
+// Origin-only terms of the plane and sphere shadow tests -- dot(p0 - o, n) per plane,
+// oc = o - c and dot(oc, oc) per sphere -- computed once per shading point and shared by
+// its lights (the same operations, once instead of per light). Scene-specialized kernels
+// only (fixed counts size the arrays); the generic kernels compute them per light.
+struct OriginTerms {
+#ifdef RTX_FIXED_COUNTS
+    float pnum[RTX_FIXED_NP > 0 ? RTX_FIXED_NP : 1];
+    f3 soc[RTX_FIXED_NS > 0 ? RTX_FIXED_NS : 1];
+    float sq[RTX_FIXED_NS > 0 ? RTX_FIXED_NS : 1];
+#endif
+};
+RTX_HD void origin_terms(const SceneView& S, f3 o, float time, OriginTerms& T) {
+#ifdef RTX_FIXED_COUNTS
+    int oi = 0;
+    for (int k = 0; k < RTX_NPLANE(S); ++k, ++oi) {
+        const DObj ob = S.objs[oi];
+        T.pnum[k] = dot(sub(moved(ob, ob.a, time), o), ld3(ob.b));
+    }
+    for (int k = 0; k < RTX_NSPHERE(S); ++k, ++oi) {
+        const DObj ob = S.objs[oi];
+        T.soc[k] = sub(o, moved(ob, ob.a, time));
+        T.sq[k] = dot(T.soc[k], T.soc[k]);
+    }
+#else
+    (void)S; (void)o; (void)time; (void)T;
+#endif
+}
+
 // Any order gives the same answer; cheap objects first, and the wave leaves as soon as
 // every active lane is occluded.
 template <bool MESH, bool X, bool COUNT>
-RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, Tally& tl, const HStack& hs) {
+RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, Tally& tl, const HStack& hs,
+                     const OriginTerms* ot = nullptr) {
     const float tmax32 = (float)t_max;
     bool occ = false;
     int oi = 0;
@@ -1304,7 +1340,11 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
         const DObj ob = S.objs[oi];
         const f3 n = ld3(ob.b);
         const float denom = dot(d, n);
+#ifdef RTX_FIXED_COUNTS
+        const float num = ot ? ot->pnum[k] : dot(sub(moved(ob, ob.a, time), o), n);
+#else
         const float num = dot(sub(moved(ob, ob.a, time), o), n);
+#endif
         const float t32 = num / denom;
         const bool hit = fabsf(denom) >= kEps4Up && quot_gt(t32, num, denom, 1e-4, kEps4Near) &&
                          quot_lt(t32, num, denom, t_max, tmax32);
@@ -1314,9 +1354,17 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
     for (int k = 0; k < RTX_NSPHERE(S); ++k, ++oi) {  // simple_geometry.py:48-72 (shadow_epsilon 1e-3)
         const DObj ob = S.objs[oi];
         const f3 ctr = moved(ob, ob.a, time);
-        if (!occ && sphere_disc_sign(o, d, ctr, (float)ob.r2) >= 0) {
+#ifdef RTX_FIXED_COUNTS
+        const f3 oc = ot ? ot->soc[k] : sub(o, ctr);
+        const float q = ot ? ot->sq[k] : dot(oc, oc);
+#else
+        const f3 oc = sub(o, ctr);
+        const float q = dot(oc, oc);
+#endif
+        if (!occ && sphere_disc_sign_oc(d, oc, q, (float)ob.r2) >= 0) {
             double b, s, two_a;
-            if (sphere_roots(o, d, ctr, ob.r2, b, s, two_a)) {
+            if (RTX_ABLATE == 4 ? sphere_roots(o, d, ctr, ob.r2, b, s, two_a)
+                                : sphere_roots_oc(d, oc, q, ob.r2, b, s, two_a)) {
                 const double t1 = (-b - s) / two_a;
                 bool hit = 1e-3 < t1 && t1 < t_max;
                 if (!hit) {
@@ -1461,6 +1509,13 @@ RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const 
                            Tally& tl, const HStack& hs) {
     f3 colour = mk(0.0f, 0.0f, 0.0f);
     tally_inc<COUNT>(tl, &Tally::shade);
+    OriginTerms ot;
+    origin_terms(S, pos, time, ot);
+#ifdef RTX_FIXED_COUNTS
+    const OriginTerms* otp = RTX_NLIGHTS(S) > 1 ? &ot : nullptr;
+#else
+    const OriginTerms* otp = nullptr;
+#endif
     for (int li = 0; li < RTX_NLIGHTS(S); ++li) {
         const DLight L = S.lights[li];
 #ifdef RTX_FIXED_LDIR  // scene-specialized: bit li set = directional
@@ -1478,7 +1533,7 @@ RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const 
             t_max = INFINITY;
         }
         tally_inc<COUNT>(tl, &Tally::shadow);
-        if (RTX_ABLATE != 1 && occluded<MESH, X, COUNT>(S, pos, sdir, t_max, time, tl, hs)) continue;
+        if (RTX_ABLATE != 1 && occluded<MESH, X, COUNT>(S, pos, sdir, t_max, time, tl, hs, otp)) continue;
         if (RTX_ABLATE == 3) { colour = add(colour, mul(ld3(L.cp), diffuse)); continue; }
         f3 light_dir = point ? normalize(sdir) : ld3(L.ndir);
         f3 lambert = scale(diffuse, pos_part(dot(normal, light_dir)));
