@@ -193,6 +193,24 @@ def test_random_scenes_match_oracle(seed):
     assert_parity(img, ref, "seed %d" % seed)
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_random_static_uniform_hardness_scenes_match_oracle(seed):
+    """Random scenes whose facts the specialized kernels pin: no speeds (static scene),
+    one integer hardness for every material (pow as a fixed multiplication chain), point
+    and directional lights, AA 1 or 4 (pinned sample counts)."""
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import random_scene
+    d = random_scene(100 + seed, res=(64, 48), mesh=(seed % 4 == 0))
+    h = [0, 1, 16, 32, 50, 3, 7, 64][seed]
+    for m in d["materials"]:
+        m["hardness"] = h
+    for o in d["objects"]:
+        o.pop("speed", None)
+    if seed % 2:
+        d["AA"] = {"jitter": False, "samples": 4}
+    assert_parity(product_scene_dict(d).render(), oracle_render_dict(d), "static seed %d" % seed)
+
+
 def test_ties_follow_scene_order():
     from common import oracle_render_dict, product_scene_dict
     from scenegen import tie_scene
