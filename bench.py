@@ -95,14 +95,12 @@ VALU_PEAK_GINST_S = 1024 * 2.4 / 2.0
 
 
 def pmc_valu(path):
-    """(VALU wave-instructions, VALU-active quad-cycles) per launch from the same PMC
-    summary (SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU; SQ cycle counters count quad-cycles)."""
+    """VALU wave-instructions per launch from the same PMC summary (SQ_INSTS_VALU)."""
     try:
         with open(path) as f:
-            c = json.load(f)["counters_per_dispatch"]
-        return c["SQ_INSTS_VALU"], c.get("SQ_ACTIVE_INST_VALU")
+            return json.load(f)["counters_per_dispatch"]["SQ_INSTS_VALU"]
     except (OSError, ValueError, KeyError, TypeError):
-        return None, None
+        return None
 
 
 def make_scene(cfg):
@@ -276,20 +274,16 @@ def main():
                          "model": "B_alg = 32 B x ray segments + 12 B x pixels per frame (SURVEY.md 8d) / kernel time",
                          "bytes_alg_per_frame": b_alg},
         }
-        valu, valu_q = pmc_valu(os.path.join(REPO, traffic_src)) if traffic_src else (None, None)
+        valu = pmc_valu(os.path.join(REPO, traffic_src)) if traffic_src else None
         if valu:
             ach = valu / (kern_ms * 1e-3) / 1e9
-            # the kernel's second bound: VALU issue (the path computes, the HBM model
+            # the kernel's second bound: VALU issue (the path computes; the HBM model
             # above charges algorithmic ray traffic that stays in registers). frac prices
-            # every instruction at the 2-cycle fp32 rate; pipe_busy_frac counts the
-            # cycles the VALUs were actually busy (fp64, transcendental and VOP3 forms
-            # take longer)
+            # every instruction at the 2-cycle fp32 rate (fp64, transcendental and VOP3
+            # forms take longer, so 1.0 is not reachable)
             out["valu"] = {"insts_per_launch": int(valu), "achieved": round(ach, 1), "peak": VALU_PEAK_GINST_S,
                            "unit": "G wave64-instructions/s", "frac": round(ach / VALU_PEAK_GINST_S, 4),
                            "source": traffic_src}
-            if valu_q:
-                simd_cycles = kern_ms * 1e-3 * 2.4e9 * 1024
-                out["valu"]["pipe_busy_frac"] = round(4.0 * valu_q / simd_cycles, 4)
         if rowblock:
             out["rowblock"] = rowblock
         if world == 1 and not a.no_cpu_baseline and a.cpu_seconds > 0:
