@@ -206,8 +206,12 @@ __host__ __device__ inline int64_t launch_items(int32_t nrows, int32_t ncols) {
 
 // Block size: 256 threads, or one wave for the hierarchy/texture (X) variants, whose
 // per-thread ray/point stacks (9 words per hierarchy level) share the CU's LDS.
+// 64 and 128 measured equal to 256 within noise (tools/ablate.sh, s21)
+#ifndef RTX_BLOCK_FLAT  // threads per block of the flat-scene kernels (experiments)
+#define RTX_BLOCK_FLAT 256
+#endif
 template <bool X>
-constexpr int kBlock = X ? 64 : 256;
+constexpr int kBlock = X ? 64 : RTX_BLOCK_FLAT;
 
 // The body of k_render, shared with the scene-specialized kernels compiled at run time
 // (rtx_jit.cpp), which pin the scene's object and light counts.
