@@ -21,7 +21,7 @@
  *   rtx_occluded       <- the Geometry.shadow_intersect plugin ABI + any-hit loop
  *                         (provided/geometry/__init__.py:50-51, provided/scene.py:160-164)
  *   rtx_fb_to_rgb8     <- main.py's rot90 + truncating uint8 conversion
- *                         (provided/main.py:325-327; rot90 is the fb's row order)
+ *                         (provided/main.py:31-33; rot90 is the fb's row order)
  *
  * Conventions
  *   - Every function returns RTX_OK (0) or a negative rtx_status; no C++ exception
@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define RTX_ABI_VERSION 3
+#define RTX_ABI_VERSION 4
 
 typedef enum rtx_status {
     RTX_OK = 0,
@@ -209,8 +209,15 @@ int rtx_intersect(rtx_scene* scene, int64_t n, const float* ray_o_dev, const flo
 int rtx_occluded(rtx_scene* scene, int64_t n, const float* ray_o_dev, const float* ray_d_dev,
                  const double* t_max_dev, double time, uint8_t* occluded_dev, void* hip_stream);
 
-/* out_dev[i] = (uint8)(fb_dev[i] * 255.0) in fp64 with truncation (main.py:327). */
+/* out_dev[i] = (uint8)(fb_dev[i] * 255.0) in fp64 with truncation (main.py:33). */
 int rtx_fb_to_rgb8(const float* fb_dev, uint8_t* out_dev, int64_t n_values, void* hip_stream);
+
+/* Observability (no reference counterpart): the name of the kernel the last
+ * rtx_render / rtx_render_groups call on this scene launched — "rtx_jit_render_<flags>"
+ * for a scene-specialized (hiprtc) kernel, "k_render_<flags>" / "k_render_ext_<flags>"
+ * for the precompiled generic ones; "" before the first render. Valid until the next
+ * render call on the scene or rtx_scene_destroy. */
+const char* rtx_last_kernel(const rtx_scene* scene);
 
 #ifdef __cplusplus
 }

@@ -8,7 +8,7 @@
 //                 wave-uniform indices (scalar loads through the constant cache).
 //   k_intersect   closest hit of SoA rays (Geometry.intersect + min, scene.py:86-94)
 //   k_occluded    shadow any-hit of SoA rays (Geometry.shadow_intersect, scene.py:160-164)
-//   k_to_rgb8     (v * 255.0) truncated to uint8 (main.py:327)
+//   k_to_rgb8     (v * 255.0) truncated to uint8 (main.py:33)
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
@@ -22,6 +22,7 @@
 #include <mutex>
 #include <sstream>
 #include <string>
+#include <sys/stat.h>
 #include <unistd.h>
 #include <vector>
 
@@ -751,15 +752,65 @@ bool jit_enabled() {
     return !(e && e[0] == '0');
 }
 
+// The on-disk code-object cache: $RTX_JIT_CACHE or /tmp/rtx_jit_<uid>, created with
+// mkdir(2) mode 0700. It is used only when it is a real directory (not a symlink) owned
+// by this user and not writable by group or others; otherwise another local user could
+// plant code objects under the predictable names, so kernels are compiled uncached.
+// Returns "" when the cache must not be used.
 std::string jit_cache_dir() {
     const char* e = getenv("RTX_JIT_CACHE");
-    if (e && *e) return e;
-    return "/tmp/rtx_jit_" + std::to_string((long)getuid());
+    const std::string dir = (e && *e) ? std::string(e) : "/tmp/rtx_jit_" + std::to_string((long)getuid());
+    (void)mkdir(dir.c_str(), 0700);
+    struct stat st;
+    if (lstat(dir.c_str(), &st) != 0 || !S_ISDIR(st.st_mode) || st.st_uid != getuid() ||
+        (st.st_mode & (S_IWGRP | S_IWOTH)) != 0)
+        return "";
+    return dir;
 }
 
-// Returns the specialized kernel, or nullptr (the caller then launches the generic one).
-hipFunction_t jit_render_kernel(const SceneView& v, const KParams& kp, int fc_mode, bool any_speed, uint32_t ldir,
-                                int uniform_hard, bool mesh, bool sec, bool ext, bool cnt, bool jit, bool spp) {
+// The library's own compile-time experiment knobs (rtx_kernels.h / rtx_trace.h defaults or
+// -D overrides of this build), forwarded to hiprtc so a specialized kernel is built with
+// the same block size, tiling and launch bounds the host launches it with; they are part
+// of the cache key through the option list.
+#define RTX_STR2(x) #x
+#define RTX_STR(x) RTX_STR2(x)
+const char* const kLibMacros[] = {
+    "-DRTX_TILE=" RTX_STR(RTX_TILE),
+    "-DRTX_PPL=" RTX_STR(RTX_PPL),
+    "-DRTX_BLOCK_FLAT=" RTX_STR(RTX_BLOCK_FLAT),
+    "-DRTX_LB_XWAVES=" RTX_STR(RTX_LB_XWAVES),
+    "-DRTX_LB_WAVES(MESH,SEC)=" RTX_STR(RTX_LB_WAVES(MESH, SEC)),
+    "-DRTX_ABLATE=" RTX_STR(RTX_ABLATE),
+    "-DRTX_HIER_INLINE=" RTX_STR(RTX_HIER_INLINE),
+#ifdef RTX_PAD
+    "-DRTX_PAD=" RTX_STR(RTX_PAD),
+#endif
+};
+#undef RTX_STR
+#undef RTX_STR2
+
+// gfx arch of a device ordinal, resolved once per device.
+std::string device_arch(int device) {
+    static std::mutex mu;
+    static std::map<int, std::string> archs;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = archs.find(device);
+    if (it != archs.end()) return it->second;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return "";
+    std::string arch = prop.gcnArchName;
+    arch = arch.substr(0, arch.find(':'));
+    archs[device] = arch;
+    return arch;
+}
+
+// Returns the specialized kernel, or nullptr (the caller then launches the generic one)
+// and its name in *name_out. Modules are loaded per device: the in-memory cache key
+// carries the device ordinal (a hipFunction_t belongs to the device it was loaded on);
+// the on-disk code object depends on the arch only.
+hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& kp, int fc_mode, bool any_speed,
+                                uint32_t ldir, int uniform_hard, bool mesh, bool sec, bool ext, bool cnt, bool jit,
+                                bool spp, std::string* name_out) {
     if (!jit_enabled()) return nullptr;
     if (v.n_plane + v.n_sphere + v.n_box + v.n_mesh > 32 || v.n_lights > 8) return nullptr;  // code size
     // CSG/texture kernels: the unrolled loops raise their (already high) register
@@ -768,12 +819,8 @@ hipFunction_t jit_render_kernel(const SceneView& v, const KParams& kp, int fc_mo
         const char* e = getenv("RTX_JIT_EXT");  // experiment: specialize them anyway
         if (!(e && e[0] == '1')) return nullptr;
     }
-    int device = 0;
-    if (hipGetDevice(&device) != hipSuccess) return nullptr;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return nullptr;
-    std::string arch = prop.gcnArchName;
-    arch = arch.substr(0, arch.find(':'));
+    const std::string arch = device_arch(device);
+    if (arch.empty()) return nullptr;
     std::vector<std::string> opts = {"--offload-arch=" + arch, "-O3", "-std=c++17", "-ffp-contract=off",
                                      "-DRTX_FIXED_COUNTS",
                                      "-DRTX_FIXED_NP=" + std::to_string(v.n_plane),
@@ -793,6 +840,7 @@ hipFunction_t jit_render_kernel(const SceneView& v, const KParams& kp, int fc_mo
                                      "-DRTX_FIXED_POWBITS=" + std::to_string(v.pow_bits),
                                      "-DRTX_FIXED_DIVPOW2=" + std::to_string(kp.div_pow2)};
     if (uniform_hard >= 0) opts.push_back("-DRTX_FIXED_HARD=" + std::to_string(uniform_hard));
+    for (const char* m : kLibMacros) opts.push_back(m);
     if (const char* extra = getenv("RTX_JIT_FLAGS")) {  // experiments (tools/ablate.sh); part of the cache key
         std::istringstream is(extra);
         for (std::string o; is >> o;) opts.push_back(o);
@@ -809,16 +857,18 @@ hipFunction_t jit_render_kernel(const SceneView& v, const KParams& kp, int fc_mo
                             ", " + b(ext) + ", " + b(cnt) + ", " + b(jit) + ">(P, L);\n}\n";
     std::string key = src;
     for (const auto& o : opts) key += "\n" + o;
+    *name_out = name;
+    const std::string dkey = key + "\n#device " + std::to_string(device);
     std::lock_guard<std::mutex> lock(g_jit_mu);
-    auto it = g_jit.find(key);
+    auto it = g_jit.find(dkey);
     if (it != g_jit.end()) return it->second.fn;
     std::string all = key;
     for (int h = 0; h < kJitNumHeaders; ++h) all += kJitHeaderSrcs[h];
     char hash[32];
     snprintf(hash, sizeof(hash), "%016zx", std::hash<std::string>{}(all));
-    const std::string dir = jit_cache_dir(), path = dir + "/rtx_" + hash + ".co";
+    const std::string dir = jit_cache_dir(), path = dir.empty() ? "" : dir + "/rtx_" + hash + ".co";
     std::string code;
-    {
+    if (!path.empty()) {
         std::ifstream f(path, std::ios::binary);
         if (f) { std::stringstream ss; ss << f.rdbuf(); code = ss.str(); }
     }
@@ -845,18 +895,24 @@ hipFunction_t jit_render_kernel(const SceneView& v, const KParams& kp, int fc_mo
         code.resize(n);
         hiprtcGetCode(prog, &code[0]);
         hiprtcDestroyProgram(&prog);
-        (void)system(("mkdir -p '" + dir + "' 2>/dev/null").c_str());
-        const std::string tmp = path + "." + std::to_string((long)getpid());
-        std::ofstream f(tmp, std::ios::binary);
-        if (f.write(code.data(), (std::streamsize)code.size())) {
-            f.close();
-            (void)rename(tmp.c_str(), path.c_str());
+        if (!path.empty()) {
+            const std::string tmp = path + "." + std::to_string((long)getpid());
+            std::ofstream f(tmp, std::ios::binary);
+            if (f.write(code.data(), (std::streamsize)code.size())) {
+                f.close();
+                (void)rename(tmp.c_str(), path.c_str());
+            }
         }
     }
     JitEntry e;
-    if (hipModuleLoadData(&e.mod, code.data()) != hipSuccess) return nullptr;
-    if (hipModuleGetFunction(&e.fn, e.mod, name.c_str()) != hipSuccess) return nullptr;
-    g_jit[key] = e;
+    hipError_t he = hipModuleLoadData(&e.mod, code.data());
+    if (he == hipSuccess) he = hipModuleGetFunction(&e.fn, e.mod, name.c_str());
+    if (he != hipSuccess) {
+        fprintf(stderr, "librtx: scene-specialized kernel %s failed to load (%s), using the generic one\n",
+                name.c_str(), hipGetErrorString(he));
+        return nullptr;
+    }
+    g_jit[dkey] = e;
     return e.fn;
 }
 
@@ -900,6 +956,15 @@ struct rtx_scene {
     float* d_times = nullptr;
     float* d_noise = nullptr;
     KParams* d_kp = nullptr;
+    // the kernel resolved for each (counters, jitter, sample-parallel) variant of the
+    // current camera: looked up (and compiled) once per camera, not per frame; nullptr
+    // after a lookup means the generic kernel
+    struct Resolved {
+        bool done = false;
+        hipFunction_t fn = nullptr;
+        std::string name;
+    } resolved[8];
+    std::string last_kernel;  // name of the kernel the last render call launched
 };
 
 namespace {
@@ -920,6 +985,7 @@ void free_camera(rtx_scene* s) {
     s->d_xs = s->d_ys = s->d_dof = s->d_aa = s->d_times = s->d_noise = nullptr;
     s->d_kp = nullptr;
     s->cam_set = false;
+    for (auto& r : s->resolved) r = rtx_scene::Resolved{};  // specialized on the camera's sample counts
 }
 
 void free_scene(rtx_scene* s) {
@@ -937,6 +1003,8 @@ extern "C" {
 int rtx_abi_version(void) { return RTX_ABI_VERSION; }
 
 const char* rtx_last_error(void) { return g_last_error.c_str(); }
+
+const char* rtx_last_kernel(const rtx_scene* s) { return s ? s->last_kernel.c_str() : ""; }
 
 int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
     if (!out) return fail(RTX_ERR_INVALID, "rtx_scene_create: null argument");
@@ -1092,6 +1160,10 @@ int rtx_render_groups(rtx_scene* s, int32_t phase, int32_t stride, float* fb_dev
 namespace {
 int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream) {
     const int32_t nrows = L.nrows;
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || cur != s->device)
+        return fail(RTX_ERR_STATE, "rtx_render: the scene lives on device " + std::to_string(s->device) +
+                                       ", the current device is " + std::to_string(cur));
     L.counters = reinterpret_cast<unsigned long long*>(counters_dev);
     hipStream_t st = (hipStream_t)stream;
     const bool cnt = counters_dev != nullptr;
@@ -1110,14 +1182,25 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream) 
     };
     int64_t nblocks = blocks(spp_mode);
     if (nblocks > 0x7fffffff || blocks(false) > 0x7fffffff) return fail(RTX_ERR_INVALID, "rtx_render: launch too large");
-    if (hipFunction_t fn = jit_render_kernel(s->view, s->kp, s->fc_mode, s->any_speed, s->light_dir_mask,
-                                             s->uniform_hard, s->has_mesh, s->has_secondary, s->has_ext, cnt, jit,
-                                             spp_mode)) {
+    rtx_scene::Resolved& rs = s->resolved[(cnt ? 4 : 0) | (jit ? 2 : 0) | (spp_mode ? 1 : 0)];
+    if (!rs.done) {
+        rs.fn = jit_render_kernel(s->device, s->view, s->kp, s->fc_mode, s->any_speed, s->light_dir_mask,
+                                  s->uniform_hard, s->has_mesh, s->has_secondary, s->has_ext, cnt, jit, spp_mode,
+                                  &rs.name);
+        rs.done = true;
+    }
+    if (rs.fn && jit_enabled()) {
         void* args[] = {(void*)&kp, (void*)&L};
-        RTX_HIP(hipModuleLaunchKernel(fn, (unsigned)nblocks, 1, 1, blk, 1, 1,
+        RTX_HIP(hipModuleLaunchKernel(rs.fn, (unsigned)nblocks, 1, 1, blk, 1, 1,
                                       s->has_ext ? (unsigned)(hbytes * blk) : 0u, st, args, nullptr));
+        s->last_kernel = rs.name;
         return RTX_OK;
     }
+    char gname[48];
+    snprintf(gname, sizeof(gname), "%s_%d%d%d%d%d%s", s->has_ext ? "k_render_ext" : "k_render", s->has_mesh ? 1 : 0,
+             s->has_secondary ? 1 : 0, s->has_ext ? 1 : 0, cnt ? 1 : 0, jit ? 1 : 0,
+             (spp_mode && s->has_ext) ? "_spp" : "");
+    s->last_kernel = gname;
     if (s->has_ext) {  // precompiled in rtx_kern_ext_m{0,1}.hip
         const RenderLaunch rl{kp, (unsigned)nblocks, hbytes * kBlock<true>, st, spp_mode};
         RTX_HIP(s->has_mesh ? launch_render_ext_m1(sel, rl, L) : launch_render_ext_m0(sel, rl, L));

@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_lib", "librtx.so")
 # Experiment builds (tools/ablate.sh) point this at another build of the same HIP source.
 LIB_PATH = os.environ.get("RTX_LIB_OVERRIDE", LIB_PATH)
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 RTX_OK, RTX_ERR_INVALID, RTX_ERR_HIP, RTX_ERR_UNSUPPORTED, RTX_ERR_STATE = 0, -1, -2, -3, -4
 RTX_SPHERE, RTX_PLANE, RTX_BOX, RTX_MESH, RTX_NODE = 0, 1, 2, 3, 4
@@ -86,7 +86,8 @@ _lock = threading.Lock()
 _lib = None
 
 EXPORTS = ["rtx_abi_version", "rtx_last_error", "rtx_scene_create", "rtx_scene_destroy", "rtx_camera_set",
-           "rtx_render", "rtx_render_groups", "rtx_group_rows", "rtx_intersect", "rtx_occluded", "rtx_fb_to_rgb8"]
+           "rtx_render", "rtx_render_groups", "rtx_group_rows", "rtx_intersect", "rtx_occluded", "rtx_fb_to_rgb8",
+           "rtx_last_kernel"]
 
 
 def load():
@@ -112,8 +113,10 @@ def load():
         lib.rtx_intersect.argtypes = [vp, C.c_int64, vp, vp, C.c_double, vp, vp, vp, vp, vp, vp]
         lib.rtx_occluded.argtypes = [vp, C.c_int64, vp, vp, vp, C.c_double, vp, vp]
         lib.rtx_fb_to_rgb8.argtypes = [vp, vp, C.c_int64, vp]
-        for fn in EXPORTS[2:]:
+        for fn in EXPORTS[2:-1]:
             getattr(lib, fn).restype = C.c_int
+        lib.rtx_last_kernel.argtypes = [vp]
+        lib.rtx_last_kernel.restype = C.c_char_p
         v = lib.rtx_abi_version()
         if v != ABI_VERSION:
             raise RuntimeError("librtx.so ABI %d != binding ABI %d" % (v, ABI_VERSION))

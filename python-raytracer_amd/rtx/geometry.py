@@ -114,13 +114,9 @@ class Mesh(Geometry):
         aabb_volume = (max_x - min_x) * (max_y - min_y) * (max_z - min_z)
         sphere_volume = 4 / 3 * math.pi * max_dist ** 3
         if aabb_volume < sphere_volume:
-            self.bv_type = "aabb"
-            self.bv_min = F.vec3(min_x, min_y, min_z)
-            self.bv_max = F.vec3(max_x, max_y, max_z)
+            self.bounding_volume = BoundingAABB(F.vec3(min_x, min_y, min_z), F.vec3(max_x, max_y, max_z), None)
         else:
-            self.bv_type = "sphere"
-            self.bv_center = center
-            self.bv_radius = max_dist
+            self.bounding_volume = BoundingSphere(center, max_dist, None)
 
     def _compute_normals(self):
         """mesh.py:53-70: normals[face[k]] += normalize(e1 x e2) * area, in face order."""
@@ -135,15 +131,25 @@ class Mesh(Geometry):
         np.add.at(acc, f.ravel(), np.repeat(weighted, 3, axis=0))  # sequential, in face order
         self.norms = F.normalize(acc)
 
-    def triangles(self):
-        """(v0, v1, v2, n0, n1, n2) per face, fp32 [nfaces, 6, 3]."""
-        f = self.faces
-        v = self.verts
-        if self.flat_shaded or len(self.norms) != len(v):
-            n = np.zeros_like(v)
-        else:
-            n = self.norms
-        return np.stack([v[f[:, 0]], v[f[:, 1]], v[f[:, 2]], n[f[:, 0]], n[f[:, 1]], n[f[:, 2]]], axis=1)
+    def __repr__(self):
+        return "Mesh(%s)" % self.name
+
+
+class BoundingSphere:
+    """bounding_volumes.py:12-16 (the cull itself runs on the device: mesh_bv)."""
+
+    def __init__(self, center, radius, geometry):
+        self.center = F.vec3(center)
+        self.radius = radius
+        self.geometry = geometry
+
+
+class BoundingAABB:
+    """bounding_volumes.py:43-47."""
+
+    def __init__(self, minpos, maxpos, geometry):
+        self.minpos = F.vec3(minpos)
+        self.maxpos = F.vec3(maxpos)
 
 
 def resolve_path(path, base_dir):
@@ -199,8 +205,3 @@ def open_texture(path, base_dir=None):
     if im.mode not in ("RGB", "RGBA", "RGBX", "CMYK", "RGBa", "YCbCr", "LAB", "HSV"):
         raise TypeError("texture %s: getpixel of mode %s is not indexable as RGB" % (path, im.mode))
     return im
-
-
-def texture_rgb8(im):
-    """getpixel((i, j))[:3] for every texel: uint8 [height, width, 3]."""
-    return np.ascontiguousarray(np.asarray(im)[:, :, :3], dtype=np.uint8)

@@ -1,4 +1,4 @@
-"""Host I/O: bundled scenes and PNG output (main.py:325-328, glue.py:23-25)."""
+"""Host I/O: bundled scenes and PNG output (main.py:30-35, glue.py:17-27)."""
 import copy
 import json
 import os
@@ -34,7 +34,7 @@ def load_bundled_scene(name, verbose=False, **kw):
 
 
 def to_png_array(image):
-    """main.py:325-327: rot90(k=1, axes=(0, 1)), then (image * 255).astype(uint8)."""
+    """main.py:31-33: rot90(k=1, axes=(0, 1)), then (image * 255).astype(uint8)."""
     return (np.rot90(image, k=1, axes=(0, 1)) * 255).astype(np.uint8)
 
 

@@ -9,17 +9,15 @@ only prepares the reference's scalar tables (pixel x/y running sums, sunflower o
 motion times) and moves buffers.
 """
 import ctypes as C
+import hashlib
 
 import numpy as np
 import torch
 
 from . import _native as N
 from . import f32 as F
-from . import geometry as geom
+from . import records
 from .helperclasses import sunflower
-
-_MAT_CODE = {"diffuse": N.RTX_MAT_DIFFUSE, "mirror": N.RTX_MAT_MIRROR, "refractive": N.RTX_MAT_REFRACTIVE}
-_HIER_CODE = {"union": N.RTX_UNION, "intersection": N.RTX_INTERSECTION, "difference": N.RTX_DIFFERENCE}
 
 DEFAULT_SEED = 0x5EED
 
@@ -52,6 +50,21 @@ def group_rows(height, n, k):
     g = np.arange(k, (height + 7) // 8, n)
     rows = (g[:, None] * 8 + np.arange(8)[None, :]).ravel()
     return rows[rows < height]
+
+
+def fb_to_rgb8(fb, out=None, stream=None):
+    """rtx_fb_to_rgb8 on the device: (fb * 255.0) truncated to uint8 (main.py:33), into
+    ``out`` (a contiguous uint8 CUDA tensor of fb's shape) or a new tensor."""
+    if not (fb.is_cuda and fb.dtype == torch.float32 and fb.is_contiguous()):
+        raise ValueError("fb must be a contiguous float32 CUDA tensor")
+    if out is None:
+        out = torch.empty(fb.shape, dtype=torch.uint8, device=fb.device)
+    if out.shape != fb.shape or out.dtype != torch.uint8 or not out.is_cuda or not out.is_contiguous():
+        raise ValueError("out must be a contiguous uint8 CUDA tensor of shape %s" % (tuple(fb.shape),))
+    st = stream if stream is not None else torch.cuda.current_stream()
+    N.call("rtx_fb_to_rgb8", C.c_void_p(fb.data_ptr()), C.c_void_p(out.data_ptr()), int(fb.numel()),
+           C.c_void_p(st.cuda_stream))
+    return out
 
 
 class _NativeScene:
@@ -89,116 +102,35 @@ class Scene:
         self._native = None
         self._cam_key = None
 
+    @classmethod
+    def from_reference(cls, ref):
+        """Bind a scene built by the reference's own scene_parser.load_scene
+        (provided/scene.py:18-33): the same vc / jitter / samples / ambient / lights /
+        materials / objects, read through the reference's attribute names (rtx.records)."""
+        return cls(ref.vc, ref.jitter, ref.samples, ref.ambient, ref.lights, ref.materials, ref.objects)
+
+    def invalidate(self):
+        """Drop the uploaded scene and camera: the next render re-reads every object,
+        material, light and camera attribute (the reference reads them on every call)."""
+        if self._native is not None:
+            self._native.close()
+        self._native = None
+        self._cam_key = None
+
+    @property
+    def last_kernel(self):
+        """Name of the kernel the last render launched (rtx_last_kernel): a
+        scene-specialized "rtx_jit_render_*" or a generic "k_render*"."""
+        if self._native is None or not self._native.h:
+            return ""
+        return N.load().rtx_last_kernel(self._native.h).decode()
+
     # ------------------------------------------------------------------ scene upload
     def scene_desc(self):
-        """Flatten the objects into the rtx_scene_desc ABI arrays (scene order kept)."""
-        mats = list(self.materials)
-        index = {id(m): i for i, m in enumerate(mats)}
-
-        def value(m):
-            return (m.ID, m.name, m.mat_type, tuple(F.vec3(m.diffuse)), tuple(F.vec3(m.specular)), float(m.hardness),
-                    float(m.tint), float(m.refr_index))
-        by_value = {}
-        for i, m in enumerate(mats):
-            by_value.setdefault(value(m), i)
-
-        def mat_index(m):
-            # a `ref` node's deep copy carries copies of the scene materials: same values,
-            # same slot
-            if id(m) not in index:
-                v = value(m)
-                if v not in by_value:
-                    by_value[v] = len(mats)
-                    mats.append(m)
-                index[id(m)] = by_value[v]
-            return index[id(m)]
-
-        # Records in preorder: top-level objects in scene order, each hierarchy followed by
-        # its subtree (rtx.h: parent indices, children in child order).
-        records = []
-
-        def walk(g, parent):
-            records.append((g, parent))
-            if isinstance(g, geom.Hierarchy):
-                me = len(records) - 1
-                for c in g.children:
-                    walk(c, me)
-        for g in self.objects:
-            walk(g, -1)
-        objs = (N.rtx_object * max(1, len(records)))()
-        tris = []
-        textures, tex_index = [], {}
-
-        def texture_index(im):
-            if id(im) not in tex_index:
-                tex_index[id(im)] = len(textures)
-                textures.append(geom.texture_rgb8(im))
-            return tex_index[id(im)]
-        for i, (g, parent) in enumerate(records):
-            o = objs[i]
-            o.parent = parent
-            o.texture = -1
-            o.texture_scale = 1.0
-            o.n_mats = len(g.materials)
-            for k, m in enumerate(g.materials[:2]):
-                o.mat[k] = mat_index(m)
-            o.has_speed = 0 if g.speed is None else 1
-            o.speed = N.f3(g.speed if g.speed is not None else (0, 0, 0))
-            if isinstance(g, geom.Hierarchy):
-                o.type = N.RTX_NODE
-                o.hierarchy_type = _HIER_CODE.get(g.hierarchy_type, N.RTX_HIER_OTHER)
-                o.trs[:] = [float(x) for x in np.concatenate([g.t, g.r, g.s]).astype(np.float32)]
-            elif isinstance(g, geom.Sphere):
-                o.type, o.a, o.radius = N.RTX_SPHERE, N.f3(g.center), float(g.radius)
-            elif isinstance(g, geom.Plane):
-                o.type, o.a, o.b = N.RTX_PLANE, N.f3(g.point), N.f3(g.normal)
-                if g.texture is not None:
-                    o.texture, o.texture_scale = texture_index(g.texture), float(g.texture_scale)
-            elif isinstance(g, geom.AABB):
-                o.type, o.a, o.b = N.RTX_BOX, N.f3(g.minpos), N.f3(g.maxpos)
-                if g.texture is not None:
-                    o.texture = texture_index(g.texture)
-            elif isinstance(g, geom.Mesh):
-                o.type = N.RTX_MESH
-                o.tri_begin = sum(len(t) for t in tris)
-                t = g.triangles()
-                o.tri_count = len(t)
-                tris.append(t)
-                o.flat = 1 if g.flat_shaded else 0
-                if g.bv_type == "aabb":
-                    o.bv_type, o.bv_a, o.bv_b = N.RTX_BV_AABB, N.f3(g.bv_min), N.f3(g.bv_max)
-                else:
-                    o.bv_type, o.bv_a, o.bv_radius = N.RTX_BV_SPHERE, N.f3(g.bv_center), float(g.bv_radius)
-            else:
-                raise NotImplementedError("unsupported geometry %r" % (g,))
-            if not isinstance(g, geom.Hierarchy) and not g.materials:
-                raise IndexError("%r has no material: the reference raises IndexError (list index out of "
-                                 "range) when it is hit" % (g,))
-        cm = (N.rtx_material * max(1, len(mats)))()
-        for i, m in enumerate(mats):
-            cm[i].diffuse, cm[i].specular = N.f3(m.diffuse), N.f3(m.specular)
-            cm[i].hardness = float(m.hardness)
-            cm[i].type = _MAT_CODE.get(m.mat_type, N.RTX_MAT_DIFFUSE)  # other strings shade as diffuse
-            cm[i].tint, cm[i].refr_index = float(m.tint), float(m.refr_index)
-        cl = (N.rtx_light * max(1, len(self.lights)))()
-        for i, L in enumerate(self.lights):
-            cl[i].type = N.RTX_LIGHT_POINT if L.type == "point" else N.RTX_LIGHT_DIRECTIONAL
-            cl[i].colour, cl[i].vector, cl[i].power = N.f3(L.colour), N.f3(L.vector), float(L.power)
-        tri = np.ascontiguousarray(np.concatenate(tris).astype(np.float32)) if tris else np.zeros((1, 6, 3), np.float32)
-        desc = N.rtx_scene_desc()
-        desc.n_objects, desc.objects = len(records), objs
-        desc.n_materials, desc.materials = len(mats), cm
-        desc.n_lights, desc.lights = len(self.lights), cl
-        desc.n_triangles = sum(len(t) for t in tris)
-        desc.triangles = tri.ctypes.data_as(C.POINTER(N.rtx_triangle))
-        desc.ambient = N.f3(self.ambient)
-        ct = (N.rtx_texture * max(1, len(textures)))()
-        for i, t in enumerate(textures):
-            ct[i].height, ct[i].width = t.shape[0], t.shape[1]
-            ct[i].rgb = t.ctypes.data_as(C.POINTER(C.c_uint8))
-        desc.n_textures, desc.textures = len(textures), ct
-        desc._keep = (objs, cm, cl, tri, ct, textures)
-        return desc
+        """Flatten the objects into the rtx_scene_desc ABI arrays (scene order kept;
+        rtx.records reads the reference's attribute names, so the objects may be the
+        reference's own)."""
+        return records.scene_desc(self.objects, self.materials, self.lights, self.ambient)
 
     def native(self):
         if self._native is None or self._native.device != torch.cuda.current_device():
@@ -256,8 +188,21 @@ class Scene:
             d.jitter = N.RTX_JITTER_PHILOX
         return d, t
 
+    def _camera_key(self, subimage, tasks):
+        """Every value camera_tables / camera_desc read, so a moved camera, new lens,
+        motion or sample settings, or a new noise stream re-uploads the tables."""
+        vc = self.vc
+        vecs = b"".join(np.asarray(v, np.float32).tobytes() for v in (vc.position, vc.u, vc.v, vc.w))
+        noise = None
+        if self.jitter and self.jitter_noise is not None:
+            a = np.ascontiguousarray(np.asarray(self.jitter_noise, np.float64))
+            noise = (a.size, hashlib.blake2b(a.tobytes(), digest_size=16).digest())
+        return (subimage, tasks, vc.width, vc.height, vc.left, vc.right, vc.top, vc.bottom, vecs, vc.d,
+                vc.focal_length, vc.aperture, vc.dof_samples, tuple(vc.motion_times), self.samples, self.jitter,
+                self.seed, noise)
+
     def _set_camera(self, subimage, tasks):
-        key = (subimage, tasks, self.jitter, self.seed, id(self.jitter_noise))
+        key = self._camera_key(subimage, tasks)
         nat = self.native()
         if self._cam_key == key:
             return self._cam_info
@@ -307,12 +252,8 @@ class Scene:
         return np.ascontiguousarray(np.transpose(img[::-1], (1, 0, 2))).astype(np.float64)
 
     def render_rgb8(self, subimage=0, tasks=1):
-        """main.py:325-327 on the device: (rot90(image) * 255).astype(uint8), (H, W, 3)."""
-        fb = self.render_device(subimage, tasks)
-        out = torch.empty(fb.shape, dtype=torch.uint8, device=fb.device)
-        N.call("rtx_fb_to_rgb8", C.c_void_p(fb.data_ptr()), C.c_void_p(out.data_ptr()), int(fb.numel()),
-               C.c_void_p(torch.cuda.current_stream().cuda_stream))
-        return out.cpu().numpy()
+        """main.py:31-33 on the device: (rot90(image) * 255).astype(uint8), (H, W, 3)."""
+        return fb_to_rgb8(self.render_device(subimage, tasks)).cpu().numpy()
 
     # ------------------------------------------------------------------ Geometry ABI (batched)
     def intersect(self, origins, directions, time=0.0):

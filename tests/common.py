@@ -41,17 +41,23 @@ def compare(img, ref):
                 png_frac_diff=float((png > 0).mean()), png_max=int(png.max()))
 
 
-# Parity bar (north_star: "within a stated fp32 tolerance of the reference"):
-# the fp32 framebuffer is expected bit-identical; we allow at most 0.1% of pixels to
-# differ (fp64 pow/sqrt last-ulp effects flipping an fp32 rounding or a silhouette)
-# and a mean absolute difference of at most 1e-4 per pixel.
-MAX_FRAC_DIFF = 1e-3
-MAX_MEAN_ABS = 1e-4
+# Parity bar (north_star: "within a stated fp32 tolerance of the reference"): the fp32
+# framebuffer must be bit-identical to the oracle's — every deterministic case asserts
+# frac_diff == 0. The one documented source of allowed mismatch is `x ** hardness`:
+# the device evaluates integer exponents by fp64 binary exponentiation (rtx_trace.h
+# spec_pow), whose fp32 cast can differ from libm pow's within a few fp64 ulps of an fp32
+# rounding boundary. Only tests whose scenes draw arbitrary hardness values pass
+# pow_ulps=True, which allows 0.1 % of pixels to differ with a mean |d| <= 1e-4.
+POW_MAX_FRAC_DIFF = 1e-3
+POW_MAX_MEAN_ABS = 1e-4
 
 
-def assert_parity(img, ref, what=""):
+def assert_parity(img, ref, what="", pow_ulps=False):
     s = compare(img, ref)
-    assert s["frac_diff"] <= MAX_FRAC_DIFF and s["mean_abs"] <= MAX_MEAN_ABS, "%s parity: %s" % (what, s)
+    if pow_ulps:
+        assert s["frac_diff"] <= POW_MAX_FRAC_DIFF and s["mean_abs"] <= POW_MAX_MEAN_ABS, "%s parity: %s" % (what, s)
+    else:
+        assert s["frac_diff"] == 0.0, "%s parity (exact): %s" % (what, s)
     return s
 
 

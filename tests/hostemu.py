@@ -33,6 +33,7 @@ def lib():
         _lib = C.CDLL(build())
         vp = C.c_void_p
         _lib.rtx_hostemu_render.argtypes = [vp, vp, C.c_int32, C.c_int32, vp, vp, C.c_int]
+        _lib.rtx_hostemu_render_rows.argtypes = [vp, vp, vp, C.c_int32, vp, C.c_int]
         _lib.rtx_hostemu_intersect.argtypes = [vp, C.c_int64, vp, vp, C.c_double, vp, vp, vp, vp, vp]
         _lib.rtx_hostemu_occluded.argtypes = [vp, C.c_int64, vp, vp, vp, C.c_double, vp]
         _lib.rtx_hostemu_last_error.restype = C.c_char_p
@@ -54,6 +55,18 @@ def render(scene, subimage=0, tasks=1, threads=8):
     _chk(lib().rtx_hostemu_render(C.addressof(sd), C.addressof(cd), 0, H, fb.ctypes.data, cnt.ctypes.data, threads))
     img = np.ascontiguousarray(np.transpose(fb[::-1], (1, 0, 2))).astype(np.float64)
     return img, cnt
+
+
+def render_rows(scene, rows, threads=8):
+    """Image rows ``rows`` (row 0 = top) only, packed: float32 [len(rows), W, 3], the
+    block one rank renders (rtx_render / rtx_render_groups layout)."""
+    sd = scene.scene_desc()
+    cd, tables = scene.camera_desc()
+    rows = np.ascontiguousarray(np.asarray(rows, np.int32))
+    fb = np.zeros((len(rows), cd.ncols, 3), np.float32)
+    _chk(lib().rtx_hostemu_render_rows(C.addressof(sd), C.addressof(cd), rows.ctypes.data, len(rows), fb.ctypes.data,
+                                       threads))
+    return fb
 
 
 def intersect(scene, o, d, time=0.0):

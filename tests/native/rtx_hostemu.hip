@@ -104,6 +104,43 @@ extern "C" int rtx_hostemu_render(const rtx_scene_desc* sd, const rtx_camera_des
     return RTX_OK;
 }
 
+// The packed image rows rows[0..nrows) (row 0 = top), as one rank renders its share of a
+// frame (rtx_render's contiguous block or rtx_render_groups' interleaved 8-row groups).
+extern "C" int rtx_hostemu_render_rows(const rtx_scene_desc* sd, const rtx_camera_desc* cd, const int32_t* rows,
+                                       int32_t nrows, float* fb, int threads) {
+    HostScene H;
+    int rc = convert_scene(sd, H);
+    if (rc) return rc;
+    KParams k;
+    if ((rc = convert_camera(cd, k))) return rc;
+    for (int32_t r = 0; r < nrows; ++r)
+        if (rows[r] < 0 || rows[r] >= cd->height) return fail(RTX_ERR_INVALID, "bad rows");
+    bind_view(H, k.S);
+    std::vector<float> times(cd->n_times);
+    for (int i = 0; i < cd->n_times; ++i) times[i] = (float)cd->times[i];
+    const auto mm = std::minmax_element(times.begin(), times.end());
+    const std::vector<DBound> bounds = compute_bounds(H.nodes, H.objs, H.tris, *mm.first, *mm.second);
+    k.S.bounds = (cptr<DBound>)bounds.data();
+    std::vector<float> noise;
+    const size_t nsamp = (size_t)cd->n_dof * cd->n_aa;
+    if (cd->jitter == RTX_JITTER_REPLAY) noise.assign(cd->noise, cd->noise + 3 * (size_t)cd->ncols * cd->height * nsamp);
+    k.xs = (cptr<float>)cd->xs; k.ys = (cptr<float>)cd->ys; k.dof_o = (cptr<float>)cd->dof_origins;
+    k.aa_o = (cptr<float>)cd->aa_origins; k.times = (cptr<float>)times.data(); k.noise = (cptr<float>)noise.data();
+    const int64_t npix = (int64_t)nrows * k.ncols;
+#pragma omp parallel for num_threads(threads > 0 ? threads : 1) schedule(dynamic, 64)
+    for (int64_t p = 0; p < npix; ++p) {
+        Tally tl = {};
+        float frames[kMaxDepth * 4];
+        float hst[kMaxHLevels * 9];
+        const FrameStack fs{frames, 1};
+        const HStack hs{hst, 1};
+        const int32_t rr = (int32_t)(p / k.ncols), cc = (int32_t)(p % k.ncols);
+        // render_pixel's image row is row0 + rr
+        pixel_any(H, k, fb, rows[rr] - rr, rr, cc, tl, fs, hs, k.jitter != RTX_JITTER_OFF);
+    }
+    return RTX_OK;
+}
+
 extern "C" int rtx_hostemu_intersect(const rtx_scene_desc* sd, int64_t n, const float* ro, const float* rd, double time,
                                      double* t_out, int32_t* obj_out, int32_t* mat_out, float* n_out, float* p_out) {
     HostScene H;

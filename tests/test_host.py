@@ -149,9 +149,10 @@ def test_descriptor_is_preorder_with_parents():
 def test_texture_rgb8_matches_getpixel():
     from PIL import Image
     from rtx import geometry as geom
+    from rtx.records import texture_rgb8
     for name in ("wall1.png", "brick.jpg", "axes.png"):
         im = geom.open_texture(os.path.join(REPO, "assets", "textures", name))
-        a = geom.texture_rgb8(im)
+        a = texture_rgb8(im)
         for (i, j) in ((0, 0), (5, 17), (im.width - 1, im.height - 1), (100, 3)):
             assert tuple(a[j, i]) == tuple(im.getpixel((i, j))[:3])
 
@@ -191,7 +192,8 @@ def test_torus_mesh_preprocessing():
     sc = rtx.load_bundled_scene("TorusMesh", resolution=(8, 8))
     m = sc.objects[1]
     assert m.verts.shape == (64, 3) and m.faces.shape == (128, 3)
-    assert m.bv_type == "aabb"  # box volume < bounding sphere volume
+    # box volume < bounding sphere volume (mesh.py:48-49)
+    assert type(m.bounding_volume).__name__ == "BoundingAABB"
 
 
 def test_f32_helpers_follow_glm_order():

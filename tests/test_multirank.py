@@ -31,15 +31,13 @@ def _worker(rank, world, port, name, res, out_q):
     from rtx.distributed import render_frame
     sc = product_scene(name, res)
 
+    # each rank renders only its own rows (host build of the device code standing in
+    # for this rank's GPU), in the layout rtx_render / rtx_render_groups write
     def rows(row0, nrows):
-        img, _ = hostemu.render(sc, threads=2)   # full frame on the host, then this rank's block
-        fb = np.ascontiguousarray(np.transpose(img, (1, 0, 2))[::-1]).astype(np.float32)
-        return torch.from_numpy(fb[row0:row0 + nrows].copy())
+        return torch.from_numpy(hostemu.render_rows(sc, np.arange(row0, row0 + nrows), threads=2))
 
     def group(rws):  # interleaved 8-row groups: the given image rows
-        img, _ = hostemu.render(sc, threads=2)
-        fb = np.ascontiguousarray(np.transpose(img, (1, 0, 2))[::-1]).astype(np.float32)
-        return torch.from_numpy(fb[rws].copy())
+        return torch.from_numpy(hostemu.render_rows(sc, rws, threads=2))
 
     for dtype in (torch.float32, torch.uint8):
         frame = render_frame(sc, rank, world, render_rows=rows, dtype=dtype)
