@@ -1,13 +1,15 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X render path (BASELINE.json metric: Mrays/sec + frame ms,
-TwoSpheresPlane 1920x1080).
+TwoSpheresPlane 1920x1080 @1/2/4/8 GPUs).
 
-One step = one 1920x1080 1-spp frame of TwoSpheresPlane rendered by each rank (the
-primary sample is the reference's unit: its tqdm bar counts W*H*aa*dof*|times|,
-provided/scene.py:45,71). With N ranks the job renders N frames per step, one per GPU
-(frame-parallel weak scaling; no data-path collective). ``--rowblock`` additionally times
-the north-star strong-scaling form: one frame split across ranks (interleaved 8-row groups,
-which balance sky and ground rows) and gathered to rank 0 over RCCL.
+The unit is the reference's: primary samples W*H*aa*dof*|times| per second (its tqdm bar,
+provided/scene.py:45,71). One step = one 1920x1080 1-spp frame of TwoSpheresPlane.
+N = 1: the frame is rendered into the fp32 framebuffer on one GPU.
+N > 1 (north star, "scaling": "strong"): the SAME frame is split across the ranks —
+each renders its interleaved 8-row groups (rtx_render_groups), converts them to uint8
+on its GPU and rank 0 gathers them with one RCCL collective (rtx.distributed.FramePipeline,
+double-buffered so a frame's gather overlaps the next frame's render); the frame-parallel
+rate (each rank its own frame) is reported beside it as "weak_scaling".
 
 Launch: python bench.py [--steps K --warmup W]          (N = 1)
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -69,10 +71,12 @@ def parse():
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--config", default="tsp1080", choices=sorted(CONFIGS))
-    p.add_argument("--rowblock", action="store_true", help="also time row-block + RCCL gather of one frame")
-    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
+    p.add_argument("--cpu-seconds", type=float, default=10.0,
+                   help="budget of the C-restatement CPU line (0 = skip both CPU lines)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--force-dist", action="store_true", help="initialise torch.distributed even for one rank (tests)")
+    p.add_argument("--pipeline", action="store_true",
+                   help="run the multi-GPU frame pipeline (render groups + RCCL gather) even at N = 1 (rehearsal)")
     p.add_argument("--pmc-json", default=None,
                    help="tools/pmc_summary.py output for this config (default profiles/pmc_<config>.json)")
     return p.parse_args()
@@ -125,7 +129,7 @@ def cpu_threads():
     return max(1, min(16, avail))
 
 
-def cpu_baseline(cfg, budget_s, threads=None):
+def cpu_baseline_native(cfg, budget_s, threads=None):
     """The oracle (C restatement of the reference) on the same workload, as the reference
     parallelises it: column strips (scene.py:35-37 `np.array_split`, render.nu's tasks),
     one strip per host thread (ctypes releases the GIL; every oracle_render call builds
@@ -165,9 +169,106 @@ def cpu_baseline(cfg, budget_s, threads=None):
         sample = "full %dx%d frame(s)" % (W, H)
     else:
         sample = "columns 0..%d of %dx%d (1/%d of the frame)" % (ncol - 1, W, H, frac)
-    return {"value": nsamp / dt / 1e6, "unit": "Mrays/s", "cores": P, "kind": "port",
+    return {"value": nsamp / dt / 1e6, "unit": "Mrays/s", "cores": P, "kind": "port (C restatement)",
             "sample": "%s x %d repeats in %.1f s; %d column strips (np.array_split, as render.nu) on %d host "
                       "threads (oracle/rtx_oracle.c, gcc -O2)" % (sample, frames, dt, P, P)}
+
+
+# Python-loop baseline: rows j = 0, R, 2R, ... (reference row index) of the full-width
+# frame; every row for the 1080p configs whose whole frame fits the budget.
+PY_ROW_STRIDE = {"tsp1080": 1, "mr1080": 1, "tm1080": 16, "dof4k": 270}
+_PY = {}
+
+
+def _py_init(cfg):
+    from oracle import oracle as O
+    from oracle import pyloop as PL
+    d, base = scene_dict(cfg)
+    osc = O.OracleScene(d, base)
+    _PY["scene"] = PL.PyLoopScene(osc)
+    _PY["spp"] = osc.n_samples
+    _PY["jitter"] = osc.jitter
+
+
+def _py_strip(args):
+    """One np.array_split column strip (render.nu's --subimage k --tasks N process)."""
+    k, tasks, rows = args
+    sc = _PY["scene"]
+    ncol = len(np.array_split(np.arange(sc.width), tasks)[k])
+    noise = np.random.RandomState(k).rand(ncol * len(rows) * sc.samples * sc.dof_samples * 3) if _PY["jitter"] else None
+    t0 = time.perf_counter()
+    sc.render(k, tasks, rows=rows, noise=noise)
+    return ncol * len(rows) * _PY["spp"], time.perf_counter() - t0
+
+
+def cpu_baseline(cfg, processes=None):
+    """The reference's Python render loop (oracle/pyloop.py: per pixel, sample, ray and
+    object Python calls, PyGLM's fp32 on numpy scalars; bit-identical to the C oracle,
+    tests/test_pyloop.py) on the host, parallelised as the reference does it: P processes,
+    one np.array_split column strip each (provided/scene.py:36-37, render.nu). Runs before
+    the GPU is initialised (forked workers)."""
+    import multiprocessing as mp
+    if cfg not in PY_ROW_STRIDE:
+        return None
+    _, res, _, _ = CONFIGS[cfg]
+    W, H = res
+    P = processes or cpu_threads()
+    stride = PY_ROW_STRIDE[cfg]
+    rows = list(range(0, H, stride))
+    with mp.get_context("fork").Pool(P, initializer=_py_init, initargs=(cfg,)) as pool:
+        pool.map(_py_init, [cfg] * P)  # every worker built its scene before the clock starts
+        t0 = time.perf_counter()
+        res_ = pool.map(_py_strip, [(k, P, rows) for k in range(P)], chunksize=1)
+        dt = time.perf_counter() - t0
+    nsamp = sum(r[0] for r in res_)
+    cpu = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu = next(line.split(":", 1)[1].strip() for line in f if line.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+    sample = "full %dx%d frame" % (W, H) if stride == 1 else \
+        "rows 0, %d, 2x%d, ... (%d of %d) of the %dx%d frame" % (stride, stride, len(rows), H, W, H)
+    return {"value": nsamp / dt / 1e6, "unit": "Mrays/s", "cores": P, "kind": "port",
+            "sample": "%s, %d samples in %.1f s; %d processes, one np.array_split column strip each (as render.nu); "
+                      "oracle/pyloop.py: the reference's per-sample Python loop, bit-identical to the C oracle; "
+                      "host CPU %s" % (sample, nsamp, dt, P, cpu)}
+
+
+def kernel_ms(fn, n, stream):
+    """Average duration of fn() over n calls from HIP events on the launch stream (events
+    bracket the whole run: per-call events would insert gaps between launches)."""
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(n):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n
+
+
+def max_over_ranks(x, use_dist):
+    t = torch.tensor([float(x)], dtype=torch.float64, device="cuda")
+    if use_dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def timed(fn, steps, use_dist):
+    """Wall time of `steps` calls of fn, bracketed by barrier + synchronize on both sides;
+    the max over ranks is the job's time. Each rank's clock stops when its own work is done;
+    the closing barrier keeps every rank inside the bracket."""
+    if use_dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if use_dist:
+        dist.barrier()
+    return max_over_ranks(t1 - t0, use_dist)
 
 
 def main():
@@ -178,11 +279,19 @@ def main():
     if world != a.gpus:
         if world == 1 and a.gpus > 1:
             sys.exit("--gpus %d needs torch.distributed.run with %d processes" % (a.gpus, a.gpus))
+    cpu = {}
+    if world == 1 and not a.no_cpu_baseline and a.cpu_seconds > 0:
+        # host baselines first, before this process touches the GPU (the Python loop forks)
+        cpu["cpu_baseline"] = cpu_baseline(a.config)
+        cpu["cpu_baseline_native"] = cpu_baseline_native(a.config, a.cpu_seconds)
+        if cpu["cpu_baseline"] is None:  # hierarchy/texture/large-mesh configs: C restatement only
+            cpu["cpu_baseline"] = cpu.pop("cpu_baseline_native")
     torch.cuda.set_device(local)
-    use_dist = world > 1 or a.force_dist
+    use_dist = world > 1 or a.force_dist or a.pipeline
     if use_dist:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import rtx  # noqa: F401
+    from rtx.distributed import FramePipeline
     from rtx.scene import group_rows
 
     sc = make_scene(a.config)
@@ -200,94 +309,113 @@ def main():
     segments = cast_rays + shadow_rays
     b_alg = 32 * segments + 12 * W * H  # 32 B per segment + 12 B/pixel fp32 RGB
 
-    for _ in range(a.warmup):
-        sc.render_device(out=fb)
-    torch.cuda.synchronize()
-
-    # HIP events on the launch stream bracket the whole timed region (events between
-    # launches would insert ~10 us gaps on ROCm); kernel time = elapsed / steps.
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if use_dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    e0.record(stream)
-    for _ in range(a.steps):
+    def full_frame():
         sc.render_device(out=fb, stream=stream)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    # each rank's clock stops when its own K frames are done; the closing barrier keeps
-    # every rank inside the bracket and the max over ranks below is the job's time
-    t1 = time.perf_counter()
-    if use_dist:
-        dist.barrier()
-    wall = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
-    kern = torch.tensor([e0.elapsed_time(e1) / a.steps], dtype=torch.float64, device="cuda")
-    if use_dist:
-        dist.all_reduce(wall, op=dist.ReduceOp.MAX)
-        dist.all_reduce(kern, op=dist.ReduceOp.MAX)
-    wall_s = float(wall.item())
-    kern_ms = float(kern.item())
-    ms_per_step = wall_s * 1e3 / a.steps
-    samples_per_step = world * W * H * spp
-    value = samples_per_step * a.steps / wall_s / 1e6
 
-    rowblock = None
-    if a.rowblock and use_dist:
-        from rtx.distributed import render_frame
+    extra = {}
+    if world == 1 and not a.pipeline:
+        # N = 1: one step = one whole frame into the fp32 framebuffer
+        for _ in range(a.warmup):
+            full_frame()
+        torch.cuda.synchronize()
+        wall_s = timed(full_frame, a.steps, use_dist)
+        kern_ms = kernel_ms(full_frame, a.steps, stream)  # the render kernel alone, same launches
+        kernel = sc.last_kernel
+        rows_frac = 1.0
+        scaling, parallelism = "strong", "single GPU"
+    else:
+        # N > 1 (north star): one step = ONE frame sharded across the ranks — interleaved
+        # 8-row groups per rank (rtx_render_groups), uint8 on the GPU (rtx_fb_to_rgb8), one
+        # RCCL gather to rank 0; frame k's gather overlaps frame k + 1's render.
+        pipe = FramePipeline(sc, rank, world)
+        for _ in range(a.warmup):
+            pipe.step()
+        pipe.flush()
+        torch.cuda.synchronize()
+        if use_dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            pipe.step()
+        pipe.flush()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if use_dist:
+            dist.barrier()
+        wall_s = max_over_ranks(t1 - t0, use_dist)
+        # breakdown (outside the timed region): this rank's render + uint8 conversion, and
+        # the gather + reorder alone, each from HIP events on the launch stream
+        kern_ms = max_over_ranks(kernel_ms(lambda: pipe.render_block(pipe.fb), a.steps, stream), use_dist)
+        kernel = sc.last_kernel
+        render_ms = max_over_ranks(kernel_ms(pipe.render, a.steps, stream), use_dist)
+        slot = pipe.slots[0]
+        if use_dist:
+            dist.barrier()
+        gather_ms = max_over_ranks(kernel_ms(slot, a.steps, stream), use_dist)
+        rows_frac = len(group_rows(H, world, rank)) / H
+        nrows = [len(group_rows(H, world, r)) for r in range(world)]
+        extra["multi_gpu"] = {
+            "frame_ms": round(wall_s * 1e3 / a.steps, 5),
+            "render_ms_per_rank": round(kern_ms, 5), "render_rgb8_ms_per_rank": round(render_ms, 5),
+            "gather_ms": round(gather_ms, 5),
+            "rows_per_rank": [min(nrows), max(nrows)],
+            "partition": "interleaved 8-row groups r, r+N, ... (rtx_render_groups)",
+            "collective": "one torch.distributed.gather of uint8 rows to rank 0 (RCCL), double-buffered",
+        }
+        # secondary: weak scaling (each rank renders its own whole frame per step)
         for _ in range(3):
-            render_frame(sc, rank, world, dtype=torch.uint8, interleave=True)
-        torch.cuda.synchronize()
-        dist.barrier()
-        r0 = time.perf_counter()
-        nrb = max(5, a.steps // 2)
-        for _ in range(nrb):
-            render_frame(sc, rank, world, dtype=torch.uint8, interleave=True)
-        torch.cuda.synchronize()
-        dist.barrier()
-        rb = torch.tensor([time.perf_counter() - r0], dtype=torch.float64, device="cuda")
-        dist.all_reduce(rb, op=dist.ReduceOp.MAX)
-        rb_ms = float(rb.item()) * 1e3 / nrb
-        rowblock = {"ms_per_frame": rb_ms, "Mrays_s": W * H * spp / rb_ms / 1e3, "scaling": "strong",
-                    "gather": "uint8 interleaved 8-row groups (rtx_render_groups) to rank 0 "
-                              "(torch.distributed.gather, RCCL)",
-                    "rows_per_rank": max(len(group_rows(H, world, r)) for r in range(world))}
+            full_frame()
+        weak_s = timed(full_frame, a.steps, use_dist)
+        extra["weak_scaling"] = {"Mrays_s": round(world * W * H * spp * a.steps / weak_s / 1e6, 3),
+                                 "ms_per_step": round(weak_s * 1e3 / a.steps, 5),
+                                 "note": "frame-parallel: each rank renders its own whole frame, no collective"}
+        scaling, parallelism = "strong", "row-groups x %d ranks + RCCL gather" % world
+    ms_per_step = wall_s * 1e3 / a.steps
+    value = W * H * spp * a.steps / wall_s / 1e6
 
     if rank == 0:
-        achieved = b_alg / (kern_ms * 1e-3) / 1e9
+        bytes_kernel = b_alg * rows_frac  # the dominant kernel's share of the frame
+        achieved = bytes_kernel / (kern_ms * 1e-3) / 1e9
         traffic, traffic_src = pmc_traffic(a.pmc_json or os.path.join(REPO, "profiles", "pmc_%s.json" % a.config))
         if traffic is not None:
-            traffic = int(round(traffic))
+            traffic = int(round(traffic * rows_frac))
             traffic_src = os.path.relpath(traffic_src, REPO)
+        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "traffic_unit": "HBM bytes/launch (rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE)",
+                "traffic_source": traffic_src,
+                "model": "achieved = B_alg / kernel time, B_alg = 32 B x ray segments + 12 B x pixels "
+                         "(SURVEY.md 8d): algorithmic ray traffic, which this megakernel keeps in registers",
+                "bytes_alg_per_launch": int(bytes_kernel)}
+        if traffic is not None:
+            meas = traffic / (kern_ms * 1e-3) / 1e9
+            roof["achieved_measured"] = round(meas, 2)
+            roof["frac_measured"] = round(meas / HBM_PEAK_GBS, 5)
+        valu = pmc_valu(os.path.join(REPO, traffic_src)) if traffic_src else None
         out = {
-            "metric": METRIC if a.config == "tsp1080" else METRIC_OTHER % CONFIGS[a.config][3], "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(ms_per_step, 5), "higher_is_better": True, "scaling": "weak",
+            "metric": METRIC if a.config == "tsp1080" else METRIC_OTHER % CONFIGS[a.config][3],
+            "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms_per_step, 5), "higher_is_better": True, "scaling": scaling,
             "vs_baseline": None, "dtype": "fp32 vectors + fp64 scalars (reference numerics)", "data": "synthetic",
             "config": {"workload": CONFIGS[a.config][3], "width": W, "height": H, "spp": spp,
-                       "frames_per_step": world,
-                       "parallelism": "frame-parallel (one frame per rank per step)" if world > 1 else "single GPU"},
-            "frame_ms": round(kern_ms, 5),
+                       "frames_per_step": 1, "parallelism": parallelism},
+            "frame_ms": round(kern_ms, 5), "kernel": kernel,
             "segments_per_frame": segments, "cast_rays_per_frame": cast_rays, "shadow_rays_per_frame": shadow_rays,
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "traffic_unit": "bytes/launch (rocprofv3 PMC)", "traffic_source": traffic_src,
-                         "model": "B_alg = 32 B x ray segments + 12 B x pixels per frame (SURVEY.md 8d) / kernel time",
-                         "bytes_alg_per_frame": b_alg},
+            "roofline": roof,
         }
-        valu = pmc_valu(os.path.join(REPO, traffic_src)) if traffic_src else None
         if valu:
-            ach = valu / (kern_ms * 1e-3) / 1e9
-            # the kernel's second bound: VALU issue (the path computes; the HBM model
-            # above charges algorithmic ray traffic that stays in registers). frac prices
-            # every instruction at the 2-cycle fp32 rate (fp64, transcendental and VOP3
-            # forms take longer, so 1.0 is not reachable)
-            out["valu"] = {"insts_per_launch": int(valu), "achieved": round(ach, 1), "peak": VALU_PEAK_GINST_S,
+            v = valu * rows_frac
+            ach = v / (kern_ms * 1e-3) / 1e9
+            # the limiter actually identified: VALU issue + per-wave latency. frac prices
+            # every instruction at the 2-cycle wave64 fp32 rate (fp64, transcendental and
+            # VOP3 forms take longer, so 1.0 is not reachable)
+            out["valu"] = {"insts_per_launch": int(v), "achieved": round(ach, 1), "peak": VALU_PEAK_GINST_S,
                            "unit": "G wave64-instructions/s", "frac": round(ach / VALU_PEAK_GINST_S, 4),
-                           "source": traffic_src}
-        if rowblock:
-            out["rowblock"] = rowblock
-        if world == 1 and not a.no_cpu_baseline and a.cpu_seconds > 0:
-            out["cpu_baseline"] = cpu_baseline(a.config, a.cpu_seconds)
+                           "issue_floor_us": round(v / VALU_PEAK_GINST_S / 1e3, 3), "source": traffic_src}
+            roof["limiter"] = "VALU issue + per-wave latency (see valu); measured HBM traffic is frac_measured"
+        out.update(extra)
+        out.update(cpu)
         print(json.dumps(out), flush=True)
     if use_dist:
         dist.destroy_process_group()

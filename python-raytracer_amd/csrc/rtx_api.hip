@@ -840,7 +840,9 @@ hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& k
                                      "-DRTX_FIXED_POWBITS=" + std::to_string(v.pow_bits),
                                      "-DRTX_FIXED_DIVPOW2=" + std::to_string(kp.div_pow2)};
     if (uniform_hard >= 0) opts.push_back("-DRTX_FIXED_HARD=" + std::to_string(uniform_hard));
-    for (const char* m : kLibMacros) opts.push_back(m);
+    const char* lm = getenv("RTX_JIT_LIBMACROS");  // experiment: 0 = do not forward them
+    if (!(lm && lm[0] == '0'))
+        for (const char* m : kLibMacros) opts.push_back(m);
     if (const char* extra = getenv("RTX_JIT_FLAGS")) {  // experiments (tools/ablate.sh); part of the cache key
         std::istringstream is(extra);
         for (std::string o; is >> o;) opts.push_back(o);
@@ -871,6 +873,11 @@ hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& k
     if (!path.empty()) {
         std::ifstream f(path, std::ios::binary);
         if (f) { std::stringstream ss; ss << f.rdbuf(); code = ss.str(); }
+    }
+    if (const char* dump = getenv("RTX_JIT_DUMP"); dump && dump[0] == '1') {  // tools/jit_resource.sh
+        fprintf(stderr, "librtx: jit %s:", name.c_str());
+        for (const auto& o : opts) fprintf(stderr, " '%s'", o.c_str());
+        fprintf(stderr, "\n%s", src.c_str());
     }
     if (code.empty()) {
         hiprtcProgram prog;

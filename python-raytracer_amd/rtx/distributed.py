@@ -112,3 +112,65 @@ def render_frame(scene, rank, world, render_rows=None, dtype=torch.float32, dst=
     if dtype == torch.uint8 and block.dtype != torch.uint8:
         block = to_rgb8(block)
     return gather_rows(block, H, world, rank, dst=dst, group=group, interleave=interleave)
+
+
+class FramePipeline:
+    """The multi-GPU frame loop of bench.py (north star: one frame sharded across the node,
+    one gather at the end): every step renders this rank's interleaved 8-row groups of
+    the next frame, converts them to uint8 on the GPU and starts their gather to ``dst``
+    asynchronously; the previous frame's gather is then awaited (a stream wait, not a host
+    wait, on RCCL) and its rows put in place. Two buffer slots, so frame k's gather runs
+    while frame k + 1 renders. ``render_block(out)`` / ``convert(fb, out)`` default to
+    rtx_render_groups and rtx_fb_to_rgb8; the CPU tests inject the host emulation."""
+
+    def __init__(self, scene, rank, world, dst=0, group=None, device=None, render_block=None, convert=None):
+        H, W = scene.vc.height, scene.vc.width
+        device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.rank, self.dst, self.group = rank, dst, group
+        self.slots = [FrameGather(H, W, 3, world, rank, torch.uint8, device, interleave=True, dst=dst, group=group)
+                      for _ in range(2)]
+        self.fb = torch.empty((self.slots[0].nrows, W, 3), dtype=torch.float32, device=device)
+        self.render_block = render_block or (lambda out: scene.render_device(groups=(rank, world), out=out))
+        self.convert = convert or self._to_rgb8
+        self.k = 0
+        self.prev = None  # (work, slot) of the last submitted frame
+
+    @staticmethod
+    def _to_rgb8(fb, out):
+        if fb.is_cuda:
+            from .scene import fb_to_rgb8
+            fb_to_rgb8(fb, out=out)
+        else:
+            out.copy_(to_rgb8(fb))
+
+    def _finish(self, work, slot):
+        work.wait()
+        if self.rank != self.dst:
+            return None
+        flat = slot.recv.view((slot.world * slot.maxrows,) + tuple(slot.recv.shape[2:]))
+        return torch.index_select(flat, 0, slot.index)
+
+    def render(self):
+        """Render and convert this rank's rows of the next frame into the free slot."""
+        slot = self.slots[self.k % 2]
+        if slot.nrows:
+            self.render_block(self.fb)
+            self.convert(self.fb, slot.block)
+        return slot
+
+    def step(self):
+        """Submit the next frame; returns the previous frame on ``dst`` (None elsewhere and
+        on the first step)."""
+        slot = self.render()
+        if self.rank == self.dst:
+            work = dist.gather(slot.send, gather_list=slot.recv_list, dst=self.dst, group=self.group, async_op=True)
+        else:
+            work = dist.gather(slot.send, dst=self.dst, group=self.group, async_op=True)
+        prev, self.prev = self.prev, (work, slot)
+        self.k += 1
+        return self._finish(*prev) if prev is not None else None
+
+    def flush(self):
+        """Wait for the last submitted frame; returns it on ``dst``."""
+        prev, self.prev = self.prev, None
+        return self._finish(*prev) if prev is not None else None

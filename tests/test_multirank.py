@@ -50,6 +50,58 @@ def _worker(rank, world, port, name, res, out_q):
     dist.destroy_process_group()
 
 
+def _pipeline_worker(rank, world, port, name, res, nframes, out_q):
+    """bench.py's multi-GPU frame loop (rtx.distributed.FramePipeline: render this rank's
+    interleaved groups, uint8, async gather, previous frame finished while the next one
+    renders) with the host emulation as each rank's renderer."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), "python-raytracer_amd"), here):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import hostemu
+    from common import product_scene
+    from rtx.distributed import FramePipeline
+    from rtx.scene import group_rows
+    sc = product_scene(name, res)
+    rows = group_rows(res[1], world, rank)
+
+    def render_block(out):
+        out.copy_(torch.from_numpy(hostemu.render_rows(sc, rows, threads=2)))
+    pipe = FramePipeline(sc, rank, world, device=torch.device("cpu"), render_block=render_block)
+    frames = [pipe.step() for _ in range(nframes)] + [pipe.flush()]
+    if rank == 0:
+        assert frames[0] is None and all(f is not None for f in frames[1:])
+        out_q.put([f.numpy() for f in frames[1:]])
+    else:
+        assert all(f is None for f in frames)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,res", [(2, (40, 23)), (3, (33, 26))])
+def test_frame_pipeline_gathers_every_frame(world, res):
+    from common import oracle_render
+    from oracle import oracle as O
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipeline_worker, args=(r, world, port, "MirrorRefraction", res, 3, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    frames = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = O.to_png_array(oracle_render("MirrorRefraction", res))
+    assert len(frames) == 3
+    for f in frames:
+        assert np.array_equal(f, want)
+
+
 @pytest.mark.parametrize("world,res", [(2, (40, 23)), (3, (17, 10))])
 def test_gather_row_blocks(world, res):
     from common import oracle_render
