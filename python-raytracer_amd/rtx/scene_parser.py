@@ -1,24 +1,60 @@
-"""JSON scene loader with the reference's schema, defaults and error behaviour
-(mirror of provided/scene_parser.py:21-294).
+"""JSON scene loading with the reference's schema, defaults, messages and error behaviour
+(provided/scene_parser.py:50-294), returning an ``rtx.scene.Scene`` that renders on the GPU.
 
-``load_scene(infile)`` returns an ``rtx.scene.Scene`` whose ``render()`` runs on the GPU.
-Defaults (scene_parser.py:62-142): resolution [1080, 720], ambient [0,0,0], AA
-{jitter: False, samples: 1}, DOF {focal_length: 1, aperture: 0, samples: 1}, motion
-{time: 0, samples: 1, final: 0}, material {type: diffuse, diffuse/specular: [0,0,0],
-hardness: 32, tint: 0.0, refr_index: 1.0}; directional lights get power 1.0; a KeyError
-inside the light list drops every light; unknown light/object types are skipped with a
-message. Hierarchy nodes (scene_parser.py:177-205, :261-285) become ``geometry.Hierarchy``
-trees, `ref` nodes deep-copy an earlier root, and every top-level hierarchy passes its
-materials to its leaves (hierarchy.py:21-28). Textures are opened with PIL like the
-reference. ``load_scene`` also accepts an already-parsed dict (used by the bench and tests).
+The reference parses with one function per JSON level; here the schema is data — the
+optional camera sections, material keys and light kinds are tables — and every geometry
+entry, at any depth, goes through one recursive builder (``_SceneBuilder.add``). What is
+kept from the reference, because renders depend on it (tests/test_host.py,
+tests/test_reference_binding.py compare against the reference's own parser):
+
+* a section (AA, DOF, motion) with any key missing falls back as a whole (:67-96);
+* a KeyError anywhere in the light list drops every light (:104-125); directional
+  lights get power 1.0 whatever the JSON says (:116-118);
+* material lists are ``associate_material``'s: for each listed ID, every scene material
+  with that ID, in scene order (:288-294);
+* a child's speed is its top-level hierarchy's speed plus its own, and nested nodes
+  hand the TOP-LEVEL speed (not their own) to their children (:268-271, :283); a child
+  of type "node" never resolves ``ref``;
+* a top-level ``ref`` node deep-copies the first earlier root of that name and takes
+  its own name, materials and transform (:190-205);
+* every top-level hierarchy appends its materials to its leaves afterwards (:153-155);
+* unknown light / object types are skipped with the reference's message.
+
+``load_scene`` also accepts an already-parsed dict (the bench and tests use this); asset
+paths that do not exist relative to the CWD are looked up next to the scene file.
 """
 import copy
 import json
 import os
 
+from . import f32 as F
 from . import geometry as geom
 from . import helperclasses as hc
 from .scene import Scene
+
+# Optional camera sections: (JSON key, fields, fallbacks, message). A missing section or
+# field takes every fallback of the section (scene_parser.py:67-96).
+_SECTIONS = (
+    ("AA", ("jitter", "samples"), (False, 1), "No Anti-Aliasing options found, setting to default"),
+    ("DOF", ("focal_length", "aperture", "samples"), (1, 0, 1), "No Depth of Field options found, setting to default"),
+    ("motion", ("time", "samples", "final"), (0, 1, 0), "No motion blur options found, setting to default"),
+)
+
+# Optional material keys in Material's argument order after (name, ID) (scene_parser.py:133-138).
+_MATERIAL_KEYS = (("specular", [0, 0, 0]), ("diffuse", [0, 0, 0]), ("hardness", 32), ("type", "diffuse"),
+                  ("tint", 0.0))
+
+# Light kinds: JSON key of the light's vector and how its power is read (scene_parser.py:112-118).
+_LIGHT_KINDS = {"point": ("position", lambda spec: spec["power"]),
+                "directional": ("direction", lambda spec: 1.0)}
+
+
+def _vec(a):
+    """A JSON 3- or 4-list as a list, anything else of another length as None (the
+    reference's populateVec, scene_parser.py:21-27)."""
+    if a is None:
+        return None
+    return list(a) if len(a) in (3, 4) else None
 
 
 class _Log:
@@ -30,39 +66,146 @@ class _Log:
             print(*a)
 
 
-def populateVec(array):
-    """scene_parser.py:21-27 (vec4 inputs are kept as 4-lists; only hierarchies use them)."""
-    if array is None:
-        return None
-    if len(array) == 3:
-        return [array[0], array[1], array[2]]
-    if len(array) == 4:
-        return [array[0], array[1], array[2], array[3]]
-    return None
+class _SceneBuilder:
+    def __init__(self, data, base_dir, log):
+        self.data, self.base_dir, self.log = data, base_dir, log
+        self.materials = []
+        self.roots = {}  # top-level hierarchies that `ref` nodes may copy, first definition wins
 
-
-def get_or(obj, keys, default, msg="", log=print):
-    """scene_parser.py:30-47."""
-    if not isinstance(keys, list) or len(keys) == 0:
+    # ------------------------------------------------------------ camera, lights, materials
+    def optional(self, key, default, message):
         try:
-            return obj[keys]
+            return self.data[key]
         except KeyError:
-            if msg != "":
-                log(msg)
+            self.log(message)
             return default
-    result = []
-    try:
-        for key in keys:
-            result.append(obj[key])
-        return result
-    except KeyError:
-        if msg != "":
-            log(msg)
-        return default
+
+    def section(self, key, fields, fallbacks, message):
+        try:
+            return tuple(self.data[key][f] for f in fields)
+        except KeyError:
+            self.log(message)
+            return fallbacks
+
+    def camera(self):
+        cam = self.data["camera"]
+        pos, lookat, up, fov = _vec(cam["position"]), _vec(cam["lookAt"]), _vec(cam["up"]), cam["fov"]
+        width, height = self.optional("resolution", [1080, 720], "No resolution found, defaulting to 1080x720.")
+        self.ambient = _vec(self.optional("ambient", [0, 0, 0], "No ambient light defined, defaulting to [0, 0, 0]"))
+        (self.jitter, self.samples), lens, motion = (self.section(*s) for s in _SECTIONS)
+        return hc.ViewportCamera().set_viewport(width, height).set_camera(pos, lookat, up, fov) \
+            .set_lens(*lens).set_motion(*motion)
+
+    def lights(self):
+        out = []
+        try:
+            for spec in self.data["lights"]:
+                kind, name, colour = spec["type"], spec["name"], _vec(spec["colour"])
+                if kind not in _LIGHT_KINDS:
+                    self.log("Unkown light type", kind, ", skipping initialization")
+                    continue
+                key, power = _LIGHT_KINDS[kind]
+                out.append(hc.Light(kind, name, colour, _vec(spec[key]), power(spec)))
+        except KeyError as e:
+            self.log("Error loading lights: ", e)
+            out = []
+        return out
+
+    def read_materials(self):
+        for spec in self.data["materials"]:
+            name, ident = spec["name"], spec["ID"]
+            specular, diffuse, hardness, kind, tint = (spec.get(k, d) for k, d in _MATERIAL_KEYS)
+            m = hc.Material(name, _vec(specular), _vec(diffuse), hardness, ident, kind, tint)
+            m.refr_index = spec.get("refr_index", 1.0)
+            self.materials.append(m)
+        return self.materials
+
+    def materials_of(self, spec):
+        return [m for i in spec.get("materials", []) for m in self.materials if m.ID == i]
+
+    # ------------------------------------------------------------ geometry
+    def asset(self, path):
+        return geom.resolve_path(path, self.base_dir)
+
+    def shape(self, kind, name, pos, mats, speed, spec):
+        """The non-hierarchy geometry classes (scene_parser.py:212-258); None if ``kind``
+        is not one of them."""
+        if kind == "sphere":
+            return geom.Sphere(name, kind, mats, pos, spec["radius"], speed)
+        if kind == "plane":
+            g = geom.Plane(name, kind, mats, pos, _vec(spec["normal"]), speed)
+            if "texture" in spec:
+                g.texture = geom.open_texture(spec["texture"], self.base_dir)
+                g.texture_scale = spec.get("texture_scale", 1.0)
+            return g
+        if kind == "box":
+            if "size" in spec:
+                g = geom.AABB(name, kind, mats, pos, _vec(spec["size"]), speed)
+            else:  # declared by its corners
+                g = geom.AABB(name, kind, mats, pos, [0, 0, 0], speed)
+                g.minpos, g.maxpos = F.vec3(_vec(spec["min"])), F.vec3(_vec(spec["max"]))
+            if "texture" in spec:
+                g.texture = geom.open_texture(spec["texture"], self.base_dir)
+            return g
+        if kind == "mesh":
+            path = self.asset(spec["filepath"])
+            return geom.Mesh(name, kind, mats, pos, spec["scale"], path, spec.get("flat_shaded", False), speed)
+        return None
+
+    def add(self, spec, into, top_speed=None, nested=False):
+        """Build one geometry entry into ``into``: a top-level object (nested=False) or a
+        child of a hierarchy whose top-level speed is ``top_speed``."""
+        name, kind = spec["name"], spec["type"]
+        pos = _vec(spec.get("position", [0, 0, 0]))
+        mats = self.materials_of(spec)
+        if not nested:
+            speed = _vec(spec.get("speed"))
+        elif top_speed is None:
+            speed = None
+        else:
+            speed = F.vec3(top_speed) + F.vec3(_vec(spec.get("speed", [0, 0, 0])))
+        g = self.shape(kind, name, pos, mats, speed, spec)
+        if g is not None:
+            into.append(g)
+            return
+        if kind != "node":
+            if nested:  # the reference re-reads the entry as a top-level one, then skips it
+                _vec(spec.get("speed"))
+            self.log("Unkown object type", kind, ", skipping initialization")
+            return
+        ref = "" if nested else spec.get("ref", "")
+        rot, scale = _vec(spec.get("rotation", [0, 0, 0])), _vec(spec.get("scale", [1, 1, 1]))
+        htype = spec.get("hierarchy_type", "union")
+        if ref != "":
+            if ref not in self.roots:
+                self.log("Node reference", ref, "not found, skipping creation")
+                return
+            node = copy.deepcopy(self.roots[ref])
+            node.name, node.materials = name, mats
+            node.make_matrices(pos, rot, scale)
+            into.append(node)
+            return
+        node = geom.Hierarchy(name, kind, mats, htype, pos, rot, scale, speed)
+        # children see the TOP-LEVEL speed, however deep (scene_parser.py:283)
+        child_speed = top_speed if nested else speed
+        for child in spec["children"]:
+            self.add(child, node.children, child_speed, nested=True)
+        if not nested:
+            self.roots.setdefault(name, node)
+        into.append(node)
+
+    def objects(self):
+        out = []
+        for spec in self.data["objects"]:
+            self.add(spec, out)
+        for g in out:  # hierarchy.py:21-28, for top-level hierarchies only
+            if isinstance(g, geom.Hierarchy):
+                g.set_fallback_material(g.materials)
+        return out
 
 
 def load_scene(infile, verbose=True):
-    """scene_parser.py:50-163."""
+    """scene_parser.load_scene: a scene JSON file (or its parsed dict) -> Scene."""
     log = _Log(verbose)
     base_dir = None
     if isinstance(infile, dict):
@@ -72,187 +215,13 @@ def load_scene(infile, verbose=True):
         with open(infile) as f:
             data = json.load(f)
         base_dir = os.path.dirname(os.path.abspath(infile))
-    base_dir = data.get("__base_dir__", base_dir)
-
-    cam_pos = populateVec(data["camera"]["position"])
-    cam_lookat = populateVec(data["camera"]["lookAt"])
-    cam_up = populateVec(data["camera"]["up"])
-    cam_fov = data["camera"]["fov"]
-
-    width, height = get_or(data, "resolution", [1080, 720], "No resolution found, defaulting to 1080x720.", log)
-    ambient = populateVec(get_or(data, "ambient", [0, 0, 0],
-                                 "No ambient light defined, defaulting to [0, 0, 0]", log))
-    try:
-        jitter = data["AA"]["jitter"]
-        samples = data["AA"]["samples"]
-    except KeyError:
-        log("No Anti-Aliasing options found, setting to default")
-        jitter, samples = False, 1
-    try:
-        focal_length = data["DOF"]["focal_length"]
-        aperture = data["DOF"]["aperture"]
-        dof_samples = data["DOF"]["samples"]
-    except KeyError:
-        log("No Depth of Field options found, setting to default")
-        focal_length, aperture, dof_samples = 1, 0, 1
-    try:
-        motion_time = data["motion"]["time"]
-        motion_samples = data["motion"]["samples"]
-        motion_final = data["motion"]["final"]
-    except KeyError:
-        log("No motion blur options found, setting to default")
-        motion_time, motion_samples, motion_final = 0, 1, 0
-
-    vc = hc.ViewportCamera() \
-        .set_viewport(width, height) \
-        .set_camera(cam_pos, cam_lookat, cam_up, cam_fov) \
-        .set_lens(focal_length, aperture, dof_samples) \
-        .set_motion(motion_time, motion_samples, motion_final)
-
-    lights = []
-    try:
-        for light in data["lights"]:
-            l_type = light["type"]
-            l_name = light["name"]
-            l_colour = populateVec(light["colour"])
-            if l_type == "point":
-                l_vector = populateVec(light["position"])
-                l_power = light["power"]
-            elif l_type == "directional":
-                l_vector = populateVec(light["direction"])
-                l_power = 1.0
-            else:
-                log("Unkown light type", l_type, ", skipping initialization")
-                continue
-            lights.append(hc.Light(l_type, l_name, l_colour, l_vector, l_power))
-    except KeyError as e:
-        log("Error loading lights: ", e)
-        lights = []
-
-    materials = []
-    for material in data["materials"]:
-        mat_name = material["name"]
-        mat_id = material["ID"]
-        mat_type = get_or(material, "type", "diffuse")
-        mat_diffuse = populateVec(get_or(material, "diffuse", [0, 0, 0]))
-        mat_specular = populateVec(get_or(material, "specular", [0, 0, 0]))
-        mat_hardness = get_or(material, "hardness", 32)
-        mat_tint = get_or(material, "tint", 0.0)
-        mat_refr_index = get_or(material, "refr_index", 1.0)
-        m = hc.Material(mat_name, mat_specular, mat_diffuse, mat_hardness, mat_id, mat_type, mat_tint)
-        m.refr_index = mat_refr_index
-        materials.append(m)
-
-    objects = []
-    rootNames = []   # hierarchies other nodes may reference (scene_parser.py:147-149)
-    roots = []
-    for geometry in data["objects"]:
-        parse_geometry(geometry, objects, rootNames, roots, materials, base_dir, log)
-
-    for obj in objects:
-        if isinstance(obj, geom.Hierarchy):
-            obj.set_fallback_material(obj.materials)
-
+    b = _SceneBuilder(data, data.get("__base_dir__", base_dir), log)
+    vc = b.camera()
+    lights = b.lights()
+    materials = b.read_materials()
+    objects = b.objects()
     log("Parsing complete")
-    sc = Scene(vc, jitter, samples, ambient, lights, materials, objects)
-    for obj in objects:
-        obj.set_scene(sc)
+    sc = Scene(vc, b.jitter, b.samples, b.ambient, lights, materials, objects)
+    for g in objects:
+        g.set_scene(sc)
     return sc
-
-
-def parse_geometry(geometry, objects, rootNames, roots, materials, base_dir=None, log=print):
-    """scene_parser.py:166-209: basic shapes, hierarchy roots, and nodes that deep-copy an
-    earlier root (`ref`) with their own materials and transform."""
-    g_name = geometry["name"]
-    g_type = geometry["type"]
-    g_pos = populateVec(get_or(geometry, "position", [0, 0, 0]))
-    g_mats = associate_material(materials, get_or(geometry, "materials", []))
-    g_speed = populateVec(get_or(geometry, "speed", None))
-    if add_basic_shape(g_name, g_type, g_pos, g_speed, g_mats, geometry, objects, base_dir):
-        return
-    if g_type == "node":
-        g_ref = get_or(geometry, "ref", "")
-        g_r = populateVec(get_or(geometry, "rotation", [0, 0, 0]))
-        g_s = populateVec(get_or(geometry, "scale", [1, 1, 1]))
-        g_hierarchy_type = get_or(geometry, "hierarchy_type", "union")
-        if g_ref == "":
-            rootNames.append(g_name)
-            node = geom.Hierarchy(g_name, g_type, g_mats, g_hierarchy_type, g_pos, g_r, g_s, g_speed)
-            traverse_children(node, geometry["children"], materials, rootNames, roots, g_speed, base_dir, log)
-            roots.append(node)
-            objects.append(node)
-        else:
-            rid = rootNames.index(g_ref) if g_ref in rootNames else -1
-            if rid != -1:
-                node = copy.deepcopy(roots[rid])
-                node.name = g_name
-                node.materials = g_mats
-                node.make_matrices(g_pos, g_r, g_s)
-                objects.append(node)
-            else:
-                log("Node reference", g_ref, "not found, skipping creation")
-        return
-    log("Unkown object type", g_type, ", skipping initialization")
-
-
-def add_basic_shape(g_name, g_type, g_pos, g_speed, g_mats, geometry, objects, base_dir=None):
-    """scene_parser.py:212-258 (textures: Image.open of the path, scale default 1.0)."""
-    if g_type == "sphere":
-        g_radius = geometry["radius"]
-        objects.append(geom.Sphere(g_name, g_type, g_mats, g_pos, g_radius, g_speed))
-    elif g_type == "plane":
-        g_normal = populateVec(geometry["normal"])
-        plane = geom.Plane(g_name, g_type, g_mats, g_pos, g_normal, g_speed)
-        if "texture" in geometry:
-            plane.texture = geom.open_texture(geometry["texture"], base_dir)
-            plane.texture_scale = get_or(geometry, "texture_scale", 1.0)
-        objects.append(plane)
-    elif g_type == "box":
-        try:
-            g_size = populateVec(geometry["size"])
-            box = geom.AABB(g_name, g_type, g_mats, g_pos, g_size, g_speed)
-        except KeyError:
-            box = geom.AABB(g_name, g_type, g_mats, g_pos, [0, 0, 0], g_speed)
-            box.minpos = geom.F.vec3(populateVec(geometry["min"]))
-            box.maxpos = geom.F.vec3(populateVec(geometry["max"]))
-        if "texture" in geometry:
-            box.texture = geom.open_texture(geometry["texture"], base_dir)
-        objects.append(box)
-    elif g_type == "mesh":
-        g_path = geom.resolve_path(geometry["filepath"], base_dir)
-        g_scale = geometry["scale"]
-        g_flat_shaded = get_or(geometry, "flat_shaded", False)
-        objects.append(geom.Mesh(g_name, g_type, g_mats, g_pos, g_scale, g_path, g_flat_shaded, g_speed))
-    else:
-        return False
-    return True
-
-
-def traverse_children(node, children, materials, rootNames, roots, speed, base_dir=None, log=print):
-    """scene_parser.py:261-285: a child's speed is the root's speed plus its own (fp32);
-    nested nodes pass the ROOT's speed on to their own children (:283)."""
-    for geometry in children:
-        g_name = geometry["name"]
-        g_type = geometry["type"]
-        g_pos = populateVec(get_or(geometry, "position", [0, 0, 0]))
-        g_mats = associate_material(materials, get_or(geometry, "materials", []))
-        if speed is None:
-            g_speed = None
-        else:
-            g_speed = geom.F.vec3(speed) + geom.F.vec3(populateVec(get_or(geometry, "speed", [0, 0, 0])))
-        if add_basic_shape(g_name, g_type, g_pos, g_speed, g_mats, geometry, node.children, base_dir):
-            continue
-        elif g_type == "node":
-            g_r = populateVec(get_or(geometry, "rotation", [0, 0, 0]))
-            g_s = populateVec(get_or(geometry, "scale", [1, 1, 1]))
-            g_hierarchy_type = get_or(geometry, "hierarchy_type", "union")
-            inner = geom.Hierarchy(g_name, g_type, g_mats, g_hierarchy_type, g_pos, g_r, g_s, g_speed)
-            node.children.append(inner)
-            traverse_children(inner, geometry["children"], materials, rootNames, roots, speed, base_dir, log)
-        else:
-            parse_geometry(geometry, node.children, rootNames, roots, materials, base_dir, log)
-
-
-def associate_material(mats, ids):
-    """scene_parser.py:288-294."""
-    return [mat for i in ids for mat in mats if i == mat.ID]
