@@ -609,6 +609,15 @@ RTX_HD bool box_maybe_hit(f3 mn, f3 mx, f3 o, const RayInv& ri, float tcap) {
     return leaf_maybe_hit(B, o, ri, cm, tcap);
 }
 
+// Conservative pre-test of a mesh's bounding volume: false only when the exact test
+// (mesh_bv) cannot pass with an entry at or before tcap. An AABB volume passes only rays
+// that enter it at start >= 0, and every face hit inside it lies beyond that entry, so the
+// padded box of the clusters' bound (box_maybe_hit) decides; sphere volumes always pass.
+template <class O>
+RTX_HD bool bv_maybe(const O& ob, f3 o, const RayInv& ri, float tcap) {
+    return ob.bv_type != BV_AABB || box_maybe_hit(ld3(ob.bv_a), ld3(ob.bv_b), o, ri, tcap);
+}
+
 // Exact fp64 t of a candidate, recomputed from the object exactly as during its test
 // (used only when two fp32 proxies tie; out of line to keep the hot loop's registers low).
 __host__ __device__ __attribute__((noinline)) inline double hit_t64(const SceneView& S, int32_t obj, int32_t sb, f3 o, f3 d, float time) {
@@ -1264,6 +1273,9 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
     if (MESH) {
         for (int k = 0; k < RTX_NMESH(S); ++k, ++oi) {  // mesh.py:72-119, faces in order
             const DObj ob = S.objs[oi];
+            // padded fp32 pre-test of an AABB volume (conservative, bv_maybe): the exact
+            // test only where some lane's ray may enter the box before its best t
+            if (!RTX_ANY(bv_maybe(ob, o, ri, h.t32))) continue;
             if (!mesh_bv(ob, o, d)) continue;  // the reference's bounding volume, quirks included
             for (int li = 0; li < ob.leaf_count;) {  // stackless wave-uniform BVH walk
                 cref<DLeaf> L = S.leaves[ob.leaf_begin + li];
@@ -1389,9 +1401,11 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
         for (int k = 0; k < RTX_NMESH(S); ++k, ++oi) {  // mesh.py:121-153 (no t_max test)
             const DObj ob = S.objs[oi];
             if (RTX_ALL(occ)) break;
-            const bool live = !occ && mesh_bv(ob, o, d);
+            if (RTX_NBOX(S) == 0 && k == 0) ri = ray_inv(o, d);
+            bool live = !occ && bv_maybe(ob, o, ri, INFINITY);  // conservative pre-test
             if (!RTX_ANY(live)) continue;
-            if (RTX_NBOX(S) == 0) ri = ray_inv(o, d);
+            live = live && mesh_bv(ob, o, d);
+            if (!RTX_ANY(live)) continue;
             for (int li = 0; li < ob.leaf_count;) {  // stackless wave-uniform BVH walk
               cref<DLeaf> L = S.leaves[ob.leaf_begin + li];
               const bool maybe = live && !occ && leaf_maybe_hit(L, o, ri, ob.cmax);
