@@ -292,7 +292,6 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import rtx  # noqa: F401
     from rtx.distributed import FramePipeline
-    from rtx.scene import group_rows
 
     sc = make_scene(a.config)
     W, H = sc.vc.width, sc.vc.height
@@ -325,7 +324,7 @@ def main():
         scaling, parallelism = "strong", "single GPU"
     else:
         # N > 1 (north star): one step = ONE frame sharded across the ranks — interleaved
-        # 8-row groups per rank (rtx_render_groups), uint8 on the GPU (rtx_fb_to_rgb8), one
+        # 8-row groups per rank rendered straight to uint8 (rtx_render_groups_rgb8), one
         # RCCL gather to rank 0; frame k's gather overlaps frame k + 1's render.
         pipe = FramePipeline(sc, rank, world)
         for _ in range(a.warmup):
@@ -346,21 +345,33 @@ def main():
         wall_s = max_over_ranks(t1 - t0, use_dist)
         # breakdown (outside the timed region): this rank's render + uint8 conversion, and
         # the gather + reorder alone, each from HIP events on the launch stream
-        kern_ms = max_over_ranks(kernel_ms(lambda: pipe.render_block(pipe.fb), a.steps, stream), use_dist)
+        rank_fb = torch.empty((pipe.slots[0].nrows, W, 3), dtype=torch.float32, device="cuda")
+
+        def fp32_rows():  # this rank's rows into fp32: the kernel the roofline below prices
+            if pipe.interleave:
+                sc.render_device(groups=(rank, world), out=rank_fb, stream=stream)
+            else:
+                sc.render_device(row0=int(pipe.rows[0]), nrows=len(pipe.rows), out=rank_fb, stream=stream)
+        fp32_rows()  # (its first call may compile the fp32 variant of the specialized kernel)
+        torch.cuda.synchronize()
+        kern_ms = max_over_ranks(kernel_ms(fp32_rows, a.steps, stream), use_dist)
         kernel = sc.last_kernel
         render_ms = max_over_ranks(kernel_ms(pipe.render, a.steps, stream), use_dist)
+        kernel_rgb8 = sc.last_kernel
         slot = pipe.slots[0]
         if use_dist:
             dist.barrier()
         gather_ms = max_over_ranks(kernel_ms(slot, a.steps, stream), use_dist)
-        rows_frac = len(group_rows(H, world, rank)) / H
-        nrows = [len(group_rows(H, world, r)) for r in range(world)]
+        rows_frac = pipe.slots[0].nrows / H
+        nrows = [len(r) for r in pipe.slots[0].rows]
         extra["multi_gpu"] = {
             "frame_ms": round(wall_s * 1e3 / a.steps, 5),
             "render_ms_per_rank": round(kern_ms, 5), "render_rgb8_ms_per_rank": round(render_ms, 5),
+            "kernel_rgb8": kernel_rgb8,
             "gather_ms": round(gather_ms, 5),
             "rows_per_rank": [min(nrows), max(nrows)],
-            "partition": "interleaved 8-row groups r, r+N, ... (rtx_render_groups)",
+            "partition": ("interleaved 8-row groups r, r+N, ... (rtx_render_groups_rgb8), reordered on rank 0"
+                          if pipe.interleave else "np.array_split row blocks (rtx_render_rgb8), gathered in image order"),
             "collective": "one torch.distributed.gather of uint8 rows to rank 0 (RCCL), double-buffered",
         }
         # secondary: weak scaling (each rank renders its own whole frame per step)

@@ -195,6 +195,15 @@ int rtx_render(rtx_scene* scene, int32_t row0, int32_t nrows, float* fb_dev,
 int rtx_render_groups(rtx_scene* scene, int32_t phase, int32_t stride, float* fb_dev,
                       uint64_t* counters_dev, void* hip_stream);
 
+/* rtx_render / rtx_render_groups with main.py's PNG conversion fused into the render
+ * (provided/main.py:31-33): out_dev receives uint8 [rows][ncols][3] = (v * 255.0) truncated
+ * of the fp32 values rtx_render would write — identical bytes to rtx_render followed by
+ * rtx_fb_to_rgb8, with 4x fewer bytes stored (and gathered, across ranks). */
+int rtx_render_rgb8(rtx_scene* scene, int32_t row0, int32_t nrows, uint8_t* out_dev,
+                    uint64_t* counters_dev, void* hip_stream);
+int rtx_render_groups_rgb8(rtx_scene* scene, int32_t phase, int32_t stride, uint8_t* out_dev,
+                           uint64_t* counters_dev, void* hip_stream);
+
 /* Rows rtx_render_groups writes for an image of `height` rows (-1: bad arguments). */
 int32_t rtx_group_rows(int32_t height, int32_t phase, int32_t stride);
 

@@ -810,7 +810,7 @@ std::string device_arch(int device) {
 // the on-disk code object depends on the arch only.
 hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& kp, int fc_mode, bool any_speed,
                                 uint32_t ldir, int uniform_hard, bool mesh, bool sec, bool ext, bool cnt, bool jit,
-                                bool spp, std::string* name_out) {
+                                bool spp, bool out8, std::string* name_out) {
     if (!jit_enabled()) return nullptr;
     if (v.n_plane + v.n_sphere + v.n_box + v.n_mesh > 32 || v.n_lights > 8) return nullptr;  // code size
     // CSG/texture kernels: the unrolled loops raise their (already high) register
@@ -840,6 +840,7 @@ hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& k
                                      "-DRTX_FIXED_POWBITS=" + std::to_string(v.pow_bits),
                                      "-DRTX_FIXED_DIVPOW2=" + std::to_string(kp.div_pow2)};
     if (uniform_hard >= 0) opts.push_back("-DRTX_FIXED_HARD=" + std::to_string(uniform_hard));
+    if (out8) opts.push_back("-DRTX_OUT8=1");  // uint8 framebuffer (rtx_render_rgb8)
     const char* lm = getenv("RTX_JIT_LIBMACROS");  // experiment: 0 = do not forward them
     if (!(lm && lm[0] == '0'))
         for (const char* m : kLibMacros) opts.push_back(m);
@@ -852,6 +853,7 @@ hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& k
     std::string name = "rtx_jit_render_";
     for (bool f : {mesh, sec, ext, cnt, jit}) name += f ? '1' : '0';
     if (spp) name += "_spp";
+    if (out8) name += "_rgb8";
     const std::string src = std::string("#include \"rtx_kernels.h\"\nextern \"C\" __global__ RTX_RENDER_BOUNDS(") +
                             b(mesh) + ", " + b(sec) + ", " + b(ext) + ") void " + name + "(const rtx::KParams* "
                             "__restrict__ P, const rtx::Launch L) {\n  rtx::" + (spp ? "render_body_spp<" : "render_body<") +
@@ -970,8 +972,11 @@ struct rtx_scene {
         bool done = false;
         hipFunction_t fn = nullptr;
         std::string name;
-    } resolved[8];
+    } resolved[16];
     std::string last_kernel;  // name of the kernel the last render call launched
+    // fp32 staging of the rgb8 entry points when no scene-specialized kernel is available
+    float* d_scratch = nullptr;
+    size_t scratch_floats = 0;
 };
 
 namespace {
@@ -997,6 +1002,7 @@ void free_camera(rtx_scene* s) {
 
 void free_scene(rtx_scene* s) {
     free_camera(s);
+    (void)hipFree(s->d_scratch);
     for (void* p : {s->d_objs, s->d_tris, s->d_trins, s->d_fboxes, s->d_mats, s->d_lights, s->d_leaves, s->d_tri_orig, s->d_nodes,
                     s->d_texels, s->d_lut, s->d_bounds_abi})
         (void)hipFree(p);
@@ -1118,23 +1124,50 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
 }
 
 namespace {
-int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream);
-}
+int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, bool out8);
 
-int rtx_render(rtx_scene* s, int32_t row0, int32_t nrows, float* fb_dev, uint64_t* counters_dev, void* stream) {
-    if (!s) return fail(RTX_ERR_INVALID, "rtx_render: null scene");
-    if (!s->cam_set) return fail(RTX_ERR_STATE, "rtx_render: rtx_camera_set was not called");
+int render_rows(const char* fn, rtx_scene* s, int32_t row0, int32_t nrows, void* out_dev, uint64_t* counters_dev,
+                void* stream, bool out8) {
+    if (!s) return fail(RTX_ERR_INVALID, std::string(fn) + ": null scene");
+    if (!s->cam_set) return fail(RTX_ERR_STATE, std::string(fn) + ": rtx_camera_set was not called");
     if (row0 < 0 || nrows < 0 || (int64_t)row0 + nrows > s->kp.height)
-        return fail(RTX_ERR_INVALID, "rtx_render: row range outside the image");
+        return fail(RTX_ERR_INVALID, std::string(fn) + ": row range outside the image");
     if (nrows == 0) return RTX_OK;
-    if (!fb_dev) return fail(RTX_ERR_INVALID, "rtx_render: null framebuffer");
+    if (!out_dev) return fail(RTX_ERR_INVALID, std::string(fn) + ": null framebuffer");
     Launch L;
-    L.fb = fb_dev;
+    L.fb = static_cast<float*>(out_dev);
     L.row0 = row0;
     L.nrows = nrows;
     L.gphase = 0;
     L.gstride = 0;
-    return render_launch(s, L, counters_dev, stream);
+    return render_launch(s, L, counters_dev, stream, out8);
+}
+
+int render_groups(const char* fn, rtx_scene* s, int32_t phase, int32_t stride, void* out_dev, uint64_t* counters_dev,
+                  void* stream, bool out8) {
+    if (!s) return fail(RTX_ERR_INVALID, std::string(fn) + ": null scene");
+    if (!s->cam_set) return fail(RTX_ERR_STATE, std::string(fn) + ": rtx_camera_set was not called");
+    const int32_t nrows = rtx_group_rows(s->kp.height, phase, stride);
+    if (nrows < 0) return fail(RTX_ERR_INVALID, std::string(fn) + ": need 0 <= phase < stride");
+    if (nrows == 0) return RTX_OK;
+    if (!out_dev) return fail(RTX_ERR_INVALID, std::string(fn) + ": null framebuffer");
+    Launch L;
+    L.fb = static_cast<float*>(out_dev);
+    L.row0 = 0;
+    L.nrows = nrows;
+    L.gphase = phase;
+    L.gstride = stride;
+    return render_launch(s, L, counters_dev, stream, out8);
+}
+}  // namespace
+
+int rtx_render(rtx_scene* s, int32_t row0, int32_t nrows, float* fb_dev, uint64_t* counters_dev, void* stream) {
+    return render_rows("rtx_render", s, row0, nrows, fb_dev, counters_dev, stream, false);
+}
+
+int rtx_render_rgb8(rtx_scene* s, int32_t row0, int32_t nrows, uint8_t* out_dev, uint64_t* counters_dev,
+                    void* stream) {
+    return render_rows("rtx_render_rgb8", s, row0, nrows, out_dev, counters_dev, stream, true);
 }
 
 int32_t rtx_group_rows(int32_t height, int32_t phase, int32_t stride) {
@@ -1149,23 +1182,25 @@ int32_t rtx_group_rows(int32_t height, int32_t phase, int32_t stride) {
 
 int rtx_render_groups(rtx_scene* s, int32_t phase, int32_t stride, float* fb_dev, uint64_t* counters_dev,
                       void* stream) {
-    if (!s) return fail(RTX_ERR_INVALID, "rtx_render_groups: null scene");
-    if (!s->cam_set) return fail(RTX_ERR_STATE, "rtx_render_groups: rtx_camera_set was not called");
-    const int32_t nrows = rtx_group_rows(s->kp.height, phase, stride);
-    if (nrows < 0) return fail(RTX_ERR_INVALID, "rtx_render_groups: need 0 <= phase < stride");
-    if (nrows == 0) return RTX_OK;
-    if (!fb_dev) return fail(RTX_ERR_INVALID, "rtx_render_groups: null framebuffer");
-    Launch L;
-    L.fb = fb_dev;
-    L.row0 = 0;
-    L.nrows = nrows;
-    L.gphase = phase;
-    L.gstride = stride;
-    return render_launch(s, L, counters_dev, stream);
+    return render_groups("rtx_render_groups", s, phase, stride, fb_dev, counters_dev, stream, false);
+}
+
+int rtx_render_groups_rgb8(rtx_scene* s, int32_t phase, int32_t stride, uint8_t* out_dev, uint64_t* counters_dev,
+                           void* stream) {
+    return render_groups("rtx_render_groups_rgb8", s, phase, stride, out_dev, counters_dev, stream, true);
 }
 
 namespace {
-int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream) {
+int launch_to_rgb8(const float* fb, uint8_t* out, int64_t n, hipStream_t st) {
+    if ((reinterpret_cast<uintptr_t>(fb) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 3) == 0)
+        hipLaunchKernelGGL(k_to_rgb8, dim3((unsigned)((n / 4 + 256) / 256)), dim3(256), 0, st, fb, out, n);
+    else
+        hipLaunchKernelGGL(k_to_rgb8_unaligned, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, fb, out, n);
+    RTX_HIP(hipGetLastError());
+    return RTX_OK;
+}
+
+int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, bool out8) {
     const int32_t nrows = L.nrows;
     int cur = -1;
     if (hipGetDevice(&cur) != hipSuccess || cur != s->device)
@@ -1189,11 +1224,11 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream) 
     };
     int64_t nblocks = blocks(spp_mode);
     if (nblocks > 0x7fffffff || blocks(false) > 0x7fffffff) return fail(RTX_ERR_INVALID, "rtx_render: launch too large");
-    rtx_scene::Resolved& rs = s->resolved[(cnt ? 4 : 0) | (jit ? 2 : 0) | (spp_mode ? 1 : 0)];
+    rtx_scene::Resolved& rs = s->resolved[(out8 ? 8 : 0) | (cnt ? 4 : 0) | (jit ? 2 : 0) | (spp_mode ? 1 : 0)];
     if (!rs.done) {
         rs.fn = jit_render_kernel(s->device, s->view, s->kp, s->fc_mode, s->any_speed, s->light_dir_mask,
                                   s->uniform_hard, s->has_mesh, s->has_secondary, s->has_ext, cnt, jit, spp_mode,
-                                  &rs.name);
+                                  out8, &rs.name);
         rs.done = true;
     }
     if (rs.fn && jit_enabled()) {
@@ -1202,6 +1237,21 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream) 
                                       s->has_ext ? (unsigned)(hbytes * blk) : 0u, st, args, nullptr));
         s->last_kernel = rs.name;
         return RTX_OK;
+    }
+    if (out8) {  // no specialized uint8 kernel: fp32 into the scene's scratch, then convert
+        const size_t n = (size_t)nrows * s->kp.ncols * 3;
+        if (s->scratch_floats < n) {
+            (void)hipFree(s->d_scratch);
+            s->d_scratch = nullptr;
+            s->scratch_floats = 0;
+            RTX_HIP(hipMalloc((void**)&s->d_scratch, n * sizeof(float)));
+            s->scratch_floats = n;
+        }
+        uint8_t* out = reinterpret_cast<uint8_t*>(L.fb);
+        L.fb = s->d_scratch;
+        if (int rc = render_launch(s, L, counters_dev, stream, false)) return rc;
+        s->last_kernel += "+k_to_rgb8";
+        return launch_to_rgb8(s->d_scratch, out, (int64_t)n, st);
     }
     char gname[48];
     snprintf(gname, sizeof(gname), "%s_%d%d%d%d%d%s", s->has_ext ? "k_render_ext" : "k_render", s->has_mesh ? 1 : 0,
@@ -1287,9 +1337,7 @@ int rtx_occluded(rtx_scene* s, int64_t n, const float* ro, const float* rd, cons
 int rtx_fb_to_rgb8(const float* fb, uint8_t* out, int64_t n, void* stream) {
     if (n < 0 || (n > 0 && (!fb || !out))) return fail(RTX_ERR_INVALID, "rtx_fb_to_rgb8: bad argument");
     if (n == 0) return RTX_OK;
-    hipLaunchKernelGGL(k_to_rgb8, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, fb, out, n);
-    RTX_HIP(hipGetLastError());
-    return RTX_OK;
+    return launch_to_rgb8(fb, out, n, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -102,6 +102,19 @@ RTX_HD float sample_mean(const KParams& P, float c) {
 #endif
 }
 
+// The framebuffer store. fp32 RGB (rtx_render), or -- scene-specialized kernels built
+// with RTX_OUT8=1 for rtx_render_rgb8 -- main.py:33's (v * 255).astype(uint8) of the same
+// fp32 value, written as bytes (the PNG's layout: 4x fewer bytes to store and to gather).
+#ifndef RTX_OUT8
+#define RTX_OUT8 0
+#endif
+RTX_HD void put_channel(float* fb, int64_t i, float v) {
+    if (RTX_OUT8)
+        reinterpret_cast<uint8_t*>(fb)[i] = (uint8_t)(int)((double)v * 255.0);
+    else
+        fb[i] = v;
+}
+
 // scene.py:47-79 for pixel p of the output block (host/device: the tests-only host
 // emulation runs the same body).
 template <bool MESH, bool SEC, bool X, bool COUNT, bool JIT>
@@ -109,7 +122,7 @@ RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, 
                          const FrameStack& fs, const HStack& hs) {
     const int64_t p = (int64_t)rr * P.ncols + cc;
     if (RTX_ABLATE == 14) {  // cost probe only: store a constant (launch + framebuffer write)
-        fb[3 * p] = 0.5f; fb[3 * p + 1] = 0.25f; fb[3 * p + 2] = 0.125f;
+        put_channel(fb, 3 * p, 0.5f); put_channel(fb, 3 * p + 1, 0.25f); put_channel(fb, 3 * p + 2, 0.125f);
         return;
     }
     const int j = P.height - 1 - (row0 + rr);  // reference row index (y grows upward)
@@ -138,10 +151,9 @@ RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, 
         colour = mk(c0, c1, c2 + c3 * 0.0f);
     }
 #endif
-    float* out = fb + 3 * p;
-    out[0] = colour.x;
-    out[1] = colour.y;
-    out[2] = colour.z;
+    put_channel(fb, 3 * p, colour.x);
+    put_channel(fb, 3 * p + 1, colour.y);
+    put_channel(fb, 3 * p + 2, colour.z);
 }
 
 // The per-frame parameters live in device memory (uploaded by rtx_camera_set) and are
@@ -309,7 +321,7 @@ __device__ __forceinline__ void render_body_spp(const KParams* __restrict__ Pp, 
                     const float* src = sbuf + ch * B + pp * S;
                     float a = 0.0f;
                     for (int k = 0; k < S; ++k) a += src[k];
-                    L.fb[3 * (pix0 + pp) + ch] = sample_mean(P, a);
+                    put_channel(L.fb, 3 * (pix0 + pp) + ch, sample_mean(P, a));
                 }
             }
         } else if (tid < 3) {  // this round's samples of the block's pixel
@@ -319,7 +331,7 @@ __device__ __forceinline__ void render_body_spp(const KParams* __restrict__ Pp, 
         }
         if (rounds > 1) __syncthreads();  // sbuf is reused by the next round
     }
-    if (rounds > 1 && tid < 3 && pix0 < npix) L.fb[3 * pix0 + tid] = sample_mean(P, acc);
+    if (rounds > 1 && tid < 3 && pix0 < npix) put_channel(L.fb, 3 * pix0 + tid, sample_mean(P, acc));
     flush_tally<COUNT>(tl, L.counters, any_active);
 }
 
@@ -383,10 +395,22 @@ __global__ __launch_bounds__(256) void k_occluded(SceneView S, int64_t n, const 
 }
 
 #if !defined(RTX_EXT_TU)  // defined once, in rtx_api.hip
+// (v * 255.0) truncated to uint8, four values per thread: one 16-byte load and one 4-byte
+// store (fb 16-byte and out 4-byte aligned; rtx_fb_to_rgb8 checks), the tail one by one.
+__device__ __forceinline__ uint8_t to_u8(float v) { return (uint8_t)(int)((double)v * 255.0); }
 __global__ __launch_bounds__(256) void k_to_rgb8(const float* __restrict__ fb, uint8_t* __restrict__ out, int64_t n) {
+    const int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+    if (i + 4 <= n) {
+        const float4 v = *reinterpret_cast<const float4*>(fb + i);
+        *reinterpret_cast<uchar4*>(out + i) = make_uchar4(to_u8(v.x), to_u8(v.y), to_u8(v.z), to_u8(v.w));
+    } else {
+        for (int64_t k = i; k < n; ++k) out[k] = to_u8(fb[k]);
+    }
+}
+__global__ __launch_bounds__(256) void k_to_rgb8_unaligned(const float* __restrict__ fb, uint8_t* __restrict__ out,
+                                                           int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    out[i] = (uint8_t)(int)((double)fb[i] * 255.0);
+    if (i < n) out[i] = to_u8(fb[i]);
 }
 #endif
 #endif  // !__HIPCC_RTC__

@@ -45,6 +45,9 @@ class FrameGather:
         shape = (self.maxrows, width, channels)
         self.send = torch.zeros(shape, dtype=dtype, device=device)
         self.block = self.send[:self.nrows]  # this rank renders (or converts) into it
+        # contiguous equal blocks (np.array_split with world | height) arrive in image order:
+        # the receive buffer IS the frame, no reorder
+        self.in_order = not interleave and height == world * self.maxrows
         if rank == dst:
             self.recv = torch.empty((world,) + shape, dtype=dtype, device=device)
             self.recv_list = list(self.recv.unbind(0))
@@ -53,14 +56,18 @@ class FrameGather:
                 src[rows] = r * self.maxrows + np.arange(len(rows))
             self.index = torch.as_tensor(src, device=device)
 
+    def frame(self):
+        """The gathered frame [height, W, C] on ``dst`` (after the gather completed)."""
+        flat = self.recv.view((self.world * self.maxrows,) + tuple(self.recv.shape[2:]))
+        return flat if self.in_order else torch.index_select(flat, 0, self.index)
+
     def __call__(self):
         """Gather the ranks' blocks; returns the frame on ``dst`` and None elsewhere."""
         if self.rank != self.dst:
             dist.gather(self.send, dst=self.dst, group=self.group)
             return None
         dist.gather(self.send, gather_list=self.recv_list, dst=self.dst, group=self.group)
-        flat = self.recv.view((self.world * self.maxrows,) + tuple(self.recv.shape[2:]))
-        return torch.index_select(flat, 0, self.index)
+        return self.frame()
 
 
 def gather_rows(block, height, world, rank, dst=0, group=None, interleave=False):
@@ -82,7 +89,8 @@ def gather_groups(block, height, world, rank, dst=0, group=None):
 def to_rgb8(block):
     """(block * 255.0) truncated to uint8 (main.py:33): rtx_fb_to_rgb8 on the rank's GPU.
     CPU blocks (the gloo tests' host emulation of a rank) are converted with the same
-    fp64 multiply and truncation on the host."""
+    fp64 multiply and truncation on the host. (The bench's pipeline renders uint8
+    directly: rtx_render_groups_rgb8.)"""
     if block.is_cuda:
         from .scene import fb_to_rgb8
         return fb_to_rgb8(block)
@@ -116,46 +124,51 @@ def render_frame(scene, rank, world, render_rows=None, dtype=torch.float32, dst=
 
 class FramePipeline:
     """The multi-GPU frame loop of bench.py (north star: one frame sharded across the node,
-    one gather at the end): every step renders this rank's interleaved 8-row groups of
-    the next frame, converts them to uint8 on the GPU and starts their gather to ``dst``
-    asynchronously; the previous frame's gather is then awaited (a stream wait, not a host
-    wait, on RCCL) and its rows put in place. Two buffer slots, so frame k's gather runs
-    while frame k + 1 renders. ``render_block(out)`` / ``convert(fb, out)`` default to
-    rtx_render_groups and rtx_fb_to_rgb8; the CPU tests inject the host emulation."""
+    one gather at the end): every step renders this rank's rows of the next frame straight
+    into uint8 (rtx_render_rgb8 / rtx_render_groups_rgb8: main.py:33's conversion fused
+    into the render kernel) and starts their gather to ``dst`` asynchronously; the previous
+    frame's gather is then awaited (a stream wait, not a host wait, on RCCL). Two buffer
+    slots, so frame k's gather runs while frame k + 1 renders.
 
-    def __init__(self, scene, rank, world, dst=0, group=None, device=None, render_block=None, convert=None):
+    Partition: ``interleave=True`` gives rank r the 8-row groups r, r + N, ... (balances
+    cheap sky rows against expensive ground rows; rank 0 reorders the gathered rows with
+    one index_select); ``interleave=False`` the np.array_split row blocks, which for
+    N | height arrive in image order (zero-copy frame). Default: interleave when a pixel
+    has several samples (render time dominates), blocks for 1-spp frames (the gather
+    dominates). ``render_block(out, rows)`` fills this rank's uint8 rows [len(rows), W, 3];
+    the CPU tests inject the host emulation."""
+
+    def __init__(self, scene, rank, world, dst=0, group=None, device=None, render_block=None, interleave=None):
         H, W = scene.vc.height, scene.vc.width
         device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-        self.rank, self.dst, self.group = rank, dst, group
-        self.slots = [FrameGather(H, W, 3, world, rank, torch.uint8, device, interleave=True, dst=dst, group=group)
-                      for _ in range(2)]
-        self.fb = torch.empty((self.slots[0].nrows, W, 3), dtype=torch.float32, device=device)
-        self.render_block = render_block or (lambda out: scene.render_device(groups=(rank, world), out=out))
-        self.convert = convert or self._to_rgb8
+        if interleave is None:
+            interleave = scene.samples_per_pixel > 1
+        self.rank, self.dst, self.group, self.interleave = rank, dst, group, interleave
+        self.slots = [FrameGather(H, W, 3, world, rank, torch.uint8, device, interleave=interleave, dst=dst,
+                                  group=group) for _ in range(2)]
+        self.rows = self.slots[0].rows[rank]
+        if render_block is None:
+            if interleave:
+                def render_block(out, rows):
+                    scene.render_device(groups=(rank, world), out=out)
+            else:
+                r0, n = row_block(H, world, rank)
+
+                def render_block(out, rows):
+                    scene.render_device(row0=r0, nrows=n, out=out)
+        self.render_block = render_block
         self.k = 0
         self.prev = None  # (work, slot) of the last submitted frame
 
-    @staticmethod
-    def _to_rgb8(fb, out):
-        if fb.is_cuda:
-            from .scene import fb_to_rgb8
-            fb_to_rgb8(fb, out=out)
-        else:
-            out.copy_(to_rgb8(fb))
-
     def _finish(self, work, slot):
         work.wait()
-        if self.rank != self.dst:
-            return None
-        flat = slot.recv.view((slot.world * slot.maxrows,) + tuple(slot.recv.shape[2:]))
-        return torch.index_select(flat, 0, slot.index)
+        return slot.frame() if self.rank == self.dst else None
 
     def render(self):
-        """Render and convert this rank's rows of the next frame into the free slot."""
+        """Render this rank's rows of the next frame into the free slot."""
         slot = self.slots[self.k % 2]
         if slot.nrows:
-            self.render_block(self.fb)
-            self.convert(self.fb, slot.block)
+            self.render_block(slot.block, self.rows)
         return slot
 
     def step(self):

@@ -214,11 +214,13 @@ class Scene:
 
     # ------------------------------------------------------------------ rendering
     def render_device(self, subimage=0, tasks=1, row0=0, nrows=None, out=None, counters=None, stream=None,
-                      groups=None):
+                      groups=None, rgb8=False):
         """Render image rows [row0, row0 + nrows) (row 0 = top) of the strip into a float32
         CUDA tensor [nrows, strip_width, 3] (the rot90'd reference image). Asynchronous
         on ``stream`` (default: torch's current stream). ``groups=(k, n)`` instead renders
-        the interleaved 8-row groups k, k + n, ... (rows ``group_rows(H, n, k)``, packed)."""
+        the interleaved 8-row groups k, k + n, ... (rows ``group_rows(H, n, k)``, packed).
+        A uint8 ``out`` (or rgb8=True) gets main.py's PNG bytes from the fused kernel
+        (rtx_render_rgb8 / rtx_render_groups_rgb8)."""
         t = self._set_camera(subimage, tasks)
         if groups is not None:
             k, n = groups
@@ -228,20 +230,23 @@ class Scene:
         if nrows is None:
             nrows = self.vc.height - row0
         if out is None:
-            out = torch.empty((nrows, t["ncols"], 3), dtype=torch.float32, device="cuda")
-        if tuple(out.shape) != (nrows, t["ncols"], 3) or out.dtype != torch.float32 or not out.is_cuda \
-                or not out.is_contiguous():
-            raise ValueError("out must be a contiguous float32 CUDA tensor of shape %s" % ((nrows, t["ncols"], 3),))
+            out = torch.empty((nrows, t["ncols"], 3), dtype=torch.uint8 if rgb8 else torch.float32, device="cuda")
+        rgb8 = out.dtype == torch.uint8
+        if tuple(out.shape) != (nrows, t["ncols"], 3) or out.dtype not in (torch.float32, torch.uint8) \
+                or not out.is_cuda or not out.is_contiguous():
+            raise ValueError("out must be a contiguous float32 or uint8 CUDA tensor of shape %s"
+                             % ((nrows, t["ncols"], 3),))
         if counters is not None and (counters.numel() < N.RTX_COUNTERS or counters.dtype != torch.int64
                                      or not counters.is_cuda):
             raise ValueError("counters must be an int64 CUDA tensor with >= %d entries" % N.RTX_COUNTERS)
         st = stream if stream is not None else torch.cuda.current_stream()
         cnt = C.c_void_p(counters.data_ptr() if counters is not None else 0)
+        suffix = "_rgb8" if rgb8 else ""
         if groups is not None:
-            N.call("rtx_render_groups", self._native.h, int(groups[0]), int(groups[1]), C.c_void_p(out.data_ptr()),
-                   cnt, C.c_void_p(st.cuda_stream))
+            N.call("rtx_render_groups" + suffix, self._native.h, int(groups[0]), int(groups[1]),
+                   C.c_void_p(out.data_ptr()), cnt, C.c_void_p(st.cuda_stream))
         else:
-            N.call("rtx_render", self._native.h, int(row0), int(nrows), C.c_void_p(out.data_ptr()), cnt,
+            N.call("rtx_render" + suffix, self._native.h, int(row0), int(nrows), C.c_void_p(out.data_ptr()), cnt,
                    C.c_void_p(st.cuda_stream))
         return out
 
@@ -253,7 +258,7 @@ class Scene:
 
     def render_rgb8(self, subimage=0, tasks=1):
         """main.py:31-33 on the device: (rot90(image) * 255).astype(uint8), (H, W, 3)."""
-        return fb_to_rgb8(self.render_device(subimage, tasks)).cpu().numpy()
+        return self.render_device(subimage, tasks, rgb8=True).cpu().numpy()
 
     # ------------------------------------------------------------------ Geometry ABI (batched)
     def intersect(self, origins, directions, time=0.0):

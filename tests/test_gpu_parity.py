@@ -410,3 +410,47 @@ def test_interleaved_row_groups_equal_full_frame(name, res, edits):
             fb = torch.full((len(rows), res[0], 3), float("nan"), dtype=torch.float32, device="cuda")
             got = sc.render_device(groups=(k, n), out=fb)
             assert torch.equal(got, full[torch.as_tensor(rows, device="cuda")]), (n, k)
+
+
+@pytest.mark.parametrize("name,res,edits", [
+    ("TwoSpheresPlane", (160, 90), {}), ("MirrorRefraction", (97, 61), {}), ("TorusMesh", (96, 96), {}),
+    ("DepthOfField", (64, 48), {"AA": {"jitter": True, "samples": 2}}),
+    ("NovelScene1", (64, 32), {"AA": {"jitter": True, "samples": 2}}),
+])
+def test_fused_rgb8_equals_render_then_convert(name, res, edits):
+    """rtx_render_rgb8 / rtx_render_groups_rgb8 (main.py's uint8 conversion fused into the
+    scene-specialized kernel; hierarchy/texture scenes stage through fp32 + k_to_rgb8) give
+    the bytes of rtx_render followed by rtx_fb_to_rgb8, for row blocks and row groups."""
+    from rtx.scene import fb_to_rgb8, group_rows
+    sc = product_scene(name, res, **edits)
+    W, H = res
+    full = sc.render_device().clone()
+    want = fb_to_rgb8(full)
+    got = sc.render_device(rgb8=True)
+    assert got.dtype == torch.uint8 and torch.equal(got, want)
+    flat = name != "NovelScene1"
+    assert sc.last_kernel.endswith("_rgb8") if flat else sc.last_kernel.endswith("+k_to_rgb8"), sc.last_kernel
+    part = torch.full((20, W, 3), 7, dtype=torch.uint8, device="cuda")
+    assert torch.equal(sc.render_device(row0=H - 20, nrows=20, out=part), want[H - 20:])
+    for n in (2, 3):
+        for k in range(n):
+            rows = torch.as_tensor(group_rows(H, n, k), device="cuda")
+            assert torch.equal(sc.render_device(groups=(k, n), rgb8=True), want[rows]), (n, k)
+    assert np.array_equal(sc.render_rgb8(), want.cpu().numpy())
+
+
+def test_rgb8_conversion_unaligned_and_tails():
+    """rtx_fb_to_rgb8's vector kernel (16-byte fp32 loads) and its unaligned / tail paths."""
+    import ctypes as C
+    from rtx import _native as N
+    g = torch.Generator(device="cpu").manual_seed(3)
+    base = torch.rand(3 * 1001 + 1, generator=g, dtype=torch.float32)
+    base[:7] = torch.tensor([0.0, 1.0, 0.999999, 1.0 / 255, 2.0 / 255, 0.5, 254.5 / 255])
+    for off, n in ((0, 3003), (1, 3000), (0, 3001), (2, 7)):
+        src = base[off:off + n].contiguous() if off == 0 else base.cuda()[off:off + n]
+        fb = src.cuda() if not src.is_cuda else src
+        out = torch.empty(n, dtype=torch.uint8, device="cuda")
+        N.call("rtx_fb_to_rgb8", C.c_void_p(fb.data_ptr()), C.c_void_p(out.data_ptr()), n,
+               C.c_void_p(torch.cuda.current_stream().cuda_stream))
+        want = (fb.cpu().numpy().astype(np.float64) * 255.0).astype(np.uint8)
+        assert np.array_equal(out.cpu().numpy(), want), (off, n)

@@ -50,7 +50,7 @@ def _worker(rank, world, port, name, res, out_q):
     dist.destroy_process_group()
 
 
-def _pipeline_worker(rank, world, port, name, res, nframes, out_q):
+def _pipeline_worker(rank, world, port, name, res, nframes, interleave, out_q):
     """bench.py's multi-GPU frame loop (rtx.distributed.FramePipeline: render this rank's
     interleaved groups, uint8, async gather, previous frame finished while the next one
     renders) with the host emulation as each rank's renderer."""
@@ -63,14 +63,12 @@ def _pipeline_worker(rank, world, port, name, res, nframes, out_q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import hostemu
     from common import product_scene
-    from rtx.distributed import FramePipeline
-    from rtx.scene import group_rows
+    from rtx.distributed import FramePipeline, to_rgb8
     sc = product_scene(name, res)
-    rows = group_rows(res[1], world, rank)
 
-    def render_block(out):
-        out.copy_(torch.from_numpy(hostemu.render_rows(sc, rows, threads=2)))
-    pipe = FramePipeline(sc, rank, world, device=torch.device("cpu"), render_block=render_block)
+    def render_block(out, rows):  # the fused uint8 render, emulated: fp32 rows, then main.py's conversion
+        out.copy_(to_rgb8(torch.from_numpy(hostemu.render_rows(sc, rows, threads=2))))
+    pipe = FramePipeline(sc, rank, world, device=torch.device("cpu"), render_block=render_block, interleave=interleave)
     frames = [pipe.step() for _ in range(nframes)] + [pipe.flush()]
     if rank == 0:
         assert frames[0] is None and all(f is not None for f in frames[1:])
@@ -81,14 +79,15 @@ def _pipeline_worker(rank, world, port, name, res, nframes, out_q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,res", [(2, (40, 23)), (3, (33, 26))])
-def test_frame_pipeline_gathers_every_frame(world, res):
+@pytest.mark.parametrize("world,res,interleave", [(2, (40, 23), True), (3, (33, 26), True), (2, (40, 24), False),
+                                                  (3, (20, 13), False)])
+def test_frame_pipeline_gathers_every_frame(world, res, interleave):
     from common import oracle_render
     from oracle import oracle as O
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_pipeline_worker, args=(r, world, port, "MirrorRefraction", res, 3, q))
+    procs = [ctx.Process(target=_pipeline_worker, args=(r, world, port, "MirrorRefraction", res, 3, interleave, q))
              for r in range(world)]
     for p in procs:
         p.start()
