@@ -841,6 +841,14 @@ hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& k
                                      "-DRTX_FIXED_DIVPOW2=" + std::to_string(kp.div_pow2)};
     if (uniform_hard >= 0) opts.push_back("-DRTX_FIXED_HARD=" + std::to_string(uniform_hard));
     if (out8) opts.push_back("-DRTX_OUT8=1");  // uint8 framebuffer (rtx_render_rgb8)
+    if (mesh && !spp && v.n_mesh > 0) {  // experiment: the meshes' hot records in LDS (RTX_MESH_LDS=1)
+        const char* e = getenv("RTX_MESH_LDS");
+        const size_t bytes = (size_t)v.n_tris * (sizeof(DTri) + sizeof(DFaceBox)) + (size_t)v.n_leaves * sizeof(DLeaf);
+        if (e && e[0] == '1' && bytes <= 48 * 1024) {
+            opts.push_back("-DRTX_LDS_TRIS=" + std::to_string(v.n_tris));
+            opts.push_back("-DRTX_LDS_LEAVES=" + std::to_string(v.n_leaves));
+        }
+    }
     const char* lm = getenv("RTX_JIT_LIBMACROS");  // experiment: 0 = do not forward them
     if (!(lm && lm[0] == '0'))
         for (const char* m : kLibMacros) opts.push_back(m);
@@ -1076,6 +1084,8 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
     v.texels = (cptr<uint32_t>)s->d_texels;
     v.lut255 = (cptr<float>)s->d_lut;
     v.n_nodes = (int32_t)H.nodes.size();
+    v.n_tris = (int32_t)H.tris.size();
+    v.n_leaves = (int32_t)H.leaves.size();
     v.hlevels = H.hlevels;
     *out = s;
     return RTX_OK;

@@ -227,9 +227,28 @@ constexpr int kBlock = X ? 64 : RTX_BLOCK_FLAT;
 
 // The body of k_render, shared with the scene-specialized kernels compiled at run time
 // (rtx_jit.cpp), which pin the scene's object and light counts.
+// RTX_LDS_TRIS kernels: the block copies the scene's triangles, face boxes and BVH nodes
+// into LDS (16-byte words, all lanes) before tracing (rtx_trace.h RTX_TRI / RTX_LEAF).
+__device__ __forceinline__ void stage_mesh_lds(const SceneView& S) {
+#if defined(RTX_LDS_TRIS) && defined(__HIP_DEVICE_COMPILE__)
+    auto copy = [](void* dst, const void RTX_CONST* src, int words) {
+        uint4* d = static_cast<uint4*>(dst);
+        const uint4 RTX_CONST* s = static_cast<const uint4 RTX_CONST*>(src);
+        for (int i = threadIdx.x; i < words; i += blockDim.x) d[i] = s[i];
+    };
+    copy(g_lds_tris, S.tris, RTX_LDS_TRIS * (int)(sizeof(DTri) / 16));
+    copy(g_lds_fboxes, S.fboxes, RTX_LDS_TRIS * (int)(sizeof(DFaceBox) / 16));
+    copy(g_lds_leaves, S.leaves, RTX_LDS_LEAVES * (int)(sizeof(DLeaf) / 16));
+    __syncthreads();
+#else
+    (void)S;
+#endif
+}
+
 template <bool MESH, bool SEC, bool X, bool COUNT, bool JIT>
 __device__ __forceinline__ void render_body(const KParams* __restrict__ Pp, const Launch L) {
     constexpr int B = kBlock<X>;
+    if (MESH) stage_mesh_lds(Pp->S);
     const int32_t ncols = Pp->ncols;
     Tally tl = {};
     // secondary-ray frames: [frame][word][thread] in LDS (40 KB per 256-thread block)

@@ -223,8 +223,26 @@ struct SceneView {
     cptr<uint32_t> texels;           // all textures, RGBA8 (A unused)
     cptr<float> lut255;              // fl32(k / 255) (simple_geometry.py:169)
     cptr<DBound> bounds;             // per node, for the current motion-time range
-    int32_t n_nodes, hlevels, pad3, pad4;  // hlevels: stack levels the hierarchies need
+    int32_t n_nodes, hlevels;        // hlevels: stack levels the hierarchies need
+    int32_t n_tris, n_leaves;        // all triangles / mesh BVH nodes
 };
+
+// Mesh records read by the hot BVH walks (closest_hit / occluded). Scene-specialized
+// kernels built with RTX_LDS_TRIS / RTX_LDS_LEAVES (the scene's triangle and BVH-node
+// counts; rtx_api.hip, RTX_MESH_LDS=1) stage them in LDS once per block (render_body) and
+// read them from there; everything else reads them through the constant cache.
+#if defined(RTX_LDS_TRIS) && defined(__HIP_DEVICE_COMPILE__)
+__shared__ DTri g_lds_tris[RTX_LDS_TRIS];
+__shared__ DFaceBox g_lds_fboxes[RTX_LDS_TRIS];
+__shared__ DLeaf g_lds_leaves[RTX_LDS_LEAVES];
+#define RTX_TRI(S, i) (g_lds_tris[i])
+#define RTX_FBOX(S, i) (g_lds_fboxes[i])
+#define RTX_LEAF(S, i) (g_lds_leaves[i])
+#else
+#define RTX_TRI(S, i) ((S).tris[i])
+#define RTX_FBOX(S, i) ((S).fboxes[i])
+#define RTX_LEAF(S, i) ((S).leaves[i])
+#endif
 
 // ------------------------------------------------------------------ counters
 struct Tally {
@@ -1278,17 +1296,17 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
             if (!RTX_ANY(bv_maybe(ob, o, ri, h.t32))) continue;
             if (!mesh_bv(ob, o, d)) continue;  // the reference's bounding volume, quirks included
             for (int li = 0; li < ob.leaf_count;) {  // stackless wave-uniform BVH walk
-                cref<DLeaf> L = S.leaves[ob.leaf_begin + li];
+                const auto& L = RTX_LEAF(S, ob.leaf_begin + li);
                 const bool maybe = leaf_maybe_hit(L, o, ri, ob.cmax, h.t32);
                 if (!RTX_ANY(maybe)) { li = L.skip; continue; }
                 ++li;
                 for (int f = L.first; f < L.first + L.count; ++f) {
                     bool fmaybe = maybe;
                     if (face_cull(ob)) {  // the face's own padded box (the cluster's bound)
-                        fmaybe = maybe && leaf_maybe_hit(S.fboxes[ob.tri_begin + f], o, ri, ob.cmax, h.t32);
+                        fmaybe = maybe && leaf_maybe_hit(RTX_FBOX(S, ob.tri_begin + f), o, ri, ob.cmax, h.t32);
                         if (!RTX_ANY(fmaybe)) continue;  // no lane's ray can pass its exact test
                     }
-                    const DTri T = S.tris[ob.tri_begin + f];
+                    const DTri T = RTX_TRI(S, ob.tri_begin + f);
                     tally_inc<COUNT>(tl, &Tally::tri);
                     const f3 n = ld3(T.n);
                     const float denom = dot(d, n);
@@ -1407,17 +1425,17 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
             live = live && mesh_bv(ob, o, d);
             if (!RTX_ANY(live)) continue;
             for (int li = 0; li < ob.leaf_count;) {  // stackless wave-uniform BVH walk
-              cref<DLeaf> L = S.leaves[ob.leaf_begin + li];
+              const auto& L = RTX_LEAF(S, ob.leaf_begin + li);
               const bool maybe = live && !occ && leaf_maybe_hit(L, o, ri, ob.cmax);
               if (!RTX_ANY(maybe)) { li = L.skip; continue; }
               ++li;
               for (int f = L.first; f < L.first + L.count; ++f) {
                 bool fmaybe = maybe;
                 if (face_cull(ob)) {
-                    fmaybe = maybe && leaf_maybe_hit(S.fboxes[ob.tri_begin + f], o, ri, ob.cmax);
+                    fmaybe = maybe && leaf_maybe_hit(RTX_FBOX(S, ob.tri_begin + f), o, ri, ob.cmax);
                     if (!RTX_ANY(fmaybe)) continue;
                 }
-                const DTri T = S.tris[ob.tri_begin + f];
+                const DTri T = RTX_TRI(S, ob.tri_begin + f);
                 tally_inc<COUNT>(tl, &Tally::tri);
                 const f3 n = ld3(T.nu);
                 const float denom = dot(d, n);
