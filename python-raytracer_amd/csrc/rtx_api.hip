@@ -709,6 +709,153 @@ int convert_camera(const rtx_camera_desc* c, KParams& k) {
     return RTX_OK;
 }
 
+// Primary-ray bins. With one sample per pixel, no lens (dof origin == camera position)
+// and no jitter, every primary ray leaves the same origin o (the AA origin, scene.py:60-61)
+// in the direction of x u + y v - d w (scene.py:54): a pinhole projection. An object whose
+// bounding points all lie in front of o projects inside the rectangle of its projected
+// points; padded by 2 pixels (far beyond the ~1e-4 px the fp32 ray setup moves a ray), it
+// holds every pixel whose primary ray can hit the object. Rectangles are binned into 8x8
+// pixel bins aligned with the strip's columns and the image rows, so a tile that starts
+// on a multiple of 8 rows finds in its bin (rtx_kernels.h primary_bin):
+//   * objmask: the static spheres (bits 0-15) and boxes (16-31) it may hit; spheres are
+//     inflated by 2^-8 (|o - c| + r), beyond the fuzz of the reference's fp32 discriminant
+//     (a ray can "hit" a sphere it misses by ~2^-10.5 |o - c|); moving objects, or more
+//     than 16 of a kind, are always tested;
+//   * the faces of the scene's one top-level mesh (if it has exactly one) it may hit,
+//     nearest first, with a lower bound of their hit t (depth <= t).
+// Other tiles and secondary/shadow rays walk everything. Returns false when the camera
+// does not qualify, or a mesh face lies near or behind the origin's plane.
+bool primary_bins(const HostScene& H, const rtx_camera_desc* c, std::vector<int32_t>& start,
+                  std::vector<int32_t>& faces, std::vector<float>& zmin, std::vector<uint32_t>& objmask,
+                  int32_t& bins_x, int32_t& mesh_bins) {
+    if (c->n_dof != 1 || c->n_aa != 1 || c->jitter != RTX_JITTER_OFF) return false;
+    if (c->ncols < 2 || c->height < 2) return false;
+    if (c->dof_origins[0] != c->position[0] || c->dof_origins[1] != c->position[1] ||
+        c->dof_origins[2] != c->position[2])
+        return false;
+    const double o[3] = {c->aa_origins[0], c->aa_origins[1], c->aa_origins[2]};
+    const double dx = (double)c->xs[1] - (double)c->xs[0], dy = (double)c->ys[1] - (double)c->ys[0];
+    if (!(dx > 0.0) || !(dy > 0.0)) return false;
+    const int32_t W = c->ncols, Hh = c->height;
+    bins_x = (W + 7) / 8;
+    const int32_t bins_y = (Hh + 7) / 8;
+    const size_t nb = (size_t)bins_x * bins_y;
+    // pixel coordinates (strip column, image row) and depth of a point; false: grazing/behind
+    auto project = [&](const double p[3], double& col, double& row, double& depth) {
+        double rel[3], len2 = 0.0, pu = 0.0, pv = 0.0, pw = 0.0;
+        for (int a = 0; a < 3; ++a) {
+            rel[a] = p[a] - o[a];
+            len2 += rel[a] * rel[a];
+            pu += rel[a] * c->u[a];
+            pv += rel[a] * c->v[a];
+            pw += rel[a] * c->w[a];
+        }
+        depth = -pw;
+        if (!(depth > 1e-3 * std::sqrt(len2)) || !(depth > 1e-9)) return false;
+        col = (c->d * pu / depth - (double)c->xs[0]) / dx;
+        row = (double)(Hh - 1) - (c->d * pv / depth - (double)c->ys[0]) / dy;
+        return true;
+    };
+    struct Rect { int32_t c0, c1, r0, r1; };
+    // bin range of the points' padded pixel rectangle (c0 > c1: off the strip); false if a
+    // point cannot be projected
+    auto rect_of = [&](const double (*pts)[3], int n, Rect& R, double& zlo) {
+        double cmin = INFINITY, cmax = -INFINITY, rmin = INFINITY, rmax = -INFINITY;
+        zlo = INFINITY;
+        for (int i = 0; i < n; ++i) {
+            double col, row, depth;
+            if (!project(pts[i], col, row, depth)) return false;
+            cmin = std::min(cmin, col); cmax = std::max(cmax, col);
+            rmin = std::min(rmin, row); rmax = std::max(rmax, row);
+            zlo = std::min(zlo, depth);
+        }
+        R = Rect{1, 0, 1, 0};
+        const double c0 = std::floor(cmin) - 2.0, c1 = std::ceil(cmax) + 2.0;
+        const double r0 = std::floor(rmin) - 2.0, r1 = std::ceil(rmax) + 2.0;
+        if (c1 >= 0.0 && c0 <= W - 1 && r1 >= 0.0 && r0 <= Hh - 1) {
+            R.c0 = (int32_t)std::max(0.0, c0) >> 3; R.c1 = (int32_t)std::min((double)(W - 1), c1) >> 3;
+            R.r0 = (int32_t)std::max(0.0, r0) >> 3; R.r1 = (int32_t)std::min((double)(Hh - 1), r1) >> 3;
+        }
+        return true;
+    };
+    auto mark = [&](const Rect& R, uint32_t bit) {
+        for (int32_t by = R.r0; by <= R.r1; ++by)
+            for (int32_t bx = R.c0; bx <= R.c1; ++bx) objmask[(size_t)by * bins_x + bx] |= bit;
+    };
+    auto box_corners = [](const double lo[3], const double hi[3], double (*pts)[3]) {
+        for (int q = 0; q < 8; ++q)
+            for (int a = 0; a < 3; ++a) pts[q][a] = (q >> a) & 1 ? hi[a] : lo[a];
+    };
+    objmask.assign(nb, 0u);
+    const Rect all{0, bins_x - 1, 0, bins_y - 1};
+    for (int32_t k = 0; k < H.n_sphere; ++k) {
+        const DObj& ob = H.objs[H.n_plane + k];
+        const uint32_t bit = 1u << (k & 15);
+        double pts[8][3], lo[3], hi[3], oc2 = 0.0, z;
+        for (int a = 0; a < 3; ++a) oc2 += ((double)ob.a[a] - o[a]) * ((double)ob.a[a] - o[a]);
+        const double re = ob.radius + 0x1p-8 * (std::sqrt(oc2) + std::fabs(ob.radius));
+        for (int a = 0; a < 3; ++a) { lo[a] = ob.a[a] - re; hi[a] = ob.a[a] + re; }
+        box_corners(lo, hi, pts);
+        Rect R;
+        if (H.n_sphere > 16 || ob.has_speed || !std::isfinite(re) || !rect_of(pts, 8, R, z)) R = all;
+        mark(R, bit);
+    }
+    for (int32_t k = 0; k < H.n_box; ++k) {
+        const DObj& ob = H.objs[H.n_plane + H.n_sphere + k];
+        const uint32_t bit = 1u << (16 + (k & 15));
+        double pts[8][3], lo[3], hi[3], z;
+        for (int a = 0; a < 3; ++a) {
+            const double p = 1e-5 * (std::fabs((double)ob.a[a]) + std::fabs((double)ob.b[a]) + std::fabs(o[a]));
+            lo[a] = std::min((double)ob.a[a], (double)ob.b[a]) - p;
+            hi[a] = std::max((double)ob.a[a], (double)ob.b[a]) + p;
+        }
+        box_corners(lo, hi, pts);
+        Rect R;
+        if (H.n_box > 16 || ob.has_speed || !rect_of(pts, 8, R, z)) R = all;
+        mark(R, bit);
+    }
+    mesh_bins = 0;
+    start.assign(nb + 1, 0);
+    faces.clear();
+    zmin.clear();
+    if (H.n_mesh != 1) return true;
+    const DObj& m = H.objs[H.n_plane + H.n_sphere + H.n_box];
+    std::vector<Rect> rects(m.tri_count);
+    // A hit point P = o + t d (|d| = 1 up to rounding) has depth (P - o).(-w) <= t, and a
+    // face's depth is smallest at a vertex: min vertex depth bounds every t on the face
+    // (lowered by 1e-4 relative, far beyond the rounding of d, of the reference's t and of
+    // the fp32 cast)
+    std::vector<double> fz(m.tri_count);
+    std::vector<int32_t> count(nb + 1, 0);
+    for (int32_t f = 0; f < m.tri_count; ++f) {
+        const DTri& T = H.tris[m.tri_begin + f];
+        double pts[3][3];
+        for (int a = 0; a < 3; ++a) { pts[0][a] = T.v0[a]; pts[1][a] = T.v1[a]; pts[2][a] = T.v2[a]; }
+        double zlo;
+        if (!rect_of(pts, 3, rects[f], zlo)) return true;  // mesh_bins stays 0: walk the BVH
+        for (int32_t by = rects[f].r0; by <= rects[f].r1; ++by)
+            for (int32_t bx = rects[f].c0; bx <= rects[f].c1; ++bx) ++count[(size_t)by * bins_x + bx];
+        fz[f] = zlo * (1.0 - 1e-4);
+    }
+    for (size_t bb = 0; bb < nb; ++bb) start[bb + 1] = start[bb] + count[bb];
+    faces.assign(start.back(), 0);
+    std::vector<int32_t> fill(start.begin(), start.end() - 1);
+    std::vector<int32_t> order(m.tri_count);
+    for (int32_t f = 0; f < m.tri_count; ++f) order[f] = f;
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a2, int32_t b2) { return fz[a2] < fz[b2]; });
+    for (int32_t f : order)  // nearest first within each bin
+        for (int32_t by = rects[f].r0; by <= rects[f].r1; ++by)
+            for (int32_t bx = rects[f].c0; bx <= rects[f].c1; ++bx) faces[fill[(size_t)by * bins_x + bx]++] = f;
+    zmin.resize(faces.size());
+    for (size_t q = 0; q < faces.size(); ++q) {
+        float z = (float)fz[faces[q]];
+        if ((double)z > fz[faces[q]]) z = std::nextafter(z, -INFINITY);  // round down
+        zmin[q] = z;
+    }
+    mesh_bins = 1;
+    return true;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ scene-specialized kernels
@@ -950,6 +1097,11 @@ struct rtx_scene {
     std::vector<DObj> h_objs;
     std::vector<DTri> h_tris;
     std::vector<DBound> h_bounds_abi;
+    HostScene h_bins;   // objs/tris and type counts, for the camera's primary-ray face bins
+    int32_t* d_bin_start = nullptr;
+    int32_t* d_bin_faces = nullptr;
+    float* d_bin_zmin = nullptr;
+    uint32_t* d_bin_mask = nullptr;
     void* d_bounds_cam = nullptr;   // for the camera's motion times
     void* d_bounds_abi = nullptr;   // for the time of the last rtx_intersect / rtx_occluded
     void* d_nodes = nullptr;
@@ -999,6 +1151,12 @@ int upload(void** dptr, const std::vector<T>& v) {
 
 void free_camera(rtx_scene* s) {
     for (float* p : {s->d_xs, s->d_ys, s->d_dof, s->d_aa, s->d_times, s->d_noise}) (void)hipFree(p);
+    for (int32_t* p : {s->d_bin_start, s->d_bin_faces}) (void)hipFree(p);
+    (void)hipFree(s->d_bin_zmin);
+    (void)hipFree(s->d_bin_mask);
+    s->d_bin_start = s->d_bin_faces = nullptr;
+    s->d_bin_zmin = nullptr;
+    s->d_bin_mask = nullptr;
     (void)hipFree(s->d_bounds_cam);
     s->d_bounds_cam = nullptr;
     (void)hipFree(s->d_kp);
@@ -1056,6 +1214,12 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
         s->uniform_hard = H.uniform_hard >= 0 ? H.uniform_hard : -1;
         for (size_t i = 0; i < H.lights.size() && i < 32; ++i)
             if (H.lights[i].type == LIGHT_DIRECTIONAL) s->light_dir_mask |= 1u << i;
+    }
+    {  // primary-ray bins (per camera, rtx_camera_set)
+        s->h_bins.objs = H.objs;
+        if (H.n_mesh == 1) s->h_bins.tris = H.tris;
+        s->h_bins.n_plane = H.n_plane; s->h_bins.n_sphere = H.n_sphere;
+        s->h_bins.n_box = H.n_box; s->h_bins.n_mesh = H.n_mesh;
     }
     if (!H.nodes.empty()) {
         s->h_nodes = H.nodes;
@@ -1123,6 +1287,33 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
         if ((rc = upload(&s->d_bounds_cam, compute_bounds(s->h_nodes, s->h_objs, s->h_tris, *mm.first, *mm.second))))
             return rc;
         k.S.bounds = (cptr<DBound>)s->d_bounds_cam;
+    }
+    {
+        std::vector<int32_t> bstart, bfaces;
+        std::vector<float> bz;
+        std::vector<uint32_t> bmask;
+        int32_t bins_x = 0, mesh_bins = 0;
+        const char* e = getenv("RTX_BINS");  // experiment: 0 = no primary-ray bins
+        if (!(e && e[0] == '0') && primary_bins(s->h_bins, c, bstart, bfaces, bz, bmask, bins_x, mesh_bins)) {
+            if (bfaces.empty()) { bfaces.push_back(0); bz.push_back(0.0f); }
+            auto upi = [&](int32_t** d, const std::vector<int32_t>& h) -> int {
+                RTX_HIP(hipMalloc((void**)d, sizeof(int32_t) * h.size()));
+                RTX_HIP(hipMemcpy(*d, h.data(), sizeof(int32_t) * h.size(), hipMemcpyHostToDevice));
+                return RTX_OK;
+            };
+            if ((rc = upi(&s->d_bin_start, bstart)) || (rc = upi(&s->d_bin_faces, bfaces))) return rc;
+            RTX_HIP(hipMalloc((void**)&s->d_bin_zmin, sizeof(float) * bz.size()));
+            RTX_HIP(hipMemcpy(s->d_bin_zmin, bz.data(), sizeof(float) * bz.size(), hipMemcpyHostToDevice));
+            RTX_HIP(hipMalloc((void**)&s->d_bin_mask, sizeof(uint32_t) * bmask.size()));
+            RTX_HIP(hipMemcpy(s->d_bin_mask, bmask.data(), sizeof(uint32_t) * bmask.size(), hipMemcpyHostToDevice));
+            k.S.bin_objmask = (cptr<uint32_t>)s->d_bin_mask;
+            k.S.mesh_bins = mesh_bins;
+            k.S.bin_start = (cptr<int32_t>)s->d_bin_start;
+            k.S.bin_faces = (cptr<int32_t>)s->d_bin_faces;
+            k.S.bin_zmin = (cptr<float>)s->d_bin_zmin;
+            k.S.bins_x = bins_x;
+            k.S.bins_on = 1;
+        }
     }
     k.xs = (cptr<float>)s->d_xs; k.ys = (cptr<float>)s->d_ys; k.dof_o = (cptr<float>)s->d_dof;
     k.aa_o = (cptr<float>)s->d_aa; k.times = (cptr<float>)s->d_times; k.noise = (cptr<float>)s->d_noise;

@@ -119,7 +119,7 @@ RTX_HD void put_channel(float* fb, int64_t i, float v) {
 // emulation runs the same body).
 template <bool MESH, bool SEC, bool X, bool COUNT, bool JIT>
 RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, int32_t cc, Tally& tl,
-                         const FrameStack& fs, const HStack& hs) {
+                         const FrameStack& fs, const HStack& hs, int32_t bin = -1) {
     const int64_t p = (int64_t)rr * P.ncols + cc;
     if (RTX_ABLATE == 14) {  // cost probe only: store a constant (launch + framebuffer write)
         put_channel(fb, 3 * p, 0.5f); put_channel(fb, 3 * p + 1, 0.25f); put_channel(fb, 3 * p + 2, 0.125f);
@@ -137,7 +137,7 @@ RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, 
             const f3 o = sample_origin<JIT>(P, cc, j, kd, ka);
 #pragma unroll 1
             for (int kt = 0; kt < RTX_NTIMES(P); ++kt)
-                colour = add(colour, cast_ray<MESH, SEC, X, COUNT>(P.S, o, ddir, P.times[kt], tl, fs, hs));
+                colour = add(colour, cast_ray<MESH, SEC, X, COUNT>(P.S, o, ddir, P.times[kt], tl, fs, hs, bin));
         }
     }
     colour = mk(sample_mean(P, colour.x), sample_mean(P, colour.y), sample_mean(P, colour.z));
@@ -170,6 +170,13 @@ struct Launch {
 // Image row (row 0 = top) of block row rr.
 __host__ __device__ inline int32_t image_row(const Launch& L, int32_t rr) {
     return L.gstride > 0 ? ((rr >> 3) * L.gstride + L.gphase) * 8 + (rr & 7) : L.row0 + rr;
+}
+
+// The primary-ray face bin of the 8x8 pixel tile whose top-left pixel is (image row,
+// strip column, a multiple of 8), or -1 when the camera has no bins or the tile straddles
+// two bin rows (row blocks that start off the 8-row grid).
+__host__ __device__ inline int32_t primary_bin(const SceneView& S, int32_t row, int32_t col) {
+    return S.bins_on && (row & 7) == 0 ? (row >> 3) * S.bins_x + (col >> 3) : -1;
 }
 
 // Occupancy request (waves per SIMD) by kernel variant: mesh kernels without secondary
@@ -261,8 +268,11 @@ __device__ __forceinline__ void render_body(const KParams* __restrict__ Pp, cons
         const PixelRC px = pixel_rc(ncols, sub);
         const bool active = px.r < L.nrows && px.c < ncols;
         any_active = any_active || active;
+        // primary-ray face bin of the wave's 8x8 tile (its top-left pixel)
+        const int32_t bin = RTX_TILE == 1 ? primary_bin(Pp->S, image_row(L, px.r & ~7), px.c & ~7) : -1;
         // render_pixel's image row is row0 + rr: pass the image row of px.r as that sum
-        if (active) render_pixel<MESH, SEC, X, COUNT, JIT>(*Pp, L.fb, image_row(L, px.r) - px.r, px.r, px.c, tl, fs, hs);
+        if (active)
+            render_pixel<MESH, SEC, X, COUNT, JIT>(*Pp, L.fb, image_row(L, px.r) - px.r, px.r, px.c, tl, fs, hs, bin);
     }
     flush_tally<COUNT>(tl, L.counters, any_active);
 }

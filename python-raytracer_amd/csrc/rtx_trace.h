@@ -225,6 +225,14 @@ struct SceneView {
     cptr<DBound> bounds;             // per node, for the current motion-time range
     int32_t n_nodes, hlevels;        // hlevels: stack levels the hierarchies need
     int32_t n_tris, n_leaves;        // all triangles / mesh BVH nodes
+    // Primary-ray face bins of the camera (rtx_api.hip primary_bins): for each 8x8 pixel
+    // bin, the faces of the scene's one mesh that a primary ray of a tile whose top-left
+    // pixel lies in the bin may hit (conservative). bins_on = 0: walk the BVH.
+    cptr<int32_t> bin_start;         // [bins + 1]
+    cptr<int32_t> bin_faces;         // stored face indices (within the mesh), nearest first
+    cptr<float> bin_zmin;            // per entry: a lower bound of any hit t on that face
+    cptr<uint32_t> bin_objmask;      // per bin: spheres (bits 0-15) and boxes (16-31) a ray may hit
+    int32_t bins_x, bins_on, mesh_bins, pad5;
 };
 
 // Mesh records read by the hot BVH walks (closest_hit / occluded). Scene-specialized
@@ -334,6 +342,15 @@ constexpr float kEps3Near = 1e-3f;             // fl32(1e-3)
 #define RTX_ANY(p) ((bool)(p))
 #define RTX_ALL(p) ((bool)(p))
 #endif
+
+// A value every active lane holds, as a wave-uniform (scalar) value.
+RTX_HD int32_t wave_uniform(int32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_readfirstlane(x);
+#else
+    return x;
+#endif
+}
 
 // Closest-hit record: t as its fp32 proxy, the object (index into the type-grouped
 // array, -1 = none) and a sub-index (sphere: root; box: entry slab label; mesh: face).
@@ -1244,7 +1261,8 @@ RTX_HY void hier_closest(const SceneView& S, const HStack& hs, f3 o, f3 d, float
 
 // ------------------------------------------------------------------ closest hit
 template <bool MESH, bool X, bool COUNT>
-RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const HStack& hs, HHit& hh) {
+RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const HStack& hs, HHit& hh,
+                       int32_t bin = -1) {
     Hit h{INFINITY, -1, 0};
     int oi = 0;
     for (int k = 0; k < RTX_NPLANE(S); ++k, ++oi) {  // simple_geometry.py:105-120
@@ -1257,7 +1275,11 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
         const bool valid = fabsf(denom) >= kEps4Up && quot_nonneg(t32, num, denom);
         offer(S, h, valid, t32, oi, 0, o, d, time);
     }
+    // primary rays of a binned tile skip the spheres and boxes whose screen footprint
+    // misses the tile (rtx_api.hip primary_bins; wave-uniform)
+    const uint32_t omask = bin >= 0 ? S.bin_objmask[wave_uniform(bin)] : ~0u;
     for (int k = 0; k < RTX_NSPHERE(S); ++k, ++oi) {  // simple_geometry.py:20-46
+        if (!((omask >> (k & 15)) & 1u)) continue;
         if (RTX_ABLATE == 7) continue;  // cost probe: no spheres in the primary test
         const DObj ob = S.objs[oi];
         const f3 ctr = moved(ob, ob.a, time);
@@ -1278,6 +1300,7 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
     RayInv ri{};
     if (RTX_NBOX(S) > 0 || (MESH && RTX_NMESH(S) > 0)) ri = ray_inv(o, d);
     for (int k = 0; k < RTX_NBOX(S); ++k, ++oi) {  // simple_geometry.py:188-249 (entry precedes exit)
+        if (!((omask >> (16 + (k & 15))) & 1u)) continue;
         const DObj ob = S.objs[oi];
         const f3 mn = moved(ob, ob.a, time), mx = moved(ob, ob.b, time);
         // the fp64 slabs only where some lane's ray may hit the box before its best t
@@ -1295,33 +1318,46 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
             // test only where some lane's ray may enter the box before its best t
             if (!RTX_ANY(bv_maybe(ob, o, ri, h.t32))) continue;
             if (!mesh_bv(ob, o, d)) continue;  // the reference's bounding volume, quirks included
+            // mesh.py:77-117 for stored face f (lanes with maybe set may take it)
+            auto test_face = [&](int f, bool maybe, bool cull) {
+                bool fmaybe = maybe;
+                if (cull) {  // the face's own padded box (the cluster's bound)
+                    fmaybe = maybe && leaf_maybe_hit(RTX_FBOX(S, ob.tri_begin + f), o, ri, ob.cmax, h.t32);
+                    if (!RTX_ANY(fmaybe)) return;  // no lane's ray can pass its exact test
+                }
+                const DTri T = RTX_TRI(S, ob.tri_begin + f);
+                tally_inc<COUNT>(tl, &Tally::tri);
+                const f3 n = ld3(T.n);
+                const float denom = dot(d, n);
+                const f3 v0 = ld3(T.v0);
+                const float num = dot(sub(v0, o), n);
+                const float t32 = num / denom;
+                // abs(denom) < epsilon -> skip; time < 0 -> skip
+                bool valid = fmaybe && !(fabsf(denom) < kEps4Up) && !quot_neg(t32, num, denom);
+                const f3 p = add(o, scale(d, t32));  // getPoint(time)
+                const float b0 = dot(cross(ld3(T.e01), sub(p, v0)), n);
+                const float b1 = dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n);
+                const float b2 = dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n);
+                valid = valid && b0 >= 0.0f && b1 >= 0.0f && b2 >= 0.0f;
+                offer(S, h, valid, t32, oi, f, o, d, time);
+            };
+            if (bin >= 0 && S.mesh_bins && k == 0) {  // a primary ray: its tile's candidate faces
+                const int32_t ub = wave_uniform(bin);  // the same in every lane of the tile's wave
+                const int32_t q1 = S.bin_start[ub + 1];
+                for (int32_t q = S.bin_start[ub]; q < q1; ++q) {
+                    // faces come nearest first: once every lane's best hit precedes a
+                    // face's nearest possible t, no later face can win (or tie)
+                    if (RTX_ALL(h.t32 < S.bin_zmin[q])) break;
+                    test_face(S.bin_faces[q], true, true);
+                }
+                continue;
+            }
             for (int li = 0; li < ob.leaf_count;) {  // stackless wave-uniform BVH walk
                 const auto& L = RTX_LEAF(S, ob.leaf_begin + li);
                 const bool maybe = leaf_maybe_hit(L, o, ri, ob.cmax, h.t32);
                 if (!RTX_ANY(maybe)) { li = L.skip; continue; }
                 ++li;
-                for (int f = L.first; f < L.first + L.count; ++f) {
-                    bool fmaybe = maybe;
-                    if (face_cull(ob)) {  // the face's own padded box (the cluster's bound)
-                        fmaybe = maybe && leaf_maybe_hit(RTX_FBOX(S, ob.tri_begin + f), o, ri, ob.cmax, h.t32);
-                        if (!RTX_ANY(fmaybe)) continue;  // no lane's ray can pass its exact test
-                    }
-                    const DTri T = RTX_TRI(S, ob.tri_begin + f);
-                    tally_inc<COUNT>(tl, &Tally::tri);
-                    const f3 n = ld3(T.n);
-                    const float denom = dot(d, n);
-                    const f3 v0 = ld3(T.v0);
-                    const float num = dot(sub(v0, o), n);
-                    const float t32 = num / denom;
-                    // abs(denom) < epsilon -> skip; time < 0 -> skip
-                    bool valid = fmaybe && !(fabsf(denom) < kEps4Up) && !quot_neg(t32, num, denom);
-                    const f3 p = add(o, scale(d, t32));  // getPoint(time)
-                    const float b0 = dot(cross(ld3(T.e01), sub(p, v0)), n);
-                    const float b1 = dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n);
-                    const float b2 = dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n);
-                    valid = valid && b0 >= 0.0f && b1 >= 0.0f && b2 >= 0.0f;
-                    offer(S, h, valid, t32, oi, f, o, d, time);
-                }
+                for (int f = L.first; f < L.first + L.count; ++f) test_face(f, maybe, face_cull(ob));
             }
         }
     }
@@ -1613,7 +1649,8 @@ struct FrameStack {
 };
 
 template <bool MESH, bool SEC, bool X, bool COUNT>
-RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const FrameStack& fs, const HStack& hs) {
+RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const FrameStack& fs, const HStack& hs,
+                   int32_t bin = -1) {
     int nfr = 0;
     f3 tail = mk(0.0f, 0.0f, 0.0f);
     bool in_shape = false;
@@ -1621,7 +1658,7 @@ RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const 
         if (COUNT) tl.cast[level]++;
         if (RTX_ABLATE == 8) { tail = d; break; }  // cost probe: camera + store only
         HHit hh;
-        const Hit h = closest_hit<MESH, X, COUNT>(S, o, d, time, tl, hs, hh);
+        const Hit h = closest_hit<MESH, X, COUNT>(S, o, d, time, tl, hs, hh, level == 0 ? bin : -1);
         if (h.obj == -1) break;  // miss -> black
         const Surface sf = resolve_hit<MESH, X>(S, h, hh, o, d, time);
         const DMat m = S.mats[sf.mat];

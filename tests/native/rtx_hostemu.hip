@@ -38,22 +38,25 @@ void bind_view(const HostScene& H, SceneView& v) {
 // Dispatch over the kernel template flags, as rtx_render's launch switch does.
 template <bool MESH, bool SEC, bool X>
 void pixel_jit(const KParams& k, float* fb, int32_t row0, int32_t rr, int32_t cc, Tally& tl, const FrameStack& fs,
-               const HStack& hs, bool jit) {
-    if (jit) render_pixel<MESH, SEC, X, true, true>(k, fb, row0, rr, cc, tl, fs, hs);
-    else render_pixel<MESH, SEC, X, true, false>(k, fb, row0, rr, cc, tl, fs, hs);
+               const HStack& hs, bool jit, int32_t bin) {
+    if (jit) render_pixel<MESH, SEC, X, true, true>(k, fb, row0, rr, cc, tl, fs, hs, bin);
+    else render_pixel<MESH, SEC, X, true, false>(k, fb, row0, rr, cc, tl, fs, hs, bin);
 }
 void pixel_any(const HostScene& H, const KParams& k, float* fb, int32_t row0, int32_t rr, int32_t cc, Tally& tl,
-               const FrameStack& fs, const HStack& hs, bool jit) {
+               const FrameStack& fs, const HStack& hs, bool jit, int32_t tile_row) {
+    // the face bin of the pixel's 8x8 tile, as render_body picks it (image row of the
+    // tile's first row, strip column of its first column)
+    const int32_t bin = primary_bin(k.S, tile_row, cc & ~7);
     const int sel = (H.has_mesh ? 4 : 0) | (H.has_secondary ? 2 : 0) | (H.has_ext ? 1 : 0);
     switch (sel) {
-        case 0: pixel_jit<false, false, false>(k, fb, row0, rr, cc, tl, fs, hs, jit); break;
-        case 1: pixel_jit<false, false, true>(k, fb, row0, rr, cc, tl, fs, hs, jit); break;
-        case 2: pixel_jit<false, true, false>(k, fb, row0, rr, cc, tl, fs, hs, jit); break;
-        case 3: pixel_jit<false, true, true>(k, fb, row0, rr, cc, tl, fs, hs, jit); break;
-        case 4: pixel_jit<true, false, false>(k, fb, row0, rr, cc, tl, fs, hs, jit); break;
-        case 5: pixel_jit<true, false, true>(k, fb, row0, rr, cc, tl, fs, hs, jit); break;
-        case 6: pixel_jit<true, true, false>(k, fb, row0, rr, cc, tl, fs, hs, jit); break;
-        case 7: pixel_jit<true, true, true>(k, fb, row0, rr, cc, tl, fs, hs, jit); break;
+        case 0: pixel_jit<false, false, false>(k, fb, row0, rr, cc, tl, fs, hs, jit, bin); break;
+        case 1: pixel_jit<false, false, true>(k, fb, row0, rr, cc, tl, fs, hs, jit, bin); break;
+        case 2: pixel_jit<false, true, false>(k, fb, row0, rr, cc, tl, fs, hs, jit, bin); break;
+        case 3: pixel_jit<false, true, true>(k, fb, row0, rr, cc, tl, fs, hs, jit, bin); break;
+        case 4: pixel_jit<true, false, false>(k, fb, row0, rr, cc, tl, fs, hs, jit, bin); break;
+        case 5: pixel_jit<true, false, true>(k, fb, row0, rr, cc, tl, fs, hs, jit, bin); break;
+        case 6: pixel_jit<true, true, false>(k, fb, row0, rr, cc, tl, fs, hs, jit, bin); break;
+        case 7: pixel_jit<true, true, true>(k, fb, row0, rr, cc, tl, fs, hs, jit, bin); break;
     }
 }
 }  // namespace
@@ -72,6 +75,21 @@ extern "C" int rtx_hostemu_render(const rtx_scene_desc* sd, const rtx_camera_des
     const auto mm = std::minmax_element(times.begin(), times.end());
     const std::vector<DBound> bounds = compute_bounds(H.nodes, H.objs, H.tris, *mm.first, *mm.second);
     k.S.bounds = (cptr<DBound>)bounds.data();
+    std::vector<int32_t> bstart, bfaces;
+    std::vector<float> bz;
+    std::vector<uint32_t> bmask;
+    int32_t bins_x = 0, mesh_bins = 0;
+    const char* be = getenv("RTX_BINS");
+    if (!(be && be[0] == '0') && primary_bins(H, cd, bstart, bfaces, bz, bmask, bins_x, mesh_bins)) {
+        if (bfaces.empty()) { bfaces.push_back(0); bz.push_back(0.0f); }
+        k.S.bin_start = (cptr<int32_t>)bstart.data();
+        k.S.bin_faces = (cptr<int32_t>)bfaces.data();
+        k.S.bin_zmin = (cptr<float>)bz.data();
+        k.S.bin_objmask = (cptr<uint32_t>)bmask.data();
+        k.S.mesh_bins = mesh_bins;
+        k.S.bins_x = bins_x;
+        k.S.bins_on = 1;
+    }
     std::vector<float> noise;
     const size_t nsamp = (size_t)cd->n_dof * cd->n_aa;
     if (cd->jitter == RTX_JITTER_REPLAY) noise.assign(cd->noise, cd->noise + 3 * (size_t)cd->ncols * cd->height * nsamp);
@@ -90,7 +108,7 @@ extern "C" int rtx_hostemu_render(const rtx_scene_desc* sd, const rtx_camera_des
             const FrameStack fs{frames, 1};
             const HStack hs{hst, 1};
             const int32_t rr = (int32_t)(p / k.ncols), cc = (int32_t)(p % k.ncols);
-            pixel_any(H, k, fb, row0, rr, cc, tl, fs, hs, k.jitter != RTX_JITTER_OFF);
+            pixel_any(H, k, fb, row0, rr, cc, tl, fs, hs, k.jitter != RTX_JITTER_OFF, row0 + (rr & ~7));
             for (int q = 0; q < kMaxDepth; ++q) loc[q] += tl.cast[q];
             loc[RTX_CNT_SHADOW] += tl.shadow;
             loc[RTX_CNT_SHADE] += tl.shade;
@@ -121,6 +139,21 @@ extern "C" int rtx_hostemu_render_rows(const rtx_scene_desc* sd, const rtx_camer
     const auto mm = std::minmax_element(times.begin(), times.end());
     const std::vector<DBound> bounds = compute_bounds(H.nodes, H.objs, H.tris, *mm.first, *mm.second);
     k.S.bounds = (cptr<DBound>)bounds.data();
+    std::vector<int32_t> bstart, bfaces;
+    std::vector<float> bz;
+    std::vector<uint32_t> bmask;
+    int32_t bins_x = 0, mesh_bins = 0;
+    const char* be = getenv("RTX_BINS");
+    if (!(be && be[0] == '0') && primary_bins(H, cd, bstart, bfaces, bz, bmask, bins_x, mesh_bins)) {
+        if (bfaces.empty()) { bfaces.push_back(0); bz.push_back(0.0f); }
+        k.S.bin_start = (cptr<int32_t>)bstart.data();
+        k.S.bin_faces = (cptr<int32_t>)bfaces.data();
+        k.S.bin_zmin = (cptr<float>)bz.data();
+        k.S.bin_objmask = (cptr<uint32_t>)bmask.data();
+        k.S.mesh_bins = mesh_bins;
+        k.S.bins_x = bins_x;
+        k.S.bins_on = 1;
+    }
     std::vector<float> noise;
     const size_t nsamp = (size_t)cd->n_dof * cd->n_aa;
     if (cd->jitter == RTX_JITTER_REPLAY) noise.assign(cd->noise, cd->noise + 3 * (size_t)cd->ncols * cd->height * nsamp);
@@ -136,7 +169,7 @@ extern "C" int rtx_hostemu_render_rows(const rtx_scene_desc* sd, const rtx_camer
         const HStack hs{hst, 1};
         const int32_t rr = (int32_t)(p / k.ncols), cc = (int32_t)(p % k.ncols);
         // render_pixel's image row is row0 + rr
-        pixel_any(H, k, fb, rows[rr] - rr, rr, cc, tl, fs, hs, k.jitter != RTX_JITTER_OFF);
+        pixel_any(H, k, fb, rows[rr] - rr, rr, cc, tl, fs, hs, k.jitter != RTX_JITTER_OFF, rows[rr & ~7]);
     }
     return RTX_OK;
 }
