@@ -273,3 +273,55 @@ def obj_bounds(path):
     and no translation (mesh.py:31-36)."""
     v = np.array([[float(x) for x in l.split()[1:4]] for l in open(path) if l.startswith("v ")], np.float32)
     return v.min(axis=0), v.max(axis=0)
+
+
+def bins_scene(seed, res=(41, 23)):
+    """Scenes that stress the primary-ray bins (rtx_api.hip primary_bins): one sample per
+    pixel, no lens or jitter (so bins apply), wide and narrow fields of view, spheres and
+    boxes around, beside, behind and enclosing the camera, tiny far spheres (the fp32
+    discriminant's fuzz), moving objects, and sometimes the torus mesh up close."""
+    rng = np.random.RandomState(1000 + seed)
+    r = lambda lo, hi, n=None: np.round(rng.uniform(lo, hi, n), 3).tolist()  # noqa: E731
+    mats = [{"name": "m%d" % i, "ID": i, "diffuse": r(0, 1, 3), "specular": r(0, 1, 3), "hardness": 16,
+             "type": "mirror" if i == 3 else "diffuse", "tint": 0.3} for i in range(4)]
+    cam = np.array([r(-2, 2), r(0.5, 3), r(3, 8)])
+    look = np.array([r(-1, 1), r(0, 1), r(-1, 1)])
+    objs = [{"name": "ground", "type": "plane", "normal": [0.0, 1.0, 0.0], "position": [0.0, -1.0, 0.0],
+             "materials": [0, 1]}]
+    fwd = (look - cam) / np.linalg.norm(look - cam)
+    for k in range(rng.randint(2, 7)):
+        kind = rng.randint(5)
+        if kind == 0:    # beside / behind the camera
+            c = cam + rng.uniform(-3, 3, 3) - fwd * rng.uniform(0, 2)
+            rad = float(r(0.2, 1.0))
+        elif kind == 1:  # tiny and far
+            c = cam + fwd * rng.uniform(30, 80) + rng.uniform(-5, 5, 3)
+            rad = float(r(0.01, 0.2))
+        elif kind == 2:  # enclosing the camera
+            c = cam + rng.uniform(-0.2, 0.2, 3)
+            rad = float(r(1.0, 2.0))
+        else:            # in view
+            c = look + rng.uniform(-2, 2, 3)
+            rad = float(r(0.2, 1.2))
+        o = {"name": "s%d" % k, "type": "sphere", "radius": rad, "position": np.round(c, 3).tolist(),
+             "materials": [int(rng.randint(4))]}
+        if rng.rand() < 0.2:
+            o["speed"] = r(-0.5, 0.5, 3)
+        objs.append(o)
+    for k in range(rng.randint(0, 3)):
+        c = (cam if rng.rand() < 0.3 else look) + rng.uniform(-2, 2, 3)
+        objs.append({"name": "b%d" % k, "type": "box", "position": np.round(c, 3).tolist(), "size": r(0.2, 1.5, 3),
+                     "materials": [int(rng.randint(4))]})
+    if rng.rand() < 0.5:
+        objs.append({"name": "torus", "type": "mesh", "filepath": "torus_mesh.obj", "scale": float(r(0.4, 1.2)),
+                     "position": np.round(look + rng.uniform(-1, 1, 3), 3).tolist(), "materials": [2],
+                     "flat_shaded": bool(rng.rand() < 0.5)})
+    sc = {"resolution": list(res), "AA": {"jitter": False, "samples": 1}, "ambient": [0.1, 0.1, 0.1],
+          "camera": {"position": np.round(cam, 3).tolist(), "lookAt": np.round(look, 3).tolist(),
+                     "up": [0.0, 1.0, 0.0], "fov": float(rng.choice([15.0, 45.0, 90.0, 120.0]))},
+          "materials": mats, "objects": objs,
+          "lights": [{"name": "p", "type": "point", "position": [2.0, 6.0, 3.0], "colour": [1.0, 1.0, 1.0],
+                      "power": 1.0}]}
+    if rng.rand() < 0.3:
+        sc["motion"] = {"time": 1.0, "samples": 2, "final": 1}
+    return sc

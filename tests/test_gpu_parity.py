@@ -454,3 +454,28 @@ def test_rgb8_conversion_unaligned_and_tails():
                C.c_void_p(torch.cuda.current_stream().cuda_stream))
         want = (fb.cpu().numpy().astype(np.float64) * 255.0).astype(np.uint8)
         assert np.array_equal(out.cpu().numpy(), want), (off, n)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_primary_bins_equal_walk(seed, monkeypatch):
+    """Primary-ray bins (a tile's primary rays test only the objects / faces its bin lists)
+    change no pixel: binned == full walk == oracle, whole frames, 8-row groups and row
+    blocks that start off the 8-row grid (which walk everything)."""
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import bins_scene
+    d = bins_scene(seed, res=(97, 61))
+    on = product_scene_dict(d)
+    a = on.render_device().clone()
+    monkeypatch.setenv("RTX_BINS", "0")
+    off = product_scene_dict(d)  # RTX_BINS is read when the camera is uploaded
+    b = off.render_device().clone()
+    monkeypatch.delenv("RTX_BINS")
+    assert torch.equal(a, b)
+    img = np.ascontiguousarray(np.transpose(a.cpu().numpy()[::-1], (1, 0, 2))).astype(np.float64)
+    assert_parity(img, oracle_render_dict(d), "bins seed %d" % seed)
+    from rtx.scene import group_rows
+    for n in (3,):
+        for k in range(n):
+            rows = torch.as_tensor(group_rows(61, n, k), device="cuda")
+            assert torch.equal(on.render_device(groups=(k, n)), a[rows])
+    assert torch.equal(on.render_device(row0=13, nrows=30), a[13:43])

@@ -227,3 +227,22 @@ def test_hostemu_large_mesh_kat(blob5):
     assert np.array_equal(got["normal"][hit], nn[hit]) and np.array_equal(got["position"][hit], pp[hit])
     for tmax in (1.0, np.inf):
         assert np.array_equal(hostemu.occluded(sc, o, dd, tmax, 0.0), osc.shadow(0.0, o, dd, tmax).astype(bool))
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_hostemu_primary_bins_equal_walk(seed, monkeypatch):
+    """The primary-ray bins (objects and faces a tile's primary rays may hit) change no
+    pixel: binned == full walk == oracle, for whole frames and column strips."""
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import bins_scene
+    d = bins_scene(seed)
+    sc = product_scene_dict(d)
+    img, _ = hostemu.render(sc)
+    monkeypatch.setenv("RTX_BINS", "0")
+    walk, _ = hostemu.render(sc)
+    assert np.array_equal(img, walk)
+    monkeypatch.delenv("RTX_BINS")
+    assert_parity(img, oracle_render_dict(d), "bins seed %d" % seed)
+    for k in range(3):
+        strip, _ = hostemu.render(sc, k, 3)
+        assert np.array_equal(strip, oracle_render_dict(d, k, 3)), k
