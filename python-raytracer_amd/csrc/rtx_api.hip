@@ -988,6 +988,7 @@ hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& k
                                      "-DRTX_FIXED_DIVPOW2=" + std::to_string(kp.div_pow2)};
     if (uniform_hard >= 0) opts.push_back("-DRTX_FIXED_HARD=" + std::to_string(uniform_hard));
     if (out8) opts.push_back("-DRTX_OUT8=1");  // uint8 framebuffer (rtx_render_rgb8)
+    opts.push_back(std::string("-DRTX_PRIMARY_BINS=") + (kp.S.bins_on ? "1" : "0"));
     if (mesh && !spp && v.n_mesh > 0) {  // experiment: the meshes' hot records in LDS (RTX_MESH_LDS=1)
         const char* e = getenv("RTX_MESH_LDS");
         const size_t bytes = (size_t)v.n_tris * (sizeof(DTri) + sizeof(DFaceBox)) + (size_t)v.n_leaves * sizeof(DLeaf);

@@ -175,8 +175,13 @@ __host__ __device__ inline int32_t image_row(const Launch& L, int32_t rr) {
 // The primary-ray face bin of the 8x8 pixel tile whose top-left pixel is (image row,
 // strip column, a multiple of 8), or -1 when the camera has no bins or the tile straddles
 // two bin rows (row blocks that start off the 8-row grid).
+// Scene-specialized kernels of cameras without bins are compiled with RTX_PRIMARY_BINS=0
+// (the bin code vanishes); the precompiled kernels check bins_on at run time.
+#ifndef RTX_PRIMARY_BINS
+#define RTX_PRIMARY_BINS 1
+#endif
 __host__ __device__ inline int32_t primary_bin(const SceneView& S, int32_t row, int32_t col) {
-    return S.bins_on && (row & 7) == 0 ? (row >> 3) * S.bins_x + (col >> 3) : -1;
+    return RTX_PRIMARY_BINS && S.bins_on && (row & 7) == 0 ? (row >> 3) * S.bins_x + (col >> 3) : -1;
 }
 
 // Occupancy request (waves per SIMD) by kernel variant: mesh kernels without secondary

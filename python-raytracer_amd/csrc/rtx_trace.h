@@ -1277,7 +1277,11 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
     }
     // primary rays of a binned tile skip the spheres and boxes whose screen footprint
     // misses the tile (rtx_api.hip primary_bins; wave-uniform)
+#if defined(RTX_PRIMARY_BINS) && !RTX_PRIMARY_BINS
+    constexpr uint32_t omask = ~0u;
+#else
     const uint32_t omask = bin >= 0 ? S.bin_objmask[wave_uniform(bin)] : ~0u;
+#endif
     for (int k = 0; k < RTX_NSPHERE(S); ++k, ++oi) {  // simple_geometry.py:20-46
         if (!((omask >> (k & 15)) & 1u)) continue;
         if (RTX_ABLATE == 7) continue;  // cost probe: no spheres in the primary test
