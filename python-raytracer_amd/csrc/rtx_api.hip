@@ -989,6 +989,14 @@ hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& k
     if (uniform_hard >= 0) opts.push_back("-DRTX_FIXED_HARD=" + std::to_string(uniform_hard));
     if (out8) opts.push_back("-DRTX_OUT8=1");  // uint8 framebuffer (rtx_render_rgb8)
     opts.push_back(std::string("-DRTX_PRIMARY_BINS=") + (kp.S.bins_on ? "1" : "0"));
+    if (!ext && !spp) {  // experiment: per-lane object / material gathers from LDS (RTX_LDS_RECORDS=1)
+        const char* e = getenv("RTX_LDS_RECORDS");
+        const size_t bytes = (size_t)v.n_objs_all * sizeof(DObj) + (size_t)v.n_mats * sizeof(DMat);
+        if (e && e[0] == '1' && v.n_objs_all > 0 && v.n_mats > 0 && bytes <= 16 * 1024) {
+            opts.push_back("-DRTX_LDS_OBJS=" + std::to_string(v.n_objs_all));
+            opts.push_back("-DRTX_LDS_MATS=" + std::to_string(v.n_mats));
+        }
+    }
     if (mesh && !spp && v.n_mesh > 0) {  // experiment: the meshes' hot records in LDS (RTX_MESH_LDS=1)
         const char* e = getenv("RTX_MESH_LDS");
         const size_t bytes = (size_t)v.n_tris * (sizeof(DTri) + sizeof(DFaceBox)) + (size_t)v.n_leaves * sizeof(DLeaf);
@@ -1241,6 +1249,8 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
     v.leaves = (cptr<DLeaf>)s->d_leaves;
     v.tri_orig = (cptr<int32_t>)s->d_tri_orig;
     v.n_objs = H.n_objs;
+    v.n_objs_all = (int32_t)H.objs.size();
+    v.n_mats = (int32_t)H.mats.size();
     v.n_lights = H.n_lights;
     v.n_plane = H.n_plane; v.n_sphere = H.n_sphere; v.n_box = H.n_box; v.n_mesh = H.n_mesh;
     v.pow_bits = H.pow_bits;

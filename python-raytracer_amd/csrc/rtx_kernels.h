@@ -257,10 +257,27 @@ __device__ __forceinline__ void stage_mesh_lds(const SceneView& S) {
 #endif
 }
 
+// RTX_LDS_OBJS kernels: the block copies the object and material records into LDS.
+__device__ __forceinline__ void stage_records_lds(const SceneView& S) {
+#if defined(RTX_LDS_OBJS) && defined(__HIP_DEVICE_COMPILE__)
+    auto copy = [](void* dst, const void RTX_CONST* src, int words) {
+        uint4* d = static_cast<uint4*>(dst);
+        const uint4 RTX_CONST* s = static_cast<const uint4 RTX_CONST*>(src);
+        for (int i = threadIdx.x; i < words; i += blockDim.x) d[i] = s[i];
+    };
+    copy(g_lds_objs, S.objs, RTX_LDS_OBJS * (int)(sizeof(DObj) / 16));
+    copy(g_lds_mats, S.mats, RTX_LDS_MATS * (int)(sizeof(DMat) / 16));
+    __syncthreads();
+#else
+    (void)S;
+#endif
+}
+
 template <bool MESH, bool SEC, bool X, bool COUNT, bool JIT>
 __device__ __forceinline__ void render_body(const KParams* __restrict__ Pp, const Launch L) {
     constexpr int B = kBlock<X>;
     if (MESH) stage_mesh_lds(Pp->S);
+    stage_records_lds(Pp->S);
     const int32_t ncols = Pp->ncols;
     Tally tl = {};
     // secondary-ray frames: [frame][word][thread] in LDS (40 KB per 256-thread block)

@@ -233,6 +233,7 @@ struct SceneView {
     cptr<float> bin_zmin;            // per entry: a lower bound of any hit t on that face
     cptr<uint32_t> bin_objmask;      // per bin: spheres (bits 0-15) and boxes (16-31) a ray may hit
     int32_t bins_x, bins_on, mesh_bins, pad5;
+    int32_t n_objs_all, n_mats, pad6, pad7;  // object records (incl. hierarchy leaves), materials
 };
 
 // Mesh records read by the hot BVH walks (closest_hit / occluded). Scene-specialized
@@ -250,6 +251,21 @@ __shared__ DLeaf g_lds_leaves[RTX_LDS_LEAVES];
 #define RTX_TRI(S, i) ((S).tris[i])
 #define RTX_FBOX(S, i) ((S).fboxes[i])
 #define RTX_LEAF(S, i) ((S).leaves[i])
+#endif
+
+// Object and material records fetched with a per-lane index (the hit object of each lane,
+// its material): scene-specialized kernels built with RTX_LDS_OBJS / RTX_LDS_MATS (the
+// scene's record counts) copy both tables into LDS once per block (render_body), so these
+// gathers are LDS reads instead of L2 round trips on the shading path. Loops over objects
+// with a wave-uniform index keep their scalar loads.
+#if defined(RTX_LDS_OBJS) && defined(__HIP_DEVICE_COMPILE__)
+__shared__ DObj g_lds_objs[RTX_LDS_OBJS];
+__shared__ DMat g_lds_mats[RTX_LDS_MATS];
+#define RTX_OBJ(S, i) (g_lds_objs[i])
+#define RTX_MAT(S, i) (g_lds_mats[i])
+#else
+#define RTX_OBJ(S, i) ((S).objs[i])
+#define RTX_MAT(S, i) ((S).mats[i])
 #endif
 
 // ------------------------------------------------------------------ counters
@@ -1518,7 +1534,7 @@ RTX_HD Surface resolve_hit(const SceneView& S, const Hit& h, const HHit& hh, f3 
         sf.gobj = hh.gobj;
         return sf;
     }
-    const DObj ob = S.objs[h.obj];
+    const DObj ob = RTX_OBJ(S, h.obj);
     sf.gobj = (X && ob.has_tex) ? h.obj : -1;
     sf.position = add(o, scale(d, h.t32));  // getPoint(t): fl32(t64) == t32
     sf.mat = ob.mat0;
@@ -1665,7 +1681,7 @@ RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const 
         const Hit h = closest_hit<MESH, X, COUNT>(S, o, d, time, tl, hs, hh, level == 0 ? bin : -1);
         if (h.obj == -1) break;  // miss -> black
         const Surface sf = resolve_hit<MESH, X>(S, h, hh, o, d, time);
-        const DMat m = S.mats[sf.mat];
+        const DMat m = RTX_MAT(S, sf.mat);
         f3 n = sf.normal;
         bool chain = false, tir = false;
         f3 next_o = o, next_d = d;
@@ -1702,7 +1718,7 @@ RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const 
         for (int k = nfr - 1; k >= 0; --k) {
             int32_t mi;
             const f3 L = fs.get(k, mi);
-            const DMat m = S.mats[mi];
+            const DMat m = RTX_MAT(S, mi);
             tail = clamp01(add(scale(L, m.tint), scale(tail, m.omt)));
         }
     }
