@@ -230,7 +230,10 @@ __host__ __device__ inline int64_t launch_items(int32_t nrows, int32_t ncols) {
 
 // Block size: 256 threads, or one wave for the hierarchy/texture (X) variants, whose
 // per-thread ray/point stacks (9 words per hierarchy level) share the CU's LDS.
-// 64 and 128 measured equal to 256 within noise (tools/ablate.sh, s21)
+// 64 and 128 measured equal to 256 within noise with matching JIT kernels (library and
+// hiprtc kernels both built with the value; tools/ab_block.sh, profiles/r02/blk: TSP
+// 28.7/29.1/29.0 us, TM 83.0/82.1/81.9, MR 51.6/52.8/52.2, DOF 7.23/7.21/7.28 ms for
+// 256/64/128)
 #ifndef RTX_BLOCK_FLAT  // threads per block of the flat-scene kernels (experiments)
 #define RTX_BLOCK_FLAT 256
 #endif
