@@ -1276,6 +1276,115 @@ RTX_HY void hier_closest(const SceneView& S, const HStack& hs, f3 o, f3 d, float
 #endif
 
 // ------------------------------------------------------------------ closest hit
+// Mesh.intersect's test of one face (mesh.py:77-117): t32 and whether the hit counts
+// (lanes with maybe unset never do).
+RTX_HD bool tri_hit(const DTri T, f3 o, f3 d, bool maybe, float& t32) {
+    const f3 n = ld3(T.n);
+    const float denom = dot(d, n);
+    const f3 v0 = ld3(T.v0);
+    const float num = dot(sub(v0, o), n);
+    t32 = num / denom;
+    // abs(denom) < epsilon -> skip; time < 0 -> skip
+    bool valid = maybe && !(fabsf(denom) < kEps4Up) && !quot_neg(t32, num, denom);
+    const f3 p = add(o, scale(d, t32));  // getPoint(time)
+    const float b0 = dot(cross(ld3(T.e01), sub(p, v0)), n);
+    const float b1 = dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n);
+    const float b2 = dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n);
+    return valid && b0 >= 0.0f && b1 >= 0.0f && b2 >= 0.0f;
+}
+
+// Wave-cooperative closest hit on a large mesh (experiment, -DRTX_WCOOP=1; off by
+// default): the active lanes take their rays one at a time; for ray r
+// every lane walks the same BVH path and the faces of the leaves it reaches (or of the
+// tile's bin list, for a binned primary ray) are spread across the lanes, each lane
+// folding its faces with `offer` (the same total order as the lane-per-ray loop: t32,
+// then t64, then OBJ face index), and the lanes holding the smallest t32 hand their
+// candidates to lane r, whose own `offer` keeps the reference's first-minimum choice.
+#ifndef RTX_WCOOP
+#define RTX_WCOOP 0
+#endif
+#ifndef RTX_WCOOP_MIN
+#define RTX_WCOOP_MIN 1024  // faces: smaller meshes keep one ray per lane
+#endif
+#if RTX_WCOOP && defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ float lane_f(float x, int r) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), r));
+}
+// The active lanes holding the smallest non-negative key (ballots from the top bit down;
+// lanes outside `active` never vote, whatever their registers hold).
+__device__ __forceinline__ uint64_t wave_argmin(float v, uint64_t active) {
+    const uint32_t key = __float_as_uint(v) & 0x7fffffffu;  // -0 ranks with +0
+    uint64_t cand = active;
+    for (int b = 30; b >= 0; --b) {
+        const uint64_t z = __ballot(((key >> b) & 1u) == 0u) & cand;
+        if (z) cand = z;
+    }
+    return cand;
+}
+__device__ __forceinline__ void coop_mesh(const SceneView& S, const DObj& ob, int32_t oi, int32_t bin,
+                                          f3 o, f3 d, float time, Hit& h) {
+    const uint64_t active = __ballot(1);
+    const int lane = __lane_id();
+    const int rank = __popcll(active & ((1ull << lane) - 1ull));
+    const int nact = __popcll(active);
+    const bool cull = face_cull(ob);
+    const int32_t ub = bin >= 0 ? wave_uniform(bin) : -1;
+    for (uint64_t pending = active; pending; pending &= pending - 1ull) {
+        const int r = __builtin_amdgcn_readfirstlane(__builtin_ctzll(pending));
+        const f3 ro{lane_f(o.x, r), lane_f(o.y, r), lane_f(o.z, r)};
+        const f3 rd{lane_f(d.x, r), lane_f(d.y, r), lane_f(d.z, r)};
+        const RayInv rri = ray_inv(ro, rd);
+        float cap = lane_f(h.t32, r);  // ray r's best so far: a face must reach it
+        Hit hl{INFINITY, -1, 0};
+        int32_t face = -1;  // this lane's face of the batch
+        int nbuf = 0;
+        auto flush = [&]() {
+            if (face >= 0) {
+                bool fmaybe = true;
+                if (cull) fmaybe = leaf_maybe_hit(RTX_FBOX(S, ob.tri_begin + face), ro, rri, ob.cmax, cap);
+                float t32;
+                const bool valid = tri_hit(RTX_TRI(S, ob.tri_begin + face), ro, rd, fmaybe, t32);
+                offer(S, hl, valid, t32, oi, face, ro, rd, time);
+            }
+            face = -1;
+            nbuf = 0;
+            cap = fminf(cap, lane_f(hl.t32, __builtin_ctzll(wave_argmin(hl.t32, active))));
+        };
+        if (ub >= 0) {  // the tile's candidate faces, nearest first (rtx_api.hip primary_bins)
+            const int32_t q1 = S.bin_start[ub + 1];
+            for (int32_t q0 = S.bin_start[ub]; q0 < q1; q0 += nact) {
+                if (cap < S.bin_zmin[q0]) break;
+                const int32_t q = q0 + rank;
+                face = q < q1 ? S.bin_faces[q] : -1;
+                flush();
+            }
+        } else {
+            for (int li = 0; li < ob.leaf_count;) {  // ray r's walk, the same in every lane
+                const auto& L = RTX_LEAF(S, ob.leaf_begin + li);
+                if (!RTX_ANY(leaf_maybe_hit(L, ro, rri, ob.cmax, cap))) { li = L.skip; continue; }
+                ++li;
+                for (int f0 = 0; f0 < L.count;) {  // the leaf's faces onto the free lanes
+                    const int take = min(L.count - f0, nact - nbuf);
+                    if (rank >= nbuf && rank < nbuf + take) face = L.first + f0 + (rank - nbuf);
+                    nbuf += take;
+                    f0 += take;
+                    if (nbuf == nact) flush();
+                }
+            }
+            if (nbuf > 0) flush();
+        }
+        const uint64_t has = __ballot(hl.obj >= 0);
+        if (!has) continue;
+        for (uint64_t win = wave_argmin(hl.obj >= 0 ? hl.t32 : INFINITY, active) & has; win; win &= win - 1ull) {
+            const int j = __builtin_amdgcn_readfirstlane(__builtin_ctzll(win));
+            const float t32 = lane_f(hl.t32, j);
+            const int32_t sb = __builtin_amdgcn_readlane(hl.sub, j);
+            if (lane == r) offer(S, h, true, t32, oi, sb, o, d, time);
+        }
+    }
+}
+#endif
+
 template <bool MESH, bool X, bool COUNT>
 RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const HStack& hs, HHit& hh,
                        int32_t bin = -1) {
@@ -1339,26 +1448,21 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
             if (!RTX_ANY(bv_maybe(ob, o, ri, h.t32))) continue;
             if (!mesh_bv(ob, o, d)) continue;  // the reference's bounding volume, quirks included
             // mesh.py:77-117 for stored face f (lanes with maybe set may take it)
+#if RTX_WCOOP && defined(__HIP_DEVICE_COMPILE__)
+            if (ob.tri_count >= RTX_WCOOP_MIN) {  // experiment: one ray per wave, faces across lanes
+                coop_mesh(S, ob, oi, (bin >= 0 && S.mesh_bins && k == 0) ? bin : -1, o, d, time, h);
+                continue;
+            }
+#endif
             auto test_face = [&](int f, bool maybe, bool cull) {
                 bool fmaybe = maybe;
                 if (cull) {  // the face's own padded box (the cluster's bound)
                     fmaybe = maybe && leaf_maybe_hit(RTX_FBOX(S, ob.tri_begin + f), o, ri, ob.cmax, h.t32);
                     if (!RTX_ANY(fmaybe)) return;  // no lane's ray can pass its exact test
                 }
-                const DTri T = RTX_TRI(S, ob.tri_begin + f);
                 tally_inc<COUNT>(tl, &Tally::tri);
-                const f3 n = ld3(T.n);
-                const float denom = dot(d, n);
-                const f3 v0 = ld3(T.v0);
-                const float num = dot(sub(v0, o), n);
-                const float t32 = num / denom;
-                // abs(denom) < epsilon -> skip; time < 0 -> skip
-                bool valid = fmaybe && !(fabsf(denom) < kEps4Up) && !quot_neg(t32, num, denom);
-                const f3 p = add(o, scale(d, t32));  // getPoint(time)
-                const float b0 = dot(cross(ld3(T.e01), sub(p, v0)), n);
-                const float b1 = dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n);
-                const float b2 = dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n);
-                valid = valid && b0 >= 0.0f && b1 >= 0.0f && b2 >= 0.0f;
+                float t32;
+                const bool valid = tri_hit(RTX_TRI(S, ob.tri_begin + f), o, d, fmaybe, t32);
                 offer(S, h, valid, t32, oi, f, o, d, time);
             };
             if (bin >= 0 && S.mesh_bins && k == 0) {  // a primary ray: its tile's candidate faces

@@ -479,3 +479,28 @@ def test_primary_bins_equal_walk(seed, monkeypatch):
             rows = torch.as_tensor(group_rows(61, n, k), device="cuda")
             assert torch.equal(on.render_device(groups=(k, n)), a[rows])
     assert torch.equal(on.render_device(row0=13, nrows=30), a[13:43])
+
+
+@pytest.mark.parametrize("case", ["blob", "blob_walk", "random0", "random3", "random6", "bins0", "bins5", "bins8"])
+def test_wave_cooperative_mesh_matches_oracle(case, tmp_path, monkeypatch):
+    """The wave-cooperative mesh variant (experiment -DRTX_WCOOP=1, off by default; DESIGN
+    §6e) is exact too: RTX_WCOOP_MIN=1 puts every mesh on it -- the 81,920-face blob with
+    its primary-ray bins and with the BVH walk, and random scenes whose reflected and
+    refracted rays reach the meshes from a subset of a wave's lanes, ragged tiles included."""
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import blob_obj, blob_scene, bins_scene, random_scene
+    monkeypatch.setenv("RTX_JIT_FLAGS", "-DRTX_WCOOP=1 -DRTX_WCOOP_MIN=1")
+    if case.startswith("blob"):
+        p = str(tmp_path / "blob6.obj")
+        blob_obj(p, level=6)
+        d = blob_scene(p, (64, 64))
+        if case == "blob_walk":
+            monkeypatch.setenv("RTX_BINS", "0")
+    elif case.startswith("bins"):
+        d = bins_scene(int(case[4:]), res=(97, 61))
+    else:
+        d = random_scene(int(case[6:]), res=(64, 48), mesh=True)
+    sc = product_scene_dict(d)
+    img = sc.render()
+    assert sc.last_kernel.startswith("rtx_jit_render_1"), sc.last_kernel
+    assert_parity(img, oracle_render_dict(d), case)
