@@ -201,6 +201,25 @@ struct alignas(16) DBound {
     float slo[4], shi[4];
 };
 
+// Light grid of a point light (rtx_api.hip light_grids): the directions from the light
+// to the scene's one mesh form a cone (axis a, padded half angle with cos^2 = cos2); its
+// gnomonic plane (x, y) = (w.u, w.v) / w.a, |x|, |y| <= tmax, is cut into G x G cells,
+// and cell c lists every face whose padded footprint covers it. A shadow ray from p to
+// the light (and beyond it: Mesh.shadow_intersect has no t_max) can only hit faces listed
+// in the cell of w = p - L (the line's points all lie in the directions +-w from L).
+// Within a cell, faces come by a lower bound of their distance from L along a: when the
+// mesh is on p's side of the light (w.a > 0) only the part of the line between p and L
+// meets it, so faces farther along a than |w| cannot occlude and the list stops there.
+struct alignas(16) DLGrid {
+    float L[3];
+    int32_t G;           // cells per side; 0 = no grid for this light
+    float a[3], cos2;
+    float u[3], tmax;
+    float v[3], scale;   // G / (2 tmax)
+    float r2min, r2max;  // |w|^2 outside [r2min, r2max]: walk the BVH instead
+    int32_t start_off, pad0;  // this light's G*G + 1 entries of lg_start
+};
+
 template <class T>
 using cptr = const T RTX_CONST*;
 template <class T>
@@ -234,6 +253,12 @@ struct SceneView {
     cptr<uint32_t> bin_objmask;      // per bin: spheres (bits 0-15) and boxes (16-31) a ray may hit
     int32_t bins_x, bins_on, mesh_bins, pad5;
     int32_t n_objs_all, n_mats, pad6, pad7;  // object records (incl. hierarchy leaves), materials
+    // Light grids (per light; shadow rays of point lights against the scene's one mesh)
+    cptr<DLGrid> lgrid;
+    cptr<int32_t> lg_start;          // per light: [G * G + 1] offsets into lg_faces
+    cptr<int32_t> lg_faces;          // stored face indices (within the mesh), by lg_d2
+    cptr<float> lg_d2;               // per entry: (a lower bound of the face's distance along a)^2
+    int32_t lgrid_on, pad8, pad9, pad10;
 };
 
 // Mesh records read by the hot BVH walks (closest_hit / occluded). Scene-specialized
@@ -1518,11 +1543,61 @@ RTX_HD void origin_terms(const SceneView& S, f3 o, float time, OriginTerms& T) {
 #endif
 }
 
+// Mesh.shadow_intersect's test of one face for the ray (o, d) (mesh.py:125-151: the
+// unnormalized normal, no t_max).
+template <class Tri>
+RTX_HD bool shadow_tri(const Tri& T, f3 o, f3 d) {
+    const f3 n = ld3(T.nu);
+    const float denom = dot(d, n);
+    const f3 v0 = ld3(T.v0);
+    const float num = dot(sub(v0, o), n);
+    const float t32 = num / denom;
+    // abs(denom) < epsilon -> skip; time < shadow_epsilon -> skip
+    bool hit = !(fabsf(denom) < kEps4Up) && !quot_lt(t32, num, denom, 1e-4, kEps4Near);
+    const f3 p = add(o, scale(d, t32));
+    return hit && dot(cross(ld3(T.e01), sub(p, v0)), n) >= 0.0f &&
+           dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n) >= 0.0f &&
+           dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n) >= 0.0f;
+}
+#ifndef RTX_LGRID_LANE
+#define RTX_LGRID_LANE 1  // light-grid lists: 1 per lane, 0 one distinct cell of the wave at a time
+#endif
+
+// The light-grid cell of a shadow ray from o toward a point light, d = L - o as the
+// shader computes it (so -d = fl(o - L) exactly): >= 0 a cell, -1 the line through o and
+// the light misses the mesh's cone (no face can occlude), -2 no grid answer (|w| out of
+// the grid's range, NaN): walk the BVH.
+RTX_HD int32_t lgrid_cell(cref<DLGrid> g, f3 d) {
+    const f3 w = neg(d);
+    const float w2 = dot(w, w);
+    if (!(w2 >= g.r2min && w2 <= g.r2max)) return -2;
+    const float wa = dot(w, ld3(g.a));
+    if (wa * wa <= g.cos2 * w2) return -1;
+    const float x = dot(w, ld3(g.u)) / wa, y = dot(w, ld3(g.v)) / wa;
+    const int32_t G = g.G;
+    auto clampi = [G](float t) {
+        const int32_t i = (int32_t)floorf(t);
+        return i < 0 ? 0 : (i > G - 1 ? G - 1 : i);
+    };
+    return clampi((y + g.tmax) * g.scale) * G + clampi((x + g.tmax) * g.scale);
+}
+
+// v of the first lane where pred holds (pred must hold somewhere), as a wave-uniform value.
+RTX_HD int32_t first_where(int32_t v, bool pred) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_readlane(v, __builtin_ctzll(__ballot((int)pred)));
+#else
+    (void)pred;
+    return v;
+#endif
+}
+
 // Any order gives the same answer; cheap objects first, and the wave leaves as soon as
-// every active lane is occluded.
+// every active lane is occluded. `light` >= 0: the ray goes to point light `light` (its
+// light grid, if any, may stand in for the mesh's BVH walk).
 template <bool MESH, bool X, bool COUNT>
 RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, Tally& tl, const HStack& hs,
-                     const OriginTerms* ot = nullptr) {
+                     const OriginTerms* ot = nullptr, int light = -1) {
     const float tmax32 = (float)t_max;
     bool occ = false;
     int oi = 0;
@@ -1578,38 +1653,69 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
     if (MESH) {
         for (int k = 0; k < RTX_NMESH(S); ++k, ++oi) {  // mesh.py:121-153 (no t_max test)
             const DObj ob = S.objs[oi];
-            if (RTX_ALL(occ)) break;
+            if (RTX_ALL(occ) || RTX_ABLATE == 11) break;  // 11: cost probe, meshes never occlude
             if (RTX_NBOX(S) == 0 && k == 0) ri = ray_inv(o, d);
             bool live = !occ && bv_maybe(ob, o, ri, INFINITY);  // conservative pre-test
             if (!RTX_ANY(live)) continue;
+            if (RTX_ABLATE == 13) continue;  // cost probe: the padded box pre-test only
             live = live && mesh_bv(ob, o, d);
-            if (!RTX_ANY(live)) continue;
+            if (!RTX_ANY(live) || RTX_ABLATE == 12) continue;  // 12: cost probe, bounding volumes only
+            // mesh.py:125-151 for stored face f (lanes with maybe set may take it)
+            auto shadow_face = [&](int f, bool maybe) {
+                bool fmaybe = maybe;
+                if (face_cull(ob)) {
+                    fmaybe = maybe && leaf_maybe_hit(RTX_FBOX(S, ob.tri_begin + f), o, ri, ob.cmax);
+                    if (!RTX_ANY(fmaybe)) return;
+                }
+                tally_inc<COUNT>(tl, &Tally::tri);
+                occ = occ || (fmaybe && shadow_tri(RTX_TRI(S, ob.tri_begin + f), o, d));
+            };
+#if !(defined(RTX_LIGHT_GRIDS) && !RTX_LIGHT_GRIDS)
+            if (light >= 0 && k == 0 && S.lgrid_on) {
+                cref<DLGrid> g = S.lgrid[light];
+                if (g.G > 0) {
+                    // lanes with a cell test only its faces, one distinct cell of the wave at
+                    // a time (the faces' loads stay wave-uniform); -1: nothing to test
+                    const int32_t cell = lgrid_cell(g, d);
+                    bool todo = live && cell >= 0;
+                    live = live && cell == -2;
+#if RTX_LGRID_LANE
+                    // each lane runs its own cell's list (per-lane loads of the faces)
+                    if (todo && !occ) {
+                        const int32_t q1 = S.lg_start[g.start_off + cell + 1];
+                        const f3 w = neg(d);
+                        // the mesh side of the light: faces farther along a than |w| are out
+                        const float wcap = dot(w, ld3(g.a)) > 0.0f ? dot(w, w) : INFINITY;
+                        for (int32_t q = S.lg_start[g.start_off + cell]; q < q1; ++q) {
+                            if (S.lg_d2[q] > wcap) break;
+                            tally_inc<COUNT>(tl, &Tally::tri);
+                            if (shadow_tri(S.tris[ob.tri_begin + S.lg_faces[q]], o, d)) { occ = true; break; }
+                        }
+                    }
+                    todo = false;
+#endif
+                    while (RTX_ANY(todo)) {
+                        const int32_t c = first_where(cell, todo);
+                        const bool mine = todo && cell == c;
+                        if (mine) {
+                            const int32_t q1 = S.lg_start[g.start_off + c + 1];
+                            for (int32_t q = S.lg_start[g.start_off + c]; q < q1; ++q) {
+                                if (RTX_ALL(occ)) break;
+                                shadow_face(S.lg_faces[q], !occ);
+                            }
+                        }
+                        todo = todo && !mine;
+                    }
+                    if (!RTX_ANY(live)) continue;
+                }
+            }
+#endif
             for (int li = 0; li < ob.leaf_count;) {  // stackless wave-uniform BVH walk
               const auto& L = RTX_LEAF(S, ob.leaf_begin + li);
               const bool maybe = live && !occ && leaf_maybe_hit(L, o, ri, ob.cmax);
               if (!RTX_ANY(maybe)) { li = L.skip; continue; }
               ++li;
-              for (int f = L.first; f < L.first + L.count; ++f) {
-                bool fmaybe = maybe;
-                if (face_cull(ob)) {
-                    fmaybe = maybe && leaf_maybe_hit(RTX_FBOX(S, ob.tri_begin + f), o, ri, ob.cmax);
-                    if (!RTX_ANY(fmaybe)) continue;
-                }
-                const DTri T = RTX_TRI(S, ob.tri_begin + f);
-                tally_inc<COUNT>(tl, &Tally::tri);
-                const f3 n = ld3(T.nu);
-                const float denom = dot(d, n);
-                const f3 v0 = ld3(T.v0);
-                const float num = dot(sub(v0, o), n);
-                const float t32 = num / denom;
-                // abs(denom) < epsilon -> skip; time < shadow_epsilon -> skip
-                bool hit = !(fabsf(denom) < kEps4Up) && !quot_lt(t32, num, denom, 1e-4, kEps4Near);
-                const f3 p = add(o, scale(d, t32));
-                hit = hit && dot(cross(ld3(T.e01), sub(p, v0)), n) >= 0.0f &&
-                      dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n) >= 0.0f &&
-                      dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n) >= 0.0f;
-                occ = occ || (fmaybe && hit);
-              }
+              for (int f = L.first; f < L.first + L.count; ++f) shadow_face(f, maybe);
             }
         }
     }
@@ -1725,7 +1831,7 @@ RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const 
             t_max = INFINITY;
         }
         tally_inc<COUNT>(tl, &Tally::shadow);
-        if (RTX_ABLATE != 1 && occluded<MESH, X, COUNT>(S, pos, sdir, t_max, time, tl, hs, otp)) continue;
+        if (RTX_ABLATE != 1 && occluded<MESH, X, COUNT>(S, pos, sdir, t_max, time, tl, hs, otp, li)) continue;
         if (RTX_ABLATE == 3) { colour = add(colour, mul(ld3(L.cp), diffuse)); continue; }
         f3 light_dir = point ? normalize(sdir) : ld3(L.ndir);
         f3 lambert = scale(diffuse, pos_part(dot(normal, light_dir)));

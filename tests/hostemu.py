@@ -36,6 +36,7 @@ def lib():
         _lib.rtx_hostemu_render_rows.argtypes = [vp, vp, vp, C.c_int32, vp, C.c_int]
         _lib.rtx_hostemu_intersect.argtypes = [vp, C.c_int64, vp, vp, C.c_double, vp, vp, vp, vp, vp]
         _lib.rtx_hostemu_occluded.argtypes = [vp, C.c_int64, vp, vp, vp, C.c_double, vp]
+        _lib.rtx_hostemu_occluded_light.argtypes = [vp, C.c_int64, vp, C.c_int32, C.c_int32, vp, vp]
         _lib.rtx_hostemu_last_error.restype = C.c_char_p
     return _lib
 
@@ -91,3 +92,21 @@ def occluded(scene, o, d, t_max, time=0.0):
     _chk(lib().rtx_hostemu_occluded(C.addressof(sd), n, o.ctypes.data, d.ctypes.data, tm.ctypes.data, time,
                                     occ.ctypes.data))
     return occ.astype(bool)
+
+
+def occluded_light(scene, o, light, grids):
+    """Shadow rays from points o to point light ``light`` as regular_lighting casts them
+    (d = L - o, t_max 1), through the light's grid (grids=True; None if it has none) or
+    the BVH walk. Returns (occluded bool [n], grid cell per point: -1 outside the cone,
+    -2 walked)."""
+    sd = scene.scene_desc()
+    o = np.ascontiguousarray(np.asarray(o, np.float32).reshape(-1, 3).T)
+    n = o.shape[1]
+    occ = np.zeros(n, np.uint8)
+    cells = np.zeros(n, np.int32)
+    rc = lib().rtx_hostemu_occluded_light(C.addressof(sd), n, o.ctypes.data, light, 1 if grids else 0,
+                                          occ.ctypes.data, cells.ctypes.data)
+    if rc == -1:
+        return None
+    _chk(rc)
+    return occ.astype(bool), cells

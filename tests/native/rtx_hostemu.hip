@@ -35,6 +35,23 @@ void bind_view(const HostScene& H, SceneView& v) {
     v.hlevels = H.hlevels;
 }
 
+// The light grids rtx_scene_create builds (RTX_LGRID=0: none), bound to the view.
+struct Grids {
+    std::vector<DLGrid> grids;
+    std::vector<int32_t> start, faces;
+    std::vector<float> d2;
+    void bind(const HostScene& H, SceneView& v) {
+        const char* e = getenv("RTX_LGRID");
+        if ((e && e[0] == '0') || !light_grids(H, grids, start, faces, d2)) return;
+        if (faces.empty()) { faces.push_back(0); d2.push_back(0.0f); }
+        v.lgrid = (cptr<DLGrid>)grids.data();
+        v.lg_start = (cptr<int32_t>)start.data();
+        v.lg_faces = (cptr<int32_t>)faces.data();
+        v.lg_d2 = (cptr<float>)d2.data();
+        v.lgrid_on = 1;
+    }
+};
+
 // Dispatch over the kernel template flags, as rtx_render's launch switch does.
 template <bool MESH, bool SEC, bool X>
 void pixel_jit(const KParams& k, float* fb, int32_t row0, int32_t rr, int32_t cc, Tally& tl, const FrameStack& fs,
@@ -70,6 +87,8 @@ extern "C" int rtx_hostemu_render(const rtx_scene_desc* sd, const rtx_camera_des
     if ((rc = convert_camera(cd, k))) return rc;
     if (row0 < 0 || nrows < 0 || row0 + nrows > cd->height) return fail(RTX_ERR_INVALID, "bad rows");
     bind_view(H, k.S);
+    Grids lg;
+    lg.bind(H, k.S);
     std::vector<float> times(cd->n_times);
     for (int i = 0; i < cd->n_times; ++i) times[i] = (float)cd->times[i];
     const auto mm = std::minmax_element(times.begin(), times.end());
@@ -134,6 +153,8 @@ extern "C" int rtx_hostemu_render_rows(const rtx_scene_desc* sd, const rtx_camer
     for (int32_t r = 0; r < nrows; ++r)
         if (rows[r] < 0 || rows[r] >= cd->height) return fail(RTX_ERR_INVALID, "bad rows");
     bind_view(H, k.S);
+    Grids lg;
+    lg.bind(H, k.S);
     std::vector<float> times(cd->n_times);
     for (int i = 0; i < cd->n_times; ++i) times[i] = (float)cd->times[i];
     const auto mm = std::minmax_element(times.begin(), times.end());
@@ -179,7 +200,7 @@ extern "C" int rtx_hostemu_intersect(const rtx_scene_desc* sd, int64_t n, const 
     HostScene H;
     int rc = convert_scene(sd, H);
     if (rc) return rc;
-    SceneView v;
+    SceneView v{};
     bind_view(H, v);
     const std::vector<DBound> bounds = compute_bounds(H.nodes, H.objs, H.tris, (float)time, (float)time);
     v.bounds = (cptr<DBound>)bounds.data();
@@ -214,7 +235,7 @@ extern "C" int rtx_hostemu_occluded(const rtx_scene_desc* sd, int64_t n, const f
     HostScene H;
     int rc = convert_scene(sd, H);
     if (rc) return rc;
-    SceneView v;
+    SceneView v{};
     bind_view(H, v);
     const std::vector<DBound> bounds = compute_bounds(H.nodes, H.objs, H.tris, (float)time, (float)time);
     v.bounds = (cptr<DBound>)bounds.data();
@@ -227,6 +248,65 @@ extern "C" int rtx_hostemu_occluded(const rtx_scene_desc* sd, int64_t n, const f
         bool r = H.has_mesh ? occluded<true, true, false>(v, o, d, tmax[i], (float)time, tl, hs)
                             : occluded<false, true, false>(v, o, d, tmax[i], (float)time, tl, hs);
         occ[i] = r ? 1 : 0;
+    }
+    return RTX_OK;
+}
+
+// Shadow rays from points o to point light `light` (d = L - o in fp32, t_max 1, as
+// regular_lighting casts them): with grids = 1 through its light grid (if it has one),
+// with grids = 0 through the BVH walk. Returns -1 if grids = 1 and the light has no grid.
+extern "C" int rtx_hostemu_occluded_light(const rtx_scene_desc* sd, int64_t n, const float* ro, int32_t light,
+                                          int32_t grids, uint8_t* occ, int32_t* cells) {
+    HostScene H;
+    int rc = convert_scene(sd, H);
+    if (rc) return rc;
+    if (light < 0 || light >= (int32_t)H.lights.size() || H.lights[light].type != LIGHT_POINT)
+        return fail(RTX_ERR_INVALID, "not a point light");
+    SceneView v{};
+    bind_view(H, v);
+    Grids lg;
+    if (grids) {
+        lg.bind(H, v);
+        if (!v.lgrid_on || lg.grids[light].G == 0) return -1;
+    }
+    const std::vector<DBound> bounds = compute_bounds(H.nodes, H.objs, H.tris, 0.0f, 0.0f);
+    v.bounds = (cptr<DBound>)bounds.data();
+    const DLight& L = H.lights[light];
+    for (int64_t i = 0; i < n; ++i) {
+        const f3 o = mk(ro[i], ro[n + i], ro[2 * n + i]);
+        const f3 d = sub(ld3(L.vec), o);  // regular_lighting's sdir
+        Tally tl = {};
+        float hst[kMaxHLevels * 9];
+        const HStack hs{hst, 1};
+        const bool r = H.has_mesh ? occluded<true, true, false>(v, o, d, 1.0, 0.0f, tl, hs, nullptr, grids ? light : -1)
+                                  : occluded<false, true, false>(v, o, d, 1.0, 0.0f, tl, hs, nullptr, grids ? light : -1);
+        occ[i] = r ? 1 : 0;
+        if (cells) cells[i] = grids ? lgrid_cell(v.lgrid[light], d) : -3;
+    }
+    return RTX_OK;
+}
+
+// Light grid statistics (tests and tuning): per light G, list entries, the longest list
+// and the non-empty cells; zeros for a light without a grid.
+extern "C" int rtx_hostemu_lgrid_stats(const rtx_scene_desc* sd, int64_t* out) {
+    HostScene H;
+    int rc = convert_scene(sd, H);
+    if (rc) return rc;
+    std::vector<DLGrid> grids;
+    std::vector<int32_t> start, faces;
+    std::vector<float> d2;
+    light_grids(H, grids, start, faces, d2);
+    for (size_t li = 0; li < grids.size(); ++li) {
+        const DLGrid& g = grids[li];
+        int64_t* o = out + 4 * li;
+        o[0] = g.G; o[1] = o[2] = o[3] = 0;
+        if (!g.G) continue;
+        for (int64_t c = 0; c < (int64_t)g.G * g.G; ++c) {
+            const int64_t len = start[g.start_off + c + 1] - start[g.start_off + c];
+            o[1] += len;
+            o[2] = std::max(o[2], len);
+            o[3] += len > 0;
+        }
     }
     return RTX_OK;
 }

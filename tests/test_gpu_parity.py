@@ -504,3 +504,29 @@ def test_wave_cooperative_mesh_matches_oracle(case, tmp_path, monkeypatch):
     img = sc.render()
     assert sc.last_kernel.startswith("rtx_jit_render_1"), sc.last_kernel
     assert_parity(img, oracle_render_dict(d), case)
+
+
+@pytest.mark.parametrize("case", ["TorusMesh", "blob", "random0", "random3", "bins5", "bins8"])
+def test_light_grids_equal_walk(case, tmp_path, monkeypatch):
+    """Light grids (a point light's shadow rays test only the mesh faces listed in the cell
+    of their direction from the light; rtx_api.hip light_grids) change no pixel: grid ==
+    BVH walk (RTX_LGRID=0) == oracle."""
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import blob_obj, blob_scene, bins_scene, random_scene
+    from rtx.io import bundled_scene_dict
+    if case == "TorusMesh":
+        d = bundled_scene_dict("TorusMesh", resolution=(160, 120))
+    elif case == "blob":
+        p = str(tmp_path / "blob6.obj")
+        blob_obj(p, level=6)
+        d = blob_scene(p, (64, 64))
+    elif case.startswith("bins"):
+        d = bins_scene(int(case[4:]), res=(97, 61))
+    else:
+        d = random_scene(int(case[6:]), res=(64, 48), mesh=True)
+    a = product_scene_dict(d).render_device().clone()
+    monkeypatch.setenv("RTX_LGRID", "0")
+    b = product_scene_dict(d).render_device().clone()
+    assert torch.equal(a, b)
+    img = np.ascontiguousarray(np.transpose(a.cpu().numpy()[::-1], (1, 0, 2))).astype(np.float64)
+    assert_parity(img, oracle_render_dict(d), case)

@@ -246,3 +246,90 @@ def test_hostemu_primary_bins_equal_walk(seed, monkeypatch):
     for k in range(3):
         strip, _ = hostemu.render(sc, k, 3)
         assert np.array_equal(strip, oracle_render_dict(d, k, 3)), k
+
+
+def _mesh_probe_points(tris, light, rng, n):
+    """Points that stress a light grid: on faces (interior, edges, vertices), just above
+    and below them, around the mesh, near and beyond the light, and far away."""
+    v = tris[:, :3].astype(np.float64)
+    f = rng.randint(len(v), size=n)
+    b = rng.dirichlet([1, 1, 1], size=n)
+    b[: n // 4, rng.randint(3)] = 0.0  # on an edge
+    b[: n // 4] /= b[: n // 4].sum(1, keepdims=True)
+    b[n // 4: n // 3] = np.eye(3)[rng.randint(3, size=n // 3 - n // 4)]  # on a vertex
+    on = np.einsum("nk,nkd->nd", b, v[f])
+    nrm = np.cross(v[f, 1] - v[f, 0], v[f, 2] - v[f, 0])
+    nrm /= np.maximum(np.linalg.norm(nrm, axis=1, keepdims=True), 1e-30)
+    off = on + nrm * rng.choice([-1e-3, -1e-5, 1e-5, 1e-3, 0.05], size=(n, 1))
+    lo, hi = v.reshape(-1, 3).min(0), v.reshape(-1, 3).max(0)
+    ctr, ext = (lo + hi) / 2, (hi - lo).max()
+    around = ctr + rng.uniform(-2, 2, (n, 3)) * ext
+    L = np.asarray(light, np.float64)
+    near_l = L + rng.normal(size=(n, 3)) * rng.choice([1e-3, 0.1, 1.0], size=(n, 1))
+    beyond = L + (L - ctr) * rng.uniform(0.05, 3.0, (n, 1)) + rng.normal(size=(n, 3)) * 0.3
+    far = ctr + rng.normal(size=(n, 3)) * rng.choice([10.0, 100.0, 1e4], size=(n, 1))
+    plane = np.c_[rng.uniform(-30, 30, n), np.full(n, -1.0), rng.uniform(-30, 30, n)]
+    return np.concatenate([on, off, around, near_l, beyond, far, plane]).astype(np.float32)
+
+
+def _grid_scenes(blob_path):
+    from scenegen import blob_scene
+    from common import product_scene_dict
+    from rtx.io import bundled_scene_dict
+    out = [("TorusMesh", bundled_scene_dict("TorusMesh", resolution=(32, 32)))]
+    d = blob_scene(blob_path, (32, 32))
+    out.append(("blob", d))
+    rng = np.random.RandomState(5)
+    for k in range(4):  # the torus moved and scaled, lights close, far, above, below, inside
+        e = bundled_scene_dict("TorusMesh", resolution=(32, 32))
+        for g in e["objects"]:
+            if g["type"] == "mesh":
+                g["scale"] = float(rng.uniform(0.3, 3.0))
+                g["position"] = np.round(rng.uniform(-2, 2, 3), 3).tolist()
+        e["lights"] = [{"name": "l%d" % i, "type": "point", "colour": [1, 1, 1], "power": 1.0,
+                        "position": np.round(rng.uniform(-1, 1, 3) * s, 3).tolist()}
+                       for i, s in enumerate((1.0, 4.0, 12.0, 60.0))]
+        out.append(("torus%d" % k, e))
+    return [(n, product_scene_dict(d)) for n, d in out]
+
+
+def test_hostemu_light_grids_equal_walk(blob5):
+    """The light grids (shadow rays of point lights test only the mesh faces listed in the
+    cell of their direction from the light) change no shadow decision: grid == BVH walk
+    for points on, just off and around the faces, near and beyond the light, far away and
+    on the ground plane, for TorusMesh, the 20k-face blob and moved/scaled tori with
+    lights near, far and inside the mesh's bounding sphere (those get no grid)."""
+    from rtx import _native as N
+    from rtx import records as R
+    used = 0
+    for name, sc in _grid_scenes(blob5):
+        mesh = [g for g in sc.objects if R.kind(g) == N.RTX_MESH][0]
+        tris = R.mesh_triangles(mesh)
+        for li, lt in enumerate(sc.lights):
+            rng = np.random.RandomState(li + 17)
+            pts = _mesh_probe_points(tris, R.vec(lt.vector), rng, 3000)
+            g = hostemu.occluded_light(sc, pts, li, True)
+            if g is None:
+                continue
+            w, _ = hostemu.occluded_light(sc, pts, li, False)
+            occ, cells = g
+            assert np.array_equal(occ, w), (name, li, int((occ != w).sum()))
+            used += 1
+            assert (cells >= 0).sum() > 100 and occ.sum() > 50, (name, li)
+    assert used >= 10, used
+
+
+@pytest.mark.parametrize("flat", [False, True])
+def test_hostemu_light_grids_frames(blob5, flat, monkeypatch):
+    """Whole frames with and without the light grids: identical, and equal to the oracle."""
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import blob_scene
+    from rtx.io import bundled_scene_dict
+    for d in (bundled_scene_dict("TorusMesh", resolution=(48, 48)), blob_scene(blob5, (40, 40), flat)):
+        sc = product_scene_dict(d)
+        img, _ = hostemu.render(sc)
+        monkeypatch.setenv("RTX_LGRID", "0")
+        walk, _ = hostemu.render(sc)
+        monkeypatch.delenv("RTX_LGRID")
+        assert np.array_equal(img, walk)
+        assert_parity(img, oracle_render_dict(d), "light grids")
