@@ -462,6 +462,37 @@ RTX_HD int sphere_disc_sign_oc(f3 d, f3 oc, float q, float r2f) {
     if (D > E) return 1;
     return 0;  // also NaN/inf inputs: the exact path reproduces the reference
 }
+// Sphere.shadow_intersect's decision (simple_geometry.py:48-72: a root t with
+// 1e-3 < t < t_max) in fp32 where error bounds allow: 1 hit, 0 no hit, -1 undecided (run
+// the fp64 roots). With D within E of the exact discriminant H^2 - A C (the bound
+// sphere_disc_sign_oc uses), s = sqrtf(D) is within E / s + 2^-22 s of sqrt(H^2 - A C),
+// and the roots (-H -+ s) / A -- the reference's (-b -+ sqrt(disc)) / 2a with b = 2H --
+// within m of the computed ones (every other rounding, and the reference's own fp64
+// rounding, is below 2^-20 (|H| + s) / A). 1e-3 < t <=> t >= fl32(1e-3) for a float t.
+#ifndef RTX_SHADOW_F32
+#define RTX_SHADOW_F32 0  // measured slower (TSP 28.5 -> 30.4 us, DOF 7.23 -> 7.37 ms): off
+#endif
+// [tmax_dn, tmax_up]: the floats around t_max (equal when t_max is one, as 1.0 and inf are)
+RTX_HD int sphere_shadow_f32(f3 d, f3 oc, float q, float r2f, float tmax_dn, float tmax_up) {
+    const float a = dot(d, d), h = dot(d, oc);
+    const float hh = h * h;
+    const float D = hh - a * (q - r2f);
+    const float E = 0x1p-21f * (hh + a * (q + r2f) + fabsf(D));
+    if (D < -E) return 0;  // no real root
+    if (!(D > E) || !(a > 0.0f)) return -1;
+    const float s = sqrtf(D);
+    const float inva = 1.0f / a;
+    const float m = (E / s + 0x1p-21f * s) * inva + 0x1p-20f * ((fabsf(h) + s) * inva);
+    auto decide = [&](float t) {
+        const float lo = t - m, hi = t + m;
+        if (lo >= kEps3Near && hi < tmax_dn) return 1;
+        if (hi < kEps3Near || lo >= tmax_up) return 0;
+        return -1;
+    };
+    const int h1 = decide((-h - s) * inva), h2 = decide((-h + s) * inva);
+    if (h1 == 1 || h2 == 1) return 1;
+    return h1 == 0 && h2 == 0 ? 0 : -1;
+}
 RTX_HD int sphere_disc_sign(f3 o, f3 d, f3 c, float r2f) {
     const f3 oc = sub(o, c);
     return sphere_disc_sign_oc(d, oc, dot(oc, oc), r2f);
@@ -1599,6 +1630,9 @@ template <bool MESH, bool X, bool COUNT>
 RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, Tally& tl, const HStack& hs,
                      const OriginTerms* ot = nullptr, int light = -1) {
     const float tmax32 = (float)t_max;
+    // the floats around t_max (both tmax32 for the shader's 1.0 and inf)
+    const float tmax_dn = (double)tmax32 > t_max ? nextafterf(tmax32, -INFINITY) : tmax32;
+    const float tmax_up = (double)tmax32 < t_max ? nextafterf(tmax32, INFINITY) : tmax32;
     bool occ = false;
     int oi = 0;
     for (int k = 0; k < RTX_NPLANE(S); ++k, ++oi) {  // simple_geometry.py:122-131
@@ -1626,7 +1660,12 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
         const f3 oc = sub(o, ctr);
         const float q = dot(oc, oc);
 #endif
-        if (!occ && sphere_disc_sign_oc(d, oc, q, (float)ob.r2) >= 0) {
+        int dec = -1;
+        if (RTX_SHADOW_F32 && RTX_ABLATE != 4) {
+            dec = sphere_shadow_f32(d, oc, q, (float)ob.r2, tmax_dn, tmax_up);
+            if (!occ && dec >= 0) occ = dec == 1;
+        }
+        if (!occ && dec < 0 && sphere_disc_sign_oc(d, oc, q, (float)ob.r2) >= 0) {
             double b, s, two_a;
             if (RTX_ABLATE == 4 ? sphere_roots(o, d, ctr, ob.r2, b, s, two_a)
                                 : sphere_roots_oc(d, oc, q, ob.r2, b, s, two_a)) {

@@ -333,3 +333,56 @@ def test_hostemu_light_grids_frames(blob5, flat, monkeypatch):
         monkeypatch.delenv("RTX_LGRID")
         assert np.array_equal(img, walk)
         assert_parity(img, oracle_render_dict(d), "light grids")
+
+
+def _sphere_shadow_stress_rays(centers, radii, n, rng):
+    """Shadow rays whose quadratic roots sit on the decision boundaries of
+    Sphere.shadow_intersect (simple_geometry.py:48-72): origins on and near the surface
+    (a root at ~0), roots at 1e-3 and at t_max = 1 (+-1e-7 relative), tangent and
+    near-tangent lines, long and short directions."""
+    os_, ds_ = [], []
+    for c, r in zip(centers, radii):
+        c = np.asarray(c, np.float64)
+        for k in range(n):
+            u = rng.normal(size=3); u /= np.linalg.norm(u)
+            v = rng.normal(size=3); v -= v.dot(u) * u; v /= np.linalg.norm(v)
+            kind = k % 5
+            scale = 10.0 ** rng.uniform(-1, 1)
+            if kind == 0:    # origin on / near the surface
+                o = c + u * r * (1 + rng.choice([0, 1e-7, -1e-7, 1e-4, -1e-4]))
+                d = rng.normal(size=3) * scale
+            elif kind == 1:  # a root at t = 1e-3 (entry) or exit
+                d = -u * scale
+                t0 = 1e-3 * (1 + rng.choice([0, 1e-7, -1e-7, 1e-6, -1e-6]))
+                o = c + u * r - d * t0 if rng.rand() < 0.5 else c - u * r - d * t0
+            elif kind == 2:  # a root at t = t_max = 1
+                d = -u * scale
+                t0 = 1.0 + rng.choice([0, 1e-7, -1e-7, 1e-6, -1e-6])
+                o = c + u * r - d * t0 if rng.rand() < 0.5 else c - u * r - d * t0
+            elif kind == 3:  # tangent and near-tangent lines
+                p = c + u * r * (1 + rng.choice([0, 1e-7, -1e-7, 1e-5, -1e-5]))
+                d = v * scale
+                o = p - d * rng.uniform(-0.5, 1.5)
+            else:            # from far away through the sphere
+                o = c + u * r * rng.uniform(2, 50)
+                d = (c + v * r * rng.uniform(0, 1.2) - o) * rng.uniform(0.2, 2.0)
+            os_.append(o); ds_.append(d)
+    return np.asarray(os_, np.float32), np.asarray(ds_, np.float32)
+
+
+@pytest.mark.parametrize("name", ["TwoSpheresPlane", "MirrorRefraction"])
+def test_hostemu_sphere_shadow_stress(name):
+    """Sphere shadow decisions vs the oracle at the 1e-3 and t_max boundaries: the fp64
+    roots, and with a build of -DRTX_SHADOW_F32=1 the fp32 decision with error bounds
+    (sphere_shadow_f32; a build with zero margins fails this test)."""
+    from oracle import oracle as O
+    from rtx import _native as N
+    from rtx import records as R
+    sc = product_scene(name, (8, 8))
+    sph = [g for g in sc.objects if R.kind(g) == N.RTX_SPHERE]
+    rng = np.random.RandomState(11)
+    o, d = _sphere_shadow_stress_rays([R.vec(g.center) for g in sph], [float(g.radius) for g in sph], 1500, rng)
+    dd, base = O.load_bundle(name)
+    osc = O.OracleScene(dd, base)
+    for tmax in (1.0, np.inf, 0.7, 1e-3 * (1 + 1e-6)):
+        assert np.array_equal(hostemu.occluded(sc, o, d, tmax, 0.0), osc.shadow(0.0, o, d, tmax).astype(bool)), tmax
