@@ -1744,7 +1744,7 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
     if (MESH) {
         for (int k = 0; k < RTX_NMESH(S); ++k, ++oi) {  // mesh.py:121-153 (no t_max test)
             const DObj ob = S.objs[oi];
-            if (RTX_ALL(occ) || RTX_ABLATE == 11) break;  // 11: cost probe, meshes never occlude
+            if (RTX_ALL(occ) || RTX_ABLATE == 16) break;  // 16: cost probe, meshes never occlude
             if (RTX_NBOX(S) == 0 && k == 0) ri = ray_inv(o, d);
             bool live = !occ && bv_maybe(ob, o, ri, INFINITY);  // conservative pre-test
             if (!RTX_ANY(live)) continue;
