@@ -1181,6 +1181,13 @@ hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& k
     const char* lm = getenv("RTX_JIT_LIBMACROS");  // experiment: 0 = do not forward them
     if (!(lm && lm[0] == '0'))
         for (const char* m : kLibMacros) opts.push_back(m);
+    if (mesh && !sec && !ext && fc_mode == 1) {
+        // small meshes (every face box-culled): 5 waves/SIMD beat the mesh kernels' 4
+        // despite a 48 B/lane spill (TorusMesh 1080p 70.2 -> 66.2 us; the 81,920-face
+        // mesh, which has no face boxes, measured 1.4 % slower at 5)
+        opts.push_back("-URTX_LB_WAVES");
+        opts.push_back("-DRTX_LB_WAVES(MESH,SEC)=5");
+    }
     if (const char* extra = getenv("RTX_JIT_FLAGS")) {  // experiments (tools/ablate.sh); part of the cache key
         std::istringstream is(extra);
         for (std::string o; is >> o;) opts.push_back(o);
