@@ -256,6 +256,34 @@ NodeBoxes leaf_boxes(const DObj& o, const std::vector<DTri>& tris, double tlo, d
     return nb;
 }
 
+// The device forms of the node and box records (rtx_trace.h DNodeHot / DNodeMat / DBox).
+void split_nodes(const std::vector<DNode>& nodes, std::vector<DNodeHot>& hot, std::vector<DNodeMat>& mat) {
+    hot.resize(nodes.size());
+    mat.resize(nodes.size());
+    for (size_t i = 0; i < nodes.size(); ++i) {
+        const DNode& n = nodes[i];
+        hot[i] = DNodeHot{n.kind, n.parent, n.cidx, n.depth, n.end, n.pkind, n.obj, n.mat0, n.oid, 0, 0, 0};
+        std::memcpy(mat[i].M, n.M, sizeof(n.M));
+        std::memcpy(mat[i].Minv, n.Minv, sizeof(n.Minv));
+    }
+}
+// [hit boxes | inside boxes | shadow boxes], n each
+std::vector<DBox> split_bounds(const std::vector<DBound>& b) {
+    const size_t n = b.size();
+    std::vector<DBox> out(3 * n);
+    for (size_t i = 0; i < n; ++i) {
+        std::memcpy(out[i].lo, b[i].hlo, 16); std::memcpy(out[i].hi, b[i].hhi, 16);
+        std::memcpy(out[n + i].lo, b[i].ilo, 16); std::memcpy(out[n + i].hi, b[i].ihi, 16);
+        std::memcpy(out[2 * n + i].lo, b[i].slo, 16); std::memcpy(out[2 * n + i].hi, b[i].shi, 16);
+    }
+    return out;
+}
+void bind_boxes(SceneView& v, const DBox* base, size_t n) {
+    v.hbox = (cptr<DBox>)base;
+    v.ibox = (cptr<DBox>)(base + n);
+    v.sbox = (cptr<DBox>)(base + 2 * n);
+}
+
 std::vector<DBound> compute_bounds(const std::vector<DNode>& nodes, const std::vector<DObj>& objs,
                                    const std::vector<DTri>& tris, double tlo, double thi) {
     const int n = (int)nodes.size();
@@ -1285,7 +1313,7 @@ struct rtx_scene {
     std::vector<DNode> h_nodes;
     std::vector<DObj> h_objs;
     std::vector<DTri> h_tris;
-    std::vector<DBound> h_bounds_abi;
+    std::vector<DBox> h_bounds_abi;
     HostScene h_bins;   // objs/tris and type counts, for the camera's primary-ray face bins
     int32_t* d_bin_start = nullptr;
     int32_t* d_bin_faces = nullptr;
@@ -1298,6 +1326,7 @@ struct rtx_scene {
     void* d_bounds_cam = nullptr;   // for the camera's motion times
     void* d_bounds_abi = nullptr;   // for the time of the last rtx_intersect / rtx_occluded
     void* d_nodes = nullptr;
+    void* d_nmat = nullptr;
     void* d_texels = nullptr;
     void* d_lut = nullptr;
     void* d_objs = nullptr;
@@ -1362,7 +1391,7 @@ void free_camera(rtx_scene* s) {
 void free_scene(rtx_scene* s) {
     free_camera(s);
     (void)hipFree(s->d_scratch);
-    for (void* p : {s->d_objs, s->d_tris, s->d_trins, s->d_fboxes, s->d_mats, s->d_lights, s->d_leaves, s->d_tri_orig, s->d_nodes,
+    for (void* p : {s->d_objs, s->d_tris, s->d_trins, s->d_fboxes, s->d_mats, s->d_lights, s->d_leaves, s->d_tri_orig, s->d_nodes, s->d_nmat,
                     s->d_texels, s->d_lut, s->d_bounds_abi, s->d_lgrid, s->d_lg_start, s->d_lg_faces, s->d_lg_d2})
         (void)hipFree(p);
     delete s;
@@ -1390,9 +1419,18 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
         (rc = upload(&s->d_fboxes, H.fboxes)) ||
         (rc = upload(&s->d_mats, H.mats)) || (rc = upload(&s->d_lights, H.lights)) ||
         (rc = upload(&s->d_leaves, H.leaves)) || (rc = upload(&s->d_tri_orig, H.tri_orig)) ||
-        (rc = upload(&s->d_nodes, H.nodes)) || (rc = upload(&s->d_texels, H.texels)) || (rc = upload(&s->d_lut, H.lut255))) {
+        (rc = upload(&s->d_texels, H.texels)) || (rc = upload(&s->d_lut, H.lut255))) {
         free_scene(s);
         return rc;
+    }
+    {
+        std::vector<DNodeHot> hot;
+        std::vector<DNodeMat> mat;
+        split_nodes(H.nodes, hot, mat);
+        if ((rc = upload(&s->d_nodes, hot)) || (rc = upload(&s->d_nmat, mat))) {
+            free_scene(s);
+            return rc;
+        }
     }
     s->has_mesh = H.has_mesh;
     s->has_secondary = H.has_secondary;
@@ -1418,7 +1456,7 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
         s->h_nodes = H.nodes;
         s->h_objs = H.objs;
         s->h_tris = H.tris;
-        if ((rc = upload(&s->d_bounds_abi, std::vector<DBound>(H.nodes.size())))) {
+        if ((rc = upload(&s->d_bounds_abi, std::vector<DBox>(3 * H.nodes.size())))) {
             free_scene(s);
             return rc;
         }
@@ -1439,7 +1477,8 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
     v.n_plane = H.n_plane; v.n_sphere = H.n_sphere; v.n_box = H.n_box; v.n_mesh = H.n_mesh;
     v.pow_bits = H.pow_bits;
     std::memcpy(v.ambient, H.ambient, sizeof(v.ambient));
-    v.nodes = (cptr<DNode>)s->d_nodes;
+    v.nodes = (cptr<DNodeHot>)s->d_nodes;
+    v.nmat = (cptr<DNodeMat>)s->d_nmat;
     v.texels = (cptr<uint32_t>)s->d_texels;
     v.lut255 = (cptr<float>)s->d_lut;
     v.n_nodes = (int32_t)H.nodes.size();
@@ -1498,9 +1537,10 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     k.S = s->view;
     if (!s->h_nodes.empty()) {  // hierarchy bounds over the frame's motion-time range
         const auto mm = std::minmax_element(times.begin(), times.end());
-        if ((rc = upload(&s->d_bounds_cam, compute_bounds(s->h_nodes, s->h_objs, s->h_tris, *mm.first, *mm.second))))
+        if ((rc = upload(&s->d_bounds_cam,
+                         split_bounds(compute_bounds(s->h_nodes, s->h_objs, s->h_tris, *mm.first, *mm.second)))))
             return rc;
-        k.S.bounds = (cptr<DBound>)s->d_bounds_cam;
+        bind_boxes(k.S, (const DBox*)s->d_bounds_cam, s->h_nodes.size());
     }
     {
         std::vector<int32_t> bstart, bfaces;
@@ -1704,10 +1744,10 @@ int view_at(rtx_scene* s, double time, hipStream_t stream, SceneView& v) {
     v = s->view;
     if (s->h_nodes.empty()) return RTX_OK;
     const float t = (float)time;
-    s->h_bounds_abi = compute_bounds(s->h_nodes, s->h_objs, s->h_tris, t, t);
-    RTX_HIP(hipMemcpyAsync(s->d_bounds_abi, s->h_bounds_abi.data(), sizeof(DBound) * s->h_bounds_abi.size(),
+    s->h_bounds_abi = split_bounds(compute_bounds(s->h_nodes, s->h_objs, s->h_tris, t, t));
+    RTX_HIP(hipMemcpyAsync(s->d_bounds_abi, s->h_bounds_abi.data(), sizeof(DBox) * s->h_bounds_abi.size(),
                            hipMemcpyHostToDevice, stream));
-    v.bounds = (cptr<DBound>)s->d_bounds_abi;
+    bind_boxes(v, (const DBox*)s->d_bounds_abi, s->h_nodes.size());
     return RTX_OK;
 }
 }  // namespace

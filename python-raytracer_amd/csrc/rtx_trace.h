@@ -190,6 +190,19 @@ struct alignas(16) DNode {
 };
 constexpr int kMaxHLevels = 16;  // hierarchy depth limit (levels of the ray/point stacks)
 
+// On the device a node is split by use, so the traversal's scalar working set stays small
+// (the scalar data cache is 16 KB): the fields every step reads (48 B), and the matrices
+// (128 B) read only when a ray or point descends into the node.
+struct alignas(16) DNodeHot {
+    int32_t kind, parent, cidx, depth;
+    int32_t end, pkind, obj, mat0;
+    int32_t oid, pad0, pad1, pad2;
+};
+struct alignas(16) DNodeMat {
+    float M[16];
+    float Minv[16];
+};
+
 // Conservative regions of a hierarchy subtree, in its parent's frame, for the frame's
 // motion-time range (computed on the host, padded far beyond fp32 rounding): every
 // intersect() hit of the subtree that also passes its parent's filter lies in h,
@@ -199,6 +212,10 @@ struct alignas(16) DBound {
     float hlo[4], hhi[4];
     float ilo[4], ihi[4];
     float slo[4], shi[4];
+};
+// On the device the three kinds of box live in three arrays (a traversal reads one kind).
+struct alignas(16) DBox {
+    float lo[4], hi[4];
 };
 
 // Light grid of a point light (rtx_api.hip light_grids): the directions from the light
@@ -238,10 +255,11 @@ struct SceneView {
     int32_t n_plane, n_sphere, n_box, n_mesh;
     int32_t pow_bits, pad0, pad1, pad2;   // bit length of the largest integer hardness
     float ambient[4];
-    cptr<DNode> nodes;               // hierarchy nodes (roots: 0, nodes[0].end, ...)
+    cptr<DNodeHot> nodes;            // hierarchy nodes (roots: 0, nodes[0].end, ...)
+    cptr<DNodeMat> nmat;             // their matrices
     cptr<uint32_t> texels;           // all textures, RGBA8 (A unused)
     cptr<float> lut255;              // fl32(k / 255) (simple_geometry.py:169)
-    cptr<DBound> bounds;             // per node, for the current motion-time range
+    cptr<DBox> hbox, ibox, sbox;     // per node, for the current motion-time range (DBound)
     int32_t n_nodes, hlevels;        // hlevels: stack levels the hierarchies need
     int32_t n_tris, n_leaves;        // all triangles / mesh BVH nodes
     // Primary-ray face bins of the camera (rtx_api.hip primary_bins): for each 8x8 pixel
@@ -1091,11 +1109,11 @@ RTX_HD bool pt_in(const float RTX_CONST* lo, const float RTX_CONST* hi, f3 p) {
 
 // is_inside(x, p) for p in the frame of x's parent's children (hierarchy.py:111-129).
 RTX_HX bool is_inside(const SceneView& S, const HStack& hs, int x, f3 p, float time) {
-    if (!pt_in(S.bounds[x].ilo, S.bounds[x].ihi, p)) return false;
-    cref<DNode> X = S.nodes[x];
+    if (!pt_in(S.ibox[x].lo, S.ibox[x].hi, p)) return false;
+    cref<DNodeHot> X = S.nodes[x];
     if (X.kind == HN_LEAF) return leaf_inside(S.objs[X.obj], p, time);
     if (X.kind == HN_OTHER) return false;
-    hs.put_pt(X.depth, xform(X.Minv, p, 1.0f));
+    hs.put_pt(X.depth, xform(S.nmat[x].Minv, p, 1.0f));
     uint32_t acc = hinit(0u, X.kind, X.depth);
     int open = x;
     int32_t okind = X.kind, odepth = X.depth, oend = X.end, oparent = X.parent, ocidx = X.cidx;
@@ -1104,12 +1122,12 @@ RTX_HX bool is_inside(const SceneView& S, const HStack& hs, int x, f3 p, float t
         while (i >= oend) {  // close finished subtrees
             const bool v = ((acc >> odepth) & 1u) != 0u;
             if (open == x) return v;
-            cref<DNode> Pn = S.nodes[oparent];
+            cref<DNodeHot> Pn = S.nodes[oparent];
             acc = hfold(acc, Pn.kind, Pn.depth, ocidx, v);
             open = oparent;
             okind = Pn.kind; odepth = Pn.depth; oend = Pn.end; oparent = Pn.parent; ocidx = Pn.cidx;
         }
-        cref<DNode> c = S.nodes[i];
+        cref<DNodeHot> c = S.nodes[i];
         if ((okind == HN_DIFF && c.cidx >= 2) || hdecided(acc, okind, odepth, c.cidx)) { i = oend; continue; }
         if (c.kind == HN_LEAF) {
             acc = hfold(acc, okind, odepth, c.cidx, leaf_inside(S.objs[c.obj], hs.get_pt(odepth), time));
@@ -1118,7 +1136,7 @@ RTX_HX bool is_inside(const SceneView& S, const HStack& hs, int x, f3 p, float t
             acc = hfold(acc, okind, odepth, c.cidx, false);
             i = c.end;
         } else {
-            hs.put_pt(c.depth, xform(c.Minv, hs.get_pt(odepth), 1.0f));
+            hs.put_pt(c.depth, xform(S.nmat[i].Minv, hs.get_pt(odepth), 1.0f));
             acc = hinit(acc, c.kind, c.depth);
             open = i;
             okind = c.kind; odepth = c.depth; oend = c.end; oparent = c.parent; ocidx = c.cidx;
@@ -1131,12 +1149,12 @@ RTX_HX bool is_inside(const SceneView& S, const HStack& hs, int x, f3 p, float t
 // the first child containing the point, recursively; -1 = None.
 RTX_HX int32_t get_material(const SceneView& S, const HStack& hs, int x, f3 p, float time) {
     for (;;) {
-        cref<DNode> X = S.nodes[x];
+        cref<DNodeHot> X = S.nodes[x];
         if (X.kind == HN_LEAF) {
             cref<DObj> ob = S.objs[X.obj];
             return ob.type == OBJ_PLANE ? plane_material(ob, p, time) : ob.mat0;
         }
-        const f3 q = xform(X.Minv, p, 1.0f);
+        const f3 q = xform(S.nmat[x].Minv, p, 1.0f);
         int found = -1;
         for (int j = x + 1; j < X.end; j = S.nodes[j].end)
             if (is_inside(S, hs, j, q, time)) { found = j; break; }
@@ -1154,9 +1172,9 @@ RTX_HX int32_t get_material(const SceneView& S, const HStack& hs, int x, f3 p, f
 RTX_HX bool walk_up(const SceneView& S, const HStack& hs, int cur, int stop, float time, f3& pos, f3& n,
                     int32_t& mat) {
     while (cur != stop) {
-        cref<DNode> c = S.nodes[cur];
+        cref<DNodeHot> c = S.nodes[cur];
         const int a = c.parent;
-        cref<DNode> A = S.nodes[a];
+        cref<DNodeHot> A = S.nodes[a];
         if (A.kind == HN_INTER) {
             for (int j = a + 1; j < A.end; j = S.nodes[j].end)
                 if (j != cur && !is_inside(S, hs, j, pos, time)) return false;
@@ -1171,8 +1189,8 @@ RTX_HX bool walk_up(const SceneView& S, const HStack& hs, int cur, int stop, flo
             }
         }
         if (mat < 0) mat = A.mat0 < 0 ? 0 : A.mat0;  // the reference raises IndexError for A.mat0 < 0
-        pos = xform(A.M, pos, 1.0f);
-        n = normal_xform(A.Minv, n);
+        pos = xform(S.nmat[a].M, pos, 1.0f);
+        n = normal_xform(S.nmat[a].Minv, n);
         cur = a;
     }
     return true;
@@ -1187,9 +1205,9 @@ RTX_HD void hier_enum(const SceneView& S, const HStack& hs, int s, float time, W
     auto culled = [&](int c, int32_t depth) {
         f3 ro, rd;
         hs.get_ray(depth, ro, rd);
-        return !RTX_ANY(ray_meets(S.bounds[c].hlo, S.bounds[c].hhi, ro, rd, cap()));
+        return !RTX_ANY(ray_meets(S.hbox[c].lo, S.hbox[c].hi, ro, rd, cap()));
     };
-    cref<DNode> root = S.nodes[s];
+    cref<DNodeHot> root = S.nodes[s];
     if (culled(s, root.depth)) return;
     auto visit_leaf = [&](int li, int32_t depth, int32_t obj) {
         f3 lo, ld;
@@ -1205,17 +1223,17 @@ RTX_HD void hier_enum(const SceneView& S, const HStack& hs, int s, float time, W
     {
         f3 ro, rd;
         hs.get_ray(root.depth, ro, rd);
-        hs.put_ray(root.depth + 1, xform(root.Minv, ro, 1.0f), xform(root.Minv, rd, 0.0f));
+        hs.put_ray(root.depth + 1, xform(S.nmat[s].Minv, ro, 1.0f), xform(S.nmat[s].Minv, rd, 0.0f));
     }
     for (int i = s + 1; i < root.end;) {
-        cref<DNode> c = S.nodes[i];
+        cref<DNodeHot> c = S.nodes[i];
         if (c.pkind == HN_DIFF && c.cidx >= 2) { i = c.end; continue; }  // difference reads children 0, 1
         if (culled(i, c.depth)) { i = c.end; continue; }
         if (c.kind == HN_LEAF) { visit_leaf(i, c.depth, c.obj); ++i; continue; }
         if (c.kind == HN_OTHER) { i = c.end; continue; }
         f3 ro, rd;
         hs.get_ray(c.depth, ro, rd);
-        hs.put_ray(c.depth + 1, xform(c.Minv, ro, 1.0f), xform(c.Minv, rd, 0.0f));
+        hs.put_ray(c.depth + 1, xform(S.nmat[i].Minv, ro, 1.0f), xform(S.nmat[i].Minv, rd, 0.0f));
         ++i;
     }
 }
@@ -1224,11 +1242,11 @@ RTX_HD void hier_enum(const SceneView& S, const HStack& hs, int s, float time, W
 // the shadow epsilon that the other child does not veto; no t_max test.
 template <bool MESH>
 RTX_HD bool diff_shadow(const SceneView& S, const HStack& hs, int x, float time) {
-    cref<DNode> X = S.nodes[x];
+    cref<DNodeHot> X = S.nodes[x];
     {
         f3 ro, rd;
         hs.get_ray(X.depth, ro, rd);
-        hs.put_ray(X.depth + 1, xform(X.Minv, ro, 1.0f), xform(X.Minv, rd, 0.0f));
+        hs.put_ray(X.depth + 1, xform(S.nmat[x].Minv, ro, 1.0f), xform(S.nmat[x].Minv, rd, 0.0f));
     }
     const int c0 = x + 1, c1 = S.nodes[c0].end;
     bool found = false;
@@ -1251,11 +1269,11 @@ RTX_HD bool diff_shadow(const SceneView& S, const HStack& hs, int x, float time)
 template <bool MESH>
 RTX_HY bool hier_shadow(const SceneView& S, const HStack& hs, int r, f3 o, f3 d, double t_max, float time) {
     hs.put_ray(0, o, d);
-    if (!RTX_ANY(ray_meets(S.bounds[r].slo, S.bounds[r].shi, o, d, INFINITY))) return false;
-    cref<DNode> R = S.nodes[r];
+    if (!RTX_ANY(ray_meets(S.sbox[r].lo, S.sbox[r].hi, o, d, INFINITY))) return false;
+    cref<DNodeHot> R = S.nodes[r];
     if (R.kind == HN_OTHER) return false;
     if (R.kind == HN_DIFF) return diff_shadow<MESH>(S, hs, r, time);
-    hs.put_ray(1, xform(R.Minv, o, 1.0f), xform(R.Minv, d, 0.0f));
+    hs.put_ray(1, xform(S.nmat[r].Minv, o, 1.0f), xform(S.nmat[r].Minv, d, 0.0f));
     uint32_t acc = hinit(0u, R.kind, 0);
     int open = r;
     int32_t okind = R.kind, odepth = R.depth, oend = R.end, oparent = R.parent, ocidx = R.cidx;
@@ -1264,18 +1282,18 @@ RTX_HY bool hier_shadow(const SceneView& S, const HStack& hs, int r, f3 o, f3 d,
         while (i >= oend) {
             const bool v = ((acc >> odepth) & 1u) != 0u;
             if (open == r) return v;
-            cref<DNode> Pn = S.nodes[oparent];
+            cref<DNodeHot> Pn = S.nodes[oparent];
             acc = hfold(acc, Pn.kind, Pn.depth, ocidx, v);
             open = oparent;
             okind = Pn.kind; odepth = Pn.depth; oend = Pn.end; oparent = Pn.parent; ocidx = Pn.cidx;
         }
-        cref<DNode> c = S.nodes[i];
+        cref<DNodeHot> c = S.nodes[i];
         if (hdecided(acc, okind, odepth, c.cidx)) { i = oend; continue; }
         bool live;
         {
             f3 ro, rd;
             hs.get_ray(c.depth, ro, rd);
-            live = ray_meets(S.bounds[i].slo, S.bounds[i].shi, ro, rd, INFINITY);
+            live = ray_meets(S.sbox[i].lo, S.sbox[i].hi, ro, rd, INFINITY);
         }
         if (!RTX_ANY(live)) {  // shadow_intersect is False for every lane
             acc = hfold(acc, okind, odepth, c.cidx, false);
@@ -1294,7 +1312,7 @@ RTX_HY bool hier_shadow(const SceneView& S, const HStack& hs, int r, f3 o, f3 d,
         } else {
             f3 ro, rd;
             hs.get_ray(c.depth, ro, rd);
-            hs.put_ray(c.depth + 1, xform(c.Minv, ro, 1.0f), xform(c.Minv, rd, 0.0f));
+            hs.put_ray(c.depth + 1, xform(S.nmat[i].Minv, ro, 1.0f), xform(S.nmat[i].Minv, rd, 0.0f));
             acc = hinit(acc, c.kind, c.depth);
             open = i;
             okind = c.kind; odepth = c.depth; oend = c.end; oparent = c.parent; ocidx = c.cidx;
@@ -1328,7 +1346,7 @@ RTX_HY void hier_closest(const SceneView& S, const HStack& hs, f3 o, f3 d, float
     if (S.n_nodes > 0 && S.nodes[0].end < S.n_nodes) {
         float best = INFINITY;
         for (int r = 0; r < S.n_nodes; r = S.nodes[r].end) {
-            const float e = wave_first(box_entry(S.bounds[r].hlo, S.bounds[r].hhi, o, d));
+            const float e = wave_first(box_entry(S.hbox[r].lo, S.hbox[r].hi, o, d));
             if (e < best) { best = e; first = r; }
         }
     }

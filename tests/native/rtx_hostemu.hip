@@ -28,12 +28,26 @@ void bind_view(const HostScene& H, SceneView& v) {
     v.n_plane = H.n_plane; v.n_sphere = H.n_sphere; v.n_box = H.n_box; v.n_mesh = H.n_mesh;
     v.pow_bits = H.pow_bits;
     std::memcpy(v.ambient, H.ambient, sizeof(v.ambient));
-    v.nodes = (cptr<DNode>)H.nodes.data();
     v.texels = (cptr<uint32_t>)H.texels.data();
     v.lut255 = (cptr<float>)H.lut255.data();
     v.n_nodes = (int32_t)H.nodes.size();
     v.hlevels = H.hlevels;
 }
+
+// The device forms of the hierarchy records, as rtx_scene_create / rtx_camera_set upload
+// them: split nodes and the boxes for the time range [tlo, thi].
+struct Nodes {
+    std::vector<DNodeHot> hot;
+    std::vector<DNodeMat> mat;
+    std::vector<DBox> boxes;
+    void bind(const HostScene& H, SceneView& v, float tlo, float thi) {
+        split_nodes(H.nodes, hot, mat);
+        boxes = split_bounds(compute_bounds(H.nodes, H.objs, H.tris, tlo, thi));
+        v.nodes = (cptr<DNodeHot>)hot.data();
+        v.nmat = (cptr<DNodeMat>)mat.data();
+        bind_boxes(v, boxes.data(), H.nodes.size());
+    }
+};
 
 // The light grids rtx_scene_create builds (RTX_LGRID=0: none), bound to the view.
 struct Grids {
@@ -92,8 +106,8 @@ extern "C" int rtx_hostemu_render(const rtx_scene_desc* sd, const rtx_camera_des
     std::vector<float> times(cd->n_times);
     for (int i = 0; i < cd->n_times; ++i) times[i] = (float)cd->times[i];
     const auto mm = std::minmax_element(times.begin(), times.end());
-    const std::vector<DBound> bounds = compute_bounds(H.nodes, H.objs, H.tris, *mm.first, *mm.second);
-    k.S.bounds = (cptr<DBound>)bounds.data();
+    Nodes nv;
+    nv.bind(H, k.S, *mm.first, *mm.second);
     std::vector<int32_t> bstart, bfaces;
     std::vector<float> bz;
     std::vector<uint32_t> bmask;
@@ -158,8 +172,8 @@ extern "C" int rtx_hostemu_render_rows(const rtx_scene_desc* sd, const rtx_camer
     std::vector<float> times(cd->n_times);
     for (int i = 0; i < cd->n_times; ++i) times[i] = (float)cd->times[i];
     const auto mm = std::minmax_element(times.begin(), times.end());
-    const std::vector<DBound> bounds = compute_bounds(H.nodes, H.objs, H.tris, *mm.first, *mm.second);
-    k.S.bounds = (cptr<DBound>)bounds.data();
+    Nodes nv;
+    nv.bind(H, k.S, *mm.first, *mm.second);
     std::vector<int32_t> bstart, bfaces;
     std::vector<float> bz;
     std::vector<uint32_t> bmask;
@@ -202,8 +216,8 @@ extern "C" int rtx_hostemu_intersect(const rtx_scene_desc* sd, int64_t n, const 
     if (rc) return rc;
     SceneView v{};
     bind_view(H, v);
-    const std::vector<DBound> bounds = compute_bounds(H.nodes, H.objs, H.tris, (float)time, (float)time);
-    v.bounds = (cptr<DBound>)bounds.data();
+    Nodes nv;
+    nv.bind(H, v, (float)time, (float)time);
     for (int64_t i = 0; i < n; ++i) {
         const f3 o = mk(ro[i], ro[n + i], ro[2 * n + i]);
         const f3 d = mk(rd[i], rd[n + i], rd[2 * n + i]);
@@ -237,8 +251,8 @@ extern "C" int rtx_hostemu_occluded(const rtx_scene_desc* sd, int64_t n, const f
     if (rc) return rc;
     SceneView v{};
     bind_view(H, v);
-    const std::vector<DBound> bounds = compute_bounds(H.nodes, H.objs, H.tris, (float)time, (float)time);
-    v.bounds = (cptr<DBound>)bounds.data();
+    Nodes nv;
+    nv.bind(H, v, (float)time, (float)time);
     for (int64_t i = 0; i < n; ++i) {
         const f3 o = mk(ro[i], ro[n + i], ro[2 * n + i]);
         const f3 d = mk(rd[i], rd[n + i], rd[2 * n + i]);
@@ -269,8 +283,8 @@ extern "C" int rtx_hostemu_occluded_light(const rtx_scene_desc* sd, int64_t n, c
         lg.bind(H, v);
         if (!v.lgrid_on || lg.grids[light].G == 0) return -1;
     }
-    const std::vector<DBound> bounds = compute_bounds(H.nodes, H.objs, H.tris, 0.0f, 0.0f);
-    v.bounds = (cptr<DBound>)bounds.data();
+    Nodes nv;
+    nv.bind(H, v, 0.0f, 0.0f);
     const DLight& L = H.lights[light];
     for (int64_t i = 0; i < n; ++i) {
         const f3 o = mk(ro[i], ro[n + i], ro[2 * n + i]);
