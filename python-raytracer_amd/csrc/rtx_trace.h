@@ -1693,6 +1693,9 @@ RTX_HD int32_t first_where(int32_t v, bool pred) {
 #endif
 }
 
+#ifndef RTX_PLANE_SHADOW_RCP
+#define RTX_PLANE_SHADOW_RCP 1
+#endif
 // Any order gives the same answer; cheap objects first, and the wave leaves as soon as
 // every active lane is occluded. `light` >= 0: the ray goes to point light `light` (its
 // light grid, if any, may stand in for the mesh's BVH walk).
@@ -1703,6 +1706,7 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
     // the floats around t_max (both tmax32 for the shader's 1.0 and inf)
     const float tmax_dn = (double)tmax32 > t_max ? nextafterf(tmax32, -INFINITY) : tmax32;
     const float tmax_up = (double)tmax32 < t_max ? nextafterf(tmax32, INFINITY) : tmax32;
+    const float tmax_lim = nextafterf(tmax_dn, -INFINITY);  // a float strictly below t_max
     bool occ = false;
     int oi = 0;
     for (int k = 0; k < RTX_NPLANE(S); ++k, ++oi) {  // simple_geometry.py:122-131
@@ -1714,9 +1718,31 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
 #else
         const float num = dot(sub(moved(ob, ob.a, time), o), n);
 #endif
+#if RTX_PLANE_SHADOW_RCP
+        // num * v_rcp(denom) is within 2^-21 of num / denom: far from both thresholds it
+        // decides alone, the correctly rounded quotient only near them (experiment)
+        bool hit = false;
+        if (fabsf(denom) >= kEps4Up) {
+            const float ta = num * rcp_approx(denom), lo = ta * (1.0f - 0x1p-19f), hi = ta * (1.0f + 0x1p-19f);
+            const float tlo = fminf(lo, hi), thi = fmaxf(lo, hi);
+            // q > tlo >= kEps4Up > 1e-4; q < thi < fl32(1e-4) < 1e-4; q < thi < tmax_lim <
+            // t_max keeps fl64(q) < t_max; q > tlo >= tmax_up >= t_max; an infinite t_max
+            // holds every finite quotient (|denom| >= 1e-4)
+            const int above = tlo >= kEps4Up ? 1 : (thi < kEps4Near ? 0 : -1);
+            const int below = tmax_dn == INFINITY ? (fabsf(num) < INFINITY ? 1 : -1)
+                              : (thi < tmax_lim ? 1 : (tlo >= tmax_up && tlo < INFINITY ? 0 : -1));
+            if (above >= 0 && below >= 0) {
+                hit = above == 1 && below == 1;
+            } else {
+                const float t32 = num / denom;
+                hit = quot_gt(t32, num, denom, 1e-4, kEps4Near) && quot_lt(t32, num, denom, t_max, tmax32);
+            }
+        }
+#else
         const float t32 = num / denom;
         const bool hit = fabsf(denom) >= kEps4Up && quot_gt(t32, num, denom, 1e-4, kEps4Near) &&
                          quot_lt(t32, num, denom, t_max, tmax32);
+#endif
         occ = occ || hit;
     }
     if (RTX_ALL(occ)) return true;

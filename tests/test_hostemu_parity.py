@@ -386,3 +386,29 @@ def test_hostemu_sphere_shadow_stress(name):
     osc = O.OracleScene(dd, base)
     for tmax in (1.0, np.inf, 0.7, 1e-3 * (1 + 1e-6)):
         assert np.array_equal(hostemu.occluded(sc, o, d, tmax, 0.0), osc.shadow(0.0, o, d, tmax).astype(bool)), tmax
+
+
+def test_hostemu_plane_shadow_stress():
+    """Plane shadow decisions vs the oracle where the plane's t sits on the 1e-4 and
+    t_max boundaries (+-1e-7 relative) -- the approximate-reciprocal filter must defer to
+    the exact quotient there (rtx_trace.h occluded, RTX_PLANE_SHADOW_RCP)."""
+    from oracle import oracle as O
+    from rtx import _native as N
+    from rtx import records as R
+    sc = product_scene("TwoSpheresPlane", (8, 8))
+    pl = [g for g in sc.objects if R.kind(g) == N.RTX_PLANE][0]
+    p0, n = R.vec(pl.point).astype(np.float64), R.vec(pl.normal).astype(np.float64)
+    rng = np.random.RandomState(5)
+    os_, ds_ = [], []
+    for k in range(6000):
+        d = rng.normal(size=3) * 10.0 ** rng.uniform(-1, 1)
+        if abs(d.dot(n)) < 1e-3:
+            continue
+        q = p0 + rng.uniform(-20, 20, 3); q -= (q - p0).dot(n) * n / n.dot(n)
+        t0 = {0: 1e-4, 1: 1.0, 2: 0.7}[k % 3] * (1 + rng.choice([0, 1e-7, -1e-7, 1e-6, -1e-6, 1e-3]))
+        os_.append(q - d * t0); ds_.append(d)
+    o, d = np.asarray(os_, np.float32), np.asarray(ds_, np.float32)
+    dd, base = O.load_bundle("TwoSpheresPlane")
+    osc = O.OracleScene(dd, base)
+    for tmax in (1.0, np.inf, 0.7):
+        assert np.array_equal(hostemu.occluded(sc, o, d, tmax, 0.0), osc.shadow(0.0, o, d, tmax).astype(bool)), tmax
