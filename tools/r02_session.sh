@@ -29,6 +29,7 @@ if [ "${PMC:-1}" = 1 ]; then
 else
   for c in $CFGS; do cp profiles/pmc_$c.json "$OUT/pmc_$c.json"; done
 fi
+[ "${BENCH:-1}" = 1 ] || { echo ALL_DONE; exit 0; }  # BENCH=0: counter passes only
 step bench_default 300 python bench.py --pmc-json "$OUT/pmc_tsp1080.json" || exit 1
 for c in $CFGS; do
   steps=50; [ $c = dof4k ] && steps=10
