@@ -5,11 +5,13 @@ TwoSpheresPlane 1920x1080 @1/2/4/8 GPUs).
 The unit is the reference's: primary samples W*H*aa*dof*|times| per second (its tqdm bar,
 provided/scene.py:45,71). One step = one 1920x1080 1-spp frame of TwoSpheresPlane.
 N = 1: the frame is rendered into the fp32 framebuffer on one GPU.
-N > 1 (north star, "scaling": "strong"): the SAME frame is split across the ranks —
-each renders its interleaved 8-row groups (rtx_render_groups), converts them to uint8
-on its GPU and rank 0 gathers them with one RCCL collective (rtx.distributed.FramePipeline,
-double-buffered so a frame's gather overlaps the next frame's render); the frame-parallel
-rate (each rank its own frame) is reported beside it as "weak_scaling".
+N > 1 (north star, "scaling": "strong"): every frame is split across the ranks — each
+renders its rows straight to uint8 on its GPU (row blocks for 1-spp frames, interleaved
+8-row groups otherwise) — and gathered to ONE rank over RCCL: frame k to rank k mod N
+(rtx.distributed.FrameExchange), the gathers of N consecutive frames issued as one
+all_to_all that overlaps the next N renders. Reported beside it: every frame gathered to
+rank 0 (rtx.distributed.FramePipeline, "gather_to_rank0", bounded by rank 0's ingress)
+and the frame-parallel rate (each rank its own frame, "weak_scaling").
 
 Launch: python bench.py [--steps K --warmup W]          (N = 1)
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -76,7 +78,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--force-dist", action="store_true", help="initialise torch.distributed even for one rank (tests)")
     p.add_argument("--pipeline", action="store_true",
-                   help="run the multi-GPU frame pipeline (render groups + RCCL gather) even at N = 1 (rehearsal)")
+                   help="run the multi-GPU frame loop (sharded frames + RCCL exchange) even at N = 1 (rehearsal)")
+    p.add_argument("--no-graph", action="store_true",
+                   help="N > 1: launch each frame's render from Python instead of one HIP graph per group")
     p.add_argument("--pmc-json", default=None,
                    help="tools/pmc_summary.py output for this config (default profiles/pmc_<config>.json)")
     return p.parse_args()
@@ -291,7 +295,7 @@ def main():
     if use_dist:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import rtx  # noqa: F401
-    from rtx.distributed import FramePipeline
+    from rtx.distributed import FrameExchange, FramePipeline
 
     sc = make_scene(a.config)
     W, H = sc.vc.width, sc.vc.height
@@ -323,56 +327,70 @@ def main():
         rows_frac = 1.0
         scaling, parallelism = "strong", "single GPU"
     else:
-        # N > 1 (north star): one step = ONE frame sharded across the ranks — interleaved
-        # 8-row groups per rank rendered straight to uint8 (rtx_render_groups_rgb8), one
-        # RCCL gather to rank 0; frame k's gather overlaps frame k + 1's render.
+        # N > 1 (north star): one step = ONE frame sharded across the ranks (uint8 rows
+        # rendered by every rank) and gathered to its owner, rank k mod N; the gathers of N
+        # consecutive frames are one RCCL all_to_all overlapping the next N renders.
+        ex = FrameExchange(sc, rank, world, graph=not a.no_graph)
+
+        def run_frames(loop, n):
+            if use_dist:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(n):
+                loop.step()
+            loop.flush()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            if use_dist:
+                dist.barrier()
+            return max_over_ranks(t1 - t0, use_dist)
+        for _ in range(a.warmup):
+            ex.step()
+        ex.flush()
+        torch.cuda.synchronize()
+        wall_s = run_frames(ex, a.steps)
+        # the same frames with every gather to rank 0 (FramePipeline), for comparison
         pipe = FramePipeline(sc, rank, world)
         for _ in range(a.warmup):
             pipe.step()
         pipe.flush()
-        torch.cuda.synchronize()
-        if use_dist:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(a.steps):
-            pipe.step()
-        pipe.flush()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        if use_dist:
-            dist.barrier()
-        wall_s = max_over_ranks(t1 - t0, use_dist)
+        rank0_s = run_frames(pipe, a.steps)
         # breakdown (outside the timed region): this rank's render + uint8 conversion, and
-        # the gather + reorder alone, each from HIP events on the launch stream
-        rank_fb = torch.empty((pipe.slots[0].nrows, W, 3), dtype=torch.float32, device="cuda")
+        # one group exchange alone, each from HIP events on the launch stream
+        rank_fb = torch.empty((ex.nrows, W, 3), dtype=torch.float32, device="cuda")
 
         def fp32_rows():  # this rank's rows into fp32: the kernel the roofline below prices
-            if pipe.interleave:
+            if ex.interleave:
                 sc.render_device(groups=(rank, world), out=rank_fb, stream=stream)
             else:
-                sc.render_device(row0=int(pipe.rows[0]), nrows=len(pipe.rows), out=rank_fb, stream=stream)
+                sc.render_device(row0=int(ex.rows[0]), nrows=len(ex.rows), out=rank_fb, stream=stream)
         fp32_rows()  # (its first call may compile the fp32 variant of the specialized kernel)
         torch.cuda.synchronize()
         kern_ms = max_over_ranks(kernel_ms(fp32_rows, a.steps, stream), use_dist)
         kernel = sc.last_kernel
-        render_ms = max_over_ranks(kernel_ms(pipe.render, a.steps, stream), use_dist)
+        render_ms = max_over_ranks(kernel_ms(ex.render, a.steps, stream), use_dist)
         kernel_rgb8 = sc.last_kernel
-        slot = pipe.slots[0]
         if use_dist:
             dist.barrier()
-        gather_ms = max_over_ranks(kernel_ms(slot, a.steps, stream), use_dist)
-        rows_frac = pipe.slots[0].nrows / H
-        nrows = [len(r) for r in pipe.slots[0].rows]
+
+        exchange_ms = max_over_ranks(kernel_ms(ex.exchange_once, a.steps, stream), use_dist)
+        rows_frac = ex.nrows / H
+        nrows = [len(r) for r in ex.rows_all]
         extra["multi_gpu"] = {
             "frame_ms": round(wall_s * 1e3 / a.steps, 5),
             "render_ms_per_rank": round(kern_ms, 5), "render_rgb8_ms_per_rank": round(render_ms, 5),
             "kernel_rgb8": kernel_rgb8,
-            "gather_ms": round(gather_ms, 5),
+            "exchange_ms_per_group": round(exchange_ms, 5), "frames_per_group": world,
             "rows_per_rank": [min(nrows), max(nrows)],
-            "partition": ("interleaved 8-row groups r, r+N, ... (rtx_render_groups_rgb8), reordered on rank 0"
-                          if pipe.interleave else "np.array_split row blocks (rtx_render_rgb8), gathered in image order"),
-            "collective": "one torch.distributed.gather of uint8 rows to rank 0 (RCCL), double-buffered",
+            "partition": ("interleaved 8-row groups r, r+N, ... (rtx_render_groups_rgb8), reordered by the owner"
+                          if ex.interleave else "np.array_split row blocks (rtx_render_rgb8), received in image order"),
+            "collective": "frame k gathered to rank k mod N; the gathers of N consecutive frames are one "
+                          "torch.distributed.all_to_all_single (RCCL), double-buffered",
+            "launch": "eager" if a.no_graph else "one HIP graph of the group's N renders per group",
+            "gather_to_rank0": {"frame_ms": round(rank0_s * 1e3 / a.steps, 5),
+                                "Mrays_s": round(W * H * spp * a.steps / rank0_s / 1e6, 3),
+                                "note": "FramePipeline: every frame gathered to rank 0 (its ingress bounds the rate)"},
         }
         # secondary: weak scaling (each rank renders its own whole frame per step)
         for _ in range(3):
@@ -381,7 +399,7 @@ def main():
         extra["weak_scaling"] = {"Mrays_s": round(world * W * H * spp * a.steps / weak_s / 1e6, 3),
                                  "ms_per_step": round(weak_s * 1e3 / a.steps, 5),
                                  "note": "frame-parallel: each rank renders its own whole frame, no collective"}
-        scaling, parallelism = "strong", "row-groups x %d ranks + RCCL gather" % world
+        scaling, parallelism = "strong", "rows x %d ranks + RCCL gather to each frame's owner" % world
     ms_per_step = wall_s * 1e3 / a.steps
     value = W * H * spp * a.steps / wall_s / 1e6
 

@@ -1,5 +1,5 @@
 """Multi-GPU frame rendering: one process per GPU, each rank renders part of ONE frame, one
-gather to rank 0.
+gather of that frame to one rank (rank 0, or the frame's owner in FrameExchange).
 
 The reference parallelises by rendering column strips in separate processes and
 stitching them on the filesystem (render.nu:2-23, provided/scene.py:36-37,
@@ -123,8 +123,8 @@ def render_frame(scene, rank, world, render_rows=None, dtype=torch.float32, dst=
 
 
 class FramePipeline:
-    """The multi-GPU frame loop of bench.py (north star: one frame sharded across the node,
-    one gather at the end): every step renders this rank's rows of the next frame straight
+    """Every frame sharded across the node and gathered to ``dst`` (bench.py reports it
+    beside FrameExchange, its N > 1 headline, as "gather_to_rank0"): every step renders this rank's rows of the next frame straight
     into uint8 (rtx_render_rgb8 / rtx_render_groups_rgb8: main.py:33's conversion fused
     into the render kernel) and starts their gather to ``dst`` asynchronously; the previous
     frame's gather is then awaited (a stream wait, not a host wait, on RCCL). Two buffer
@@ -187,3 +187,141 @@ class FramePipeline:
         """Wait for the last submitted frame; returns it on ``dst``."""
         prev, self.prev = self.prev, None
         return self._finish(*prev) if prev is not None else None
+
+
+class FrameExchange:
+    """The multi-GPU frame loop of bench.py at N > 1: every frame is sharded over the N
+    ranks and gathered to ONE rank, its owner -- frame k belongs to rank k mod N, the
+    process that would write its PNG (the reference writes each strip's file from its own
+    process and glues them: provided/main.py:26-28, provided/glue.py:17-27).
+
+    FramePipeline gathers every frame to rank 0, so the frame rate is capped by rank 0's
+    ingress: (N - 1) / N of every frame over its links, while the other ranks' links idle.
+    Here the gathers of N consecutive frames (frame j of a group to rank j) are issued as
+    one ``all_to_all_single``: each rank sends its rows of frame j straight to rank j, so
+    every xGMI link of the full mesh carries 1 / N of a frame per group and the exchange
+    costs ~1 / N of a gather per frame.
+
+    Frames are submitted one per ``step``; a group is rendered once its N frames are
+    submitted (this rank's rows of each, uint8, fused, into the group's send buffer), then
+    its exchange starts asynchronously and the previous group's exchange is awaited (a
+    stream wait on RCCL), so an exchange overlaps the next group's renders. Two group
+    buffers. ``graph=True`` records the N renders of each buffer once as a HIP graph and
+    replays it per group: one launch per group instead of N, which keeps the host ahead of
+    renders that take a few microseconds at N = 8 (needs a render_block that does not
+    depend on k, like the bench's static frame). ``flush`` renders and exchanges a partial
+    last group (uneven splits: no rows for the frames that were not submitted).
+
+    ``render_block(out, rows, k)`` fills this rank's uint8 rows [len(rows), W, 3] of frame
+    k (the CPU tests inject the host emulation). ``step`` and ``flush`` return the list
+    of (k, frame [H, W, 3]) this rank owns that completed; a frame is a view of the
+    receive buffer (block partitions) valid until that buffer's next exchange, two groups
+    later."""
+
+    def __init__(self, scene, rank, world, group=None, device=None, render_block=None, interleave=None, graph=False):
+        H, W = scene.vc.height, scene.vc.width
+        device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if interleave is None:
+            interleave = scene.samples_per_pixel > 1
+        self.rank, self.world, self.group, self.interleave = rank, world, group, interleave
+        self.rows_all = [rank_rows(H, world, r, interleave) for r in range(world)]
+        self.rows = self.rows_all[rank]
+        self.nrows = len(self.rows)
+        self.maxrows = max(len(r) for r in self.rows_all)
+        self.in_order = not interleave and H == world * self.maxrows
+        shape = (world, self.maxrows, W, 3)
+        self.send = [torch.zeros(shape, dtype=torch.uint8, device=device) for _ in range(2)]
+        self.recv = [torch.empty(shape, dtype=torch.uint8, device=device) for _ in range(2)]
+        src = np.empty(H, np.int64)  # frame row -> row of a receive buffer viewed as [N * maxrows]
+        for r, rws in enumerate(self.rows_all):
+            src[rws] = r * self.maxrows + np.arange(len(rws))
+        self.index = torch.as_tensor(src, device=device)
+        if render_block is None:
+            if interleave:
+                def render_block(out, rows, k):
+                    scene.render_device(groups=(rank, world), out=out)
+            else:
+                r0, n = row_block(H, world, rank)
+
+                def render_block(out, rows, k):
+                    scene.render_device(row0=r0, nrows=n, out=out)
+        self.render_block = render_block
+        self.graph = graph and device.type == "cuda"
+        self.graphs = [None, None]
+        self.k = 0
+        self.pending = None  # (work, buffer, first frame index, frames) of the last exchange
+
+    def render_group(self, buf, first, nframes):
+        """Render this rank's rows of frames first .. first + nframes - 1 into slots
+        0 .. nframes - 1 of buffer ``buf`` (a graph replay for a full group in graph mode)."""
+        if not self.nrows:
+            return
+        if self.graph and nframes == self.world:
+            if self.graphs[buf] is None:
+                for j in range(nframes):  # eager once: compiles any specialized kernel first
+                    self.render_block(self.send[buf][j, :self.nrows], self.rows, first + j)
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for j in range(nframes):
+                        self.render_block(self.send[buf][j, :self.nrows], self.rows, first + j)
+                self.graphs[buf] = g
+            self.graphs[buf].replay()
+            return
+        for j in range(nframes):
+            self.render_block(self.send[buf][j, :self.nrows], self.rows, first + j)
+
+    def render(self):
+        """One frame's render alone (bench.py's breakdown; not part of the frame loop)."""
+        if self.nrows:
+            self.render_block(self.send[0][0, :self.nrows], self.rows, 0)
+
+    def _frame(self, buf):
+        flat = self.recv[buf].view((self.world * self.maxrows,) + tuple(self.recv[buf].shape[2:]))
+        return flat if self.in_order else torch.index_select(flat, 0, self.index)
+
+    def _submit_group(self, nframes):
+        """Render the group that ends at frame k - 1 (nframes of it) and start its one
+        collective: frame j's rows to rank j. Returns the previous group's frames."""
+        first = self.k - nframes
+        buf = (first // self.world) % 2
+        self.render_group(buf, first, nframes)
+        send = self.send[buf].view((self.world * self.maxrows,) + tuple(self.send[buf].shape[2:]))
+        recv = self.recv[buf].view(send.shape)
+        if nframes == self.world:
+            work = dist.all_to_all_single(recv, send, group=self.group, async_op=True)
+        else:
+            ins = [self.maxrows if j < nframes else 0 for j in range(self.world)]
+            outs = [self.maxrows if self.rank < nframes else 0] * self.world
+            # split sizes must add up to the tensors' first dimension
+            work = dist.all_to_all_single(recv[:sum(outs)], send[:sum(ins)], output_split_sizes=outs,
+                                          input_split_sizes=ins, group=self.group, async_op=True)
+        prev, self.pending = self.pending, (work, buf, first, nframes)
+        return self._finish(prev)
+
+    def _finish(self, pending):
+        if pending is None:
+            return []
+        work, buf, first, nframes = pending
+        work.wait()
+        return [(first + self.rank, self._frame(buf))] if self.rank < nframes else []
+
+    def exchange_once(self):
+        """One full-group exchange of buffer 0, awaited (a stream wait): its cost alone
+        (bench.py's breakdown; not part of the frame loop)."""
+        send = self.send[0].view((self.world * self.maxrows,) + tuple(self.send[0].shape[2:]))
+        dist.all_to_all_single(self.recv[0].view(send.shape), send, group=self.group, async_op=True).wait()
+
+    def step(self):
+        """Submit the next frame; returns this rank's completed frames (see the class)."""
+        self.k += 1
+        return self._submit_group(self.world) if self.k % self.world == 0 else []
+
+    def flush(self):
+        """Render and exchange a partial last group, and wait for everything submitted."""
+        out = []
+        j = self.k % self.world
+        if j:
+            out += self._submit_group(j)
+        pending, self.pending = self.pending, None
+        return out + self._finish(pending)

@@ -101,6 +101,64 @@ def test_frame_pipeline_gathers_every_frame(world, res, interleave):
         assert np.array_equal(f, want)
 
 
+def _exchange_worker(rank, world, port, name, res, nframes, interleave, out_q):
+    """bench.py's N > 1 frame loop (rtx.distributed.FrameExchange: frame k sharded over the
+    ranks and gathered to rank k mod N, N frames per all_to_all) with the host emulation as
+    each rank's renderer. Frame k's rows are the scene's plus k (mod 256), so a frame that
+    reaches the wrong owner or slot fails the comparison."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), "python-raytracer_amd"), here):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import hostemu
+    from common import product_scene
+    from rtx.distributed import FrameExchange, to_rgb8
+    sc = product_scene(name, res)
+    cache = {}
+
+    def render_block(out, rows, k):
+        if "rows" not in cache:
+            cache["rows"] = to_rgb8(torch.from_numpy(hostemu.render_rows(sc, rows, threads=2)))
+        out.copy_(cache["rows"] + k)  # uint8 wraps
+    ex = FrameExchange(sc, rank, world, device=torch.device("cpu"), render_block=render_block, interleave=interleave)
+    got = []
+    for _ in range(nframes):
+        got += ex.step()
+    got += ex.flush()
+    out_q.put((rank, [(k, f.clone().numpy()) for k, f in got]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,res,interleave,nframes", [(2, (40, 23), True, 5), (3, (33, 26), True, 7),
+                                                          (2, (40, 24), False, 4), (3, (20, 13), False, 2)])
+def test_frame_exchange_delivers_every_frame_to_its_owner(world, res, interleave, nframes):
+    from common import oracle_render
+    from oracle import oracle as O
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, "MirrorRefraction", res, nframes, interleave, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    per_rank = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = O.to_png_array(oracle_render("MirrorRefraction", res))
+    seen = []
+    for r, frames in per_rank.items():
+        for k, f in frames:
+            assert k % world == r, (k, r)
+            assert np.array_equal(f, (want.astype(np.int64) + k).astype(np.uint8)), (k, r)
+            seen.append(k)
+    assert sorted(seen) == list(range(nframes))
+
+
 @pytest.mark.parametrize("world,res", [(2, (40, 23)), (3, (17, 10))])
 def test_gather_row_blocks(world, res):
     from common import oracle_render
