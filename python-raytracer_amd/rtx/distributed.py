@@ -248,6 +248,8 @@ class FrameExchange:
         self.render_block = render_block
         self.graph = graph and device.type == "cuda"
         self.graphs = [None, None]
+        if self.graph:
+            self.capture()
         self.k = 0
         self.pending = None  # (work, buffer, first frame index, frames) of the last exchange
 
@@ -258,18 +260,30 @@ class FrameExchange:
             return
         if self.graph and nframes == self.world:
             if self.graphs[buf] is None:
-                for j in range(nframes):  # eager once: compiles any specialized kernel first
-                    self.render_block(self.send[buf][j, :self.nrows], self.rows, first + j)
-                torch.cuda.synchronize()
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    for j in range(nframes):
-                        self.render_block(self.send[buf][j, :self.nrows], self.rows, first + j)
-                self.graphs[buf] = g
+                self.capture()
             self.graphs[buf].replay()
             return
         for j in range(nframes):
             self.render_block(self.send[buf][j, :self.nrows], self.rows, first + j)
+
+    def capture(self):
+        """Record both buffers' group renders as HIP graphs (graph mode). Done before the
+        first exchange is issued, so no collective is in flight while capturing; the
+        capture is thread-local (the process group's watchdog thread keeps querying its
+        events meanwhile)."""
+        if not self.nrows:
+            return
+        for buf in (0, 1):
+            for j in range(self.world):  # eager once: compiles any specialized kernel first
+                self.render_block(self.send[buf][j, :self.nrows], self.rows, j)
+        torch.cuda.synchronize()
+        for buf in (0, 1):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                for j in range(self.world):
+                    self.render_block(self.send[buf][j, :self.nrows], self.rows, j)
+            self.graphs[buf] = g
+        torch.cuda.synchronize()
 
     def render(self):
         """One frame's render alone (bench.py's breakdown; not part of the frame loop)."""
