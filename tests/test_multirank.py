@@ -124,17 +124,18 @@ def _exchange_worker(rank, world, port, name, res, nframes, interleave, out_q):
             cache["rows"] = to_rgb8(torch.from_numpy(hostemu.render_rows(sc, rows, threads=2)))
         out.copy_(cache["rows"] + k)  # uint8 wraps
     ex = FrameExchange(sc, rank, world, device=torch.device("cpu"), render_block=render_block, interleave=interleave)
-    got = []
+    got = []  # frames are views of a receive buffer: keep copies (the buffer is reused)
     for _ in range(nframes):
-        got += ex.step()
-    got += ex.flush()
-    out_q.put((rank, [(k, f.clone().numpy()) for k, f in got]))
+        got += [(k, f.clone().numpy()) for k, f in ex.step()]
+    got += [(k, f.clone().numpy()) for k, f in ex.flush()]
+    out_q.put((rank, got))
     dist.barrier()
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world,res,interleave,nframes", [(2, (40, 23), True, 5), (3, (33, 26), True, 7),
-                                                          (2, (40, 24), False, 4), (3, (20, 13), False, 2)])
+                                                          (2, (40, 24), False, 4), (3, (20, 13), False, 2),
+                                                          (4, (24, 20), False, 9), (4, (24, 41), True, 8)])
 def test_frame_exchange_delivers_every_frame_to_its_owner(world, res, interleave, nframes):
     from common import oracle_render
     from oracle import oracle as O
