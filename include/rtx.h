@@ -204,6 +204,15 @@ int rtx_render_rgb8(rtx_scene* scene, int32_t row0, int32_t nrows, uint8_t* out_
 int rtx_render_groups_rgb8(rtx_scene* scene, int32_t phase, int32_t stride, uint8_t* out_dev,
                            uint64_t* counters_dev, void* hip_stream);
 
+/* Frames of one scene state in ONE launch (no reference counterpart: a launch-count
+ * optimisation of the multi-GPU frame loop, rtx.distributed.FrameExchange): nframes
+ * copies of rtx_render (rgb8 = 0: fp32) / rtx_render_rgb8 (rgb8 != 0) of rows
+ * [row0, row0 + nrows), frame f at out_dev + f * frame_stride_bytes (>= one frame's
+ * bytes; a multiple of 4 for fp32). gridDim.y = nframes fills the GPU that one
+ * 1/N-of-a-frame launch per rank leaves partly idle at N = 8. 1 <= nframes <= 65535. */
+int rtx_render_frames(rtx_scene* scene, int32_t row0, int32_t nrows, void* out_dev, int32_t rgb8, int32_t nframes,
+                      int64_t frame_stride_bytes, uint64_t* counters_dev, void* hip_stream);
+
 /* Rows rtx_render_groups writes for an image of `height` rows (-1: bad arguments). */
 int32_t rtx_group_rows(int32_t height, int32_t phase, int32_t stride);
 

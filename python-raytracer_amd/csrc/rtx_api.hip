@@ -1579,14 +1579,17 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
 }
 
 namespace {
-int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, bool out8);
+int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, bool out8, int32_t nframes = 1);
 
 int render_rows(const char* fn, rtx_scene* s, int32_t row0, int32_t nrows, void* out_dev, uint64_t* counters_dev,
-                void* stream, bool out8) {
+                void* stream, bool out8, int32_t nframes = 1, int64_t fstride = 0) {
     if (!s) return fail(RTX_ERR_INVALID, std::string(fn) + ": null scene");
     if (!s->cam_set) return fail(RTX_ERR_STATE, std::string(fn) + ": rtx_camera_set was not called");
     if (row0 < 0 || nrows < 0 || (int64_t)row0 + nrows > s->kp.height)
         return fail(RTX_ERR_INVALID, std::string(fn) + ": row range outside the image");
+    const int64_t block_bytes = (int64_t)nrows * s->kp.ncols * 3 * (out8 ? 1 : 4);
+    if (nframes < 1 || nframes > 65535 || (nframes > 1 && fstride < block_bytes) || (!out8 && fstride % 4))
+        return fail(RTX_ERR_INVALID, std::string(fn) + ": need 1 <= nframes <= 65535 and frames that do not overlap");
     if (nrows == 0) return RTX_OK;
     if (!out_dev) return fail(RTX_ERR_INVALID, std::string(fn) + ": null framebuffer");
     Launch L;
@@ -1595,7 +1598,8 @@ int render_rows(const char* fn, rtx_scene* s, int32_t row0, int32_t nrows, void*
     L.nrows = nrows;
     L.gphase = 0;
     L.gstride = 0;
-    return render_launch(s, L, counters_dev, stream, out8);
+    L.fstride = nframes > 1 ? fstride : 0;
+    return render_launch(s, L, counters_dev, stream, out8, nframes);
 }
 
 int render_groups(const char* fn, rtx_scene* s, int32_t phase, int32_t stride, void* out_dev, uint64_t* counters_dev,
@@ -1612,6 +1616,7 @@ int render_groups(const char* fn, rtx_scene* s, int32_t phase, int32_t stride, v
     L.nrows = nrows;
     L.gphase = phase;
     L.gstride = stride;
+    L.fstride = 0;
     return render_launch(s, L, counters_dev, stream, out8);
 }
 }  // namespace
@@ -1623,6 +1628,12 @@ int rtx_render(rtx_scene* s, int32_t row0, int32_t nrows, float* fb_dev, uint64_
 int rtx_render_rgb8(rtx_scene* s, int32_t row0, int32_t nrows, uint8_t* out_dev, uint64_t* counters_dev,
                     void* stream) {
     return render_rows("rtx_render_rgb8", s, row0, nrows, out_dev, counters_dev, stream, true);
+}
+
+int rtx_render_frames(rtx_scene* s, int32_t row0, int32_t nrows, void* out_dev, int32_t rgb8, int32_t nframes,
+                      int64_t frame_stride_bytes, uint64_t* counters_dev, void* stream) {
+    return render_rows("rtx_render_frames", s, row0, nrows, out_dev, counters_dev, stream, rgb8 != 0, nframes,
+                       frame_stride_bytes);
 }
 
 int32_t rtx_group_rows(int32_t height, int32_t phase, int32_t stride) {
@@ -1655,7 +1666,7 @@ int launch_to_rgb8(const float* fb, uint8_t* out, int64_t n, hipStream_t st) {
     return RTX_OK;
 }
 
-int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, bool out8) {
+int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, bool out8, int32_t nframes) {
     const int32_t nrows = L.nrows;
     int cur = -1;
     if (hipGetDevice(&cur) != hipSuccess || cur != s->device)
@@ -1688,9 +1699,19 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
     }
     if (rs.fn && jit_enabled()) {
         void* args[] = {(void*)&kp, (void*)&L};
-        RTX_HIP(hipModuleLaunchKernel(rs.fn, (unsigned)nblocks, 1, 1, blk, 1, 1,
+        RTX_HIP(hipModuleLaunchKernel(rs.fn, (unsigned)nblocks, (unsigned)nframes, 1, blk, 1, 1,
                                       s->has_ext ? (unsigned)(hbytes * blk) : 0u, st, args, nullptr));
         s->last_kernel = rs.name;
+        return RTX_OK;
+    }
+    if (out8 && nframes > 1) {  // generic kernels: the uint8 fallback below, one frame at a time
+        char* base = reinterpret_cast<char*>(L.fb);
+        const int64_t fstride = L.fstride;
+        L.fstride = 0;
+        for (int32_t f = 0; f < nframes; ++f) {
+            L.fb = reinterpret_cast<float*>(base + f * fstride);
+            if (int rc = render_launch(s, L, counters_dev, stream, true, 1)) return rc;
+        }
         return RTX_OK;
     }
     if (out8) {  // no specialized uint8 kernel: fp32 into the scene's scratch, then convert
@@ -1714,7 +1735,7 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
              (spp_mode && s->has_ext) ? "_spp" : "");
     s->last_kernel = gname;
     if (s->has_ext) {  // precompiled in rtx_kern_ext_m{0,1}.hip
-        const RenderLaunch rl{kp, (unsigned)nblocks, hbytes * kBlock<true>, st, spp_mode};
+        const RenderLaunch rl{kp, (unsigned)nblocks, (unsigned)nframes, hbytes * kBlock<true>, st, spp_mode};
         RTX_HIP(s->has_mesh ? launch_render_ext_m1(sel, rl, L) : launch_render_ext_m0(sel, rl, L));
         return RTX_OK;
     }
@@ -1722,7 +1743,8 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
     // are reached through the scene-specialized kernels only)
     if (spp_mode) nblocks = blocks(false);
 #define RTX_LAUNCH(M, S, C, J) \
-    hipLaunchKernelGGL((k_render<M, S, false, C, J>), dim3((unsigned)nblocks), dim3(kBlock<false>), 0, st, kp, L)
+    hipLaunchKernelGGL((k_render<M, S, false, C, J>), dim3((unsigned)nblocks, (unsigned)nframes), dim3(kBlock<false>), \
+                       0, st, kp, L)
 #define RTX_CASE(n) \
     case n: RTX_LAUNCH(((n) & 16) != 0, ((n) & 8) != 0, ((n) & 2) != 0, ((n) & 1) != 0); break
     switch (sel) {

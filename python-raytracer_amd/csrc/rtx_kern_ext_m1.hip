@@ -12,10 +12,10 @@ hipError_t launch_render_ext_m1(int sel, const RenderLaunch& r, const Launch& L)
     constexpr int B = kBlock<true>;
 #define RTX_EXT_LAUNCH(S, C, J)                                                                          \
     if (r.spp)                                                                                           \
-        hipLaunchKernelGGL((k_render_spp<true, S, true, C, J>), dim3(r.nblocks), dim3(B), r.lds_bytes,  \
+        hipLaunchKernelGGL((k_render_spp<true, S, true, C, J>), dim3(r.nblocks, r.nframes), dim3(B), r.lds_bytes,  \
                            r.stream, r.kp, L);                                                           \
     else                                                                                                 \
-        hipLaunchKernelGGL((k_render<true, S, true, C, J>), dim3(r.nblocks), dim3(B), r.lds_bytes,      \
+        hipLaunchKernelGGL((k_render<true, S, true, C, J>), dim3(r.nblocks, r.nframes), dim3(B), r.lds_bytes,      \
                            r.stream, r.kp, L)
 #define RTX_EXT_CASE(n) \
     case n: RTX_EXT_LAUNCH(((n) & 8) != 0, ((n) & 2) != 0, ((n) & 1) != 0); break

@@ -165,7 +165,14 @@ struct Launch {
     // gstride > 0 (rtx_render_groups): the block's rows are the 8-row groups gphase,
     // gphase + gstride, ... of the image, packed in order
     int32_t gphase, gstride;
+    // rtx_render_frames: blockIdx.y renders frame y of a batch into fb + y * fstride bytes
+    int64_t fstride;
 };
+
+// This block's framebuffer (frame blockIdx.y of a batched launch; the only frame otherwise).
+__device__ __forceinline__ float* frame_fb(const Launch& L) {
+    return reinterpret_cast<float*>(reinterpret_cast<char*>(L.fb) + (int64_t)blockIdx.y * L.fstride);
+}
 
 // Image row (row 0 = top) of block row rr.
 __host__ __device__ inline int32_t image_row(const Launch& L, int32_t rr) {
@@ -297,7 +304,7 @@ __device__ __forceinline__ void render_body(const KParams* __restrict__ Pp, cons
         const int32_t bin = RTX_TILE == 1 ? primary_bin(Pp->S, image_row(L, px.r & ~7), px.c & ~7) : -1;
         // render_pixel's image row is row0 + rr: pass the image row of px.r as that sum
         if (active)
-            render_pixel<MESH, SEC, X, COUNT, JIT>(*Pp, L.fb, image_row(L, px.r) - px.r, px.r, px.c, tl, fs, hs, bin);
+            render_pixel<MESH, SEC, X, COUNT, JIT>(*Pp, frame_fb(L), image_row(L, px.r) - px.r, px.r, px.c, tl, fs, hs, bin);
     }
     flush_tally<COUNT>(tl, L.counters, any_active);
 }
@@ -375,7 +382,7 @@ __device__ __forceinline__ void render_body_spp(const KParams* __restrict__ Pp, 
                     const float* src = sbuf + ch * B + pp * S;
                     float a = 0.0f;
                     for (int k = 0; k < S; ++k) a += src[k];
-                    put_channel(L.fb, 3 * (pix0 + pp) + ch, sample_mean(P, a));
+                    put_channel(frame_fb(L), 3 * (pix0 + pp) + ch, sample_mean(P, a));
                 }
             }
         } else if (tid < 3) {  // this round's samples of the block's pixel
@@ -385,7 +392,7 @@ __device__ __forceinline__ void render_body_spp(const KParams* __restrict__ Pp, 
         }
         if (rounds > 1) __syncthreads();  // sbuf is reused by the next round
     }
-    if (rounds > 1 && tid < 3 && pix0 < npix) put_channel(L.fb, 3 * pix0 + tid, sample_mean(P, acc));
+    if (rounds > 1 && tid < 3 && pix0 < npix) put_channel(frame_fb(L), 3 * pix0 + tid, sample_mean(P, acc));
     flush_tally<COUNT>(tl, L.counters, any_active);
 }
 

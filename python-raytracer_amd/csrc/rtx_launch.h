@@ -12,6 +12,7 @@ struct Launch;
 struct RenderLaunch {
     const KParams* kp;
     unsigned nblocks;
+    unsigned nframes;  // gridDim.y: frames of a batched launch (rtx_render_frames)
     size_t lds_bytes;  // dynamic LDS (hierarchy stacks)
     hipStream_t stream;
     bool spp;          // sample-parallel mapping (render_body_spp)

@@ -206,11 +206,14 @@ class FrameExchange:
     submitted (this rank's rows of each, uint8, fused, into the group's send buffer), then
     its exchange starts asynchronously and the previous group's exchange is awaited (a
     stream wait on RCCL), so an exchange overlaps the next group's renders. Two group
-    buffers. ``graph=True`` records the N renders of each buffer once as a HIP graph and
-    replays it per group: one launch per group instead of N, which keeps the host ahead of
-    renders that take a few microseconds at N = 8 (needs a render_block that does not
-    depend on k, like the bench's static frame). ``flush`` renders and exchanges a partial
-    last group (uneven splits: no rows for the frames that were not submitted).
+    buffers. With the default renderer on row blocks a group is ONE launch
+    (``Scene.render_frames``: gridDim.y = frames), which both keeps the host ahead (a
+    Python render call costs ~9 us of host time, a 1/8-frame render ~3.5 us of GPU time)
+    and fills the GPU that one 1/N-frame launch leaves partly idle. Otherwise
+    ``graph=True`` records the N renders of each buffer once as a HIP graph and replays it
+    per group (needs a render_block that does not depend on k, like the bench's static
+    frame). ``flush`` renders and exchanges a partial last group (uneven splits: no rows
+    for the frames that were not submitted).
 
     ``render_block(out, rows, k)`` fills this rank's uint8 rows [len(rows), W, 3] of frame
     k (the CPU tests inject the host emulation). ``step`` and ``flush`` return the list
@@ -236,6 +239,8 @@ class FrameExchange:
         for r, rws in enumerate(self.rows_all):
             src[rws] = r * self.maxrows + np.arange(len(rws))
         self.index = torch.as_tensor(src, device=device)
+        # the default renderer on row blocks renders a group in ONE launch (rtx_render_frames)
+        self.render_frames = None
         if render_block is None:
             if interleave:
                 def render_block(out, rows, k):
@@ -245,8 +250,12 @@ class FrameExchange:
 
                 def render_block(out, rows, k):
                     scene.render_device(row0=r0, nrows=n, out=out)
+
+                def render_frames(out):
+                    scene.render_frames(out, row0=r0, nrows=n)
+                self.render_frames = render_frames
         self.render_block = render_block
-        self.graph = graph and device.type == "cuda"
+        self.graph = graph and device.type == "cuda" and self.render_frames is None
         self.graphs = [None, None]
         if self.graph:
             self.capture()
@@ -257,6 +266,9 @@ class FrameExchange:
         """Render this rank's rows of frames first .. first + nframes - 1 into slots
         0 .. nframes - 1 of buffer ``buf`` (a graph replay for a full group in graph mode)."""
         if not self.nrows:
+            return
+        if self.render_frames is not None:
+            self.render_frames(self.send[buf][:nframes])
             return
         if self.graph and nframes == self.world:
             if self.graphs[buf] is None:

@@ -530,3 +530,33 @@ def test_light_grids_equal_walk(case, tmp_path, monkeypatch):
     assert torch.equal(a, b)
     img = np.ascontiguousarray(np.transpose(a.cpu().numpy()[::-1], (1, 0, 2))).astype(np.float64)
     assert_parity(img, oracle_render_dict(d), case)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,res,edits", [("TwoSpheresPlane", (120, 67), {}), ("MirrorRefraction", (64, 40), {}),
+                                            ("TorusMesh", (48, 48), {}), ("NovelScene1", (64, 32), {"AA": {"jitter": False, "samples": 2}})])
+@pytest.mark.parametrize("jit", ["1", "0"])
+def test_render_frames_equals_per_frame_renders(name, res, edits, jit, monkeypatch):
+    """rtx_render_frames (one launch, gridDim.y = frames) writes into every slot exactly
+    what rtx_render / rtx_render_rgb8 write for the same rows, for the specialized and the
+    generic kernels; the slots' padding rows stay untouched."""
+    monkeypatch.setenv("RTX_JIT", jit)
+    sc = product_scene(name, res, **edits)
+    H, W = res[1], res[0]
+    for dtype in (torch.uint8, torch.float32):
+        for row0, nrows in ((0, H), (8, H // 3), (3, H // 2 - 1)):
+            want = sc.render_device(row0=row0, nrows=nrows, out=torch.empty((nrows, W, 3), dtype=dtype, device="cuda"))
+            out = torch.full((3, nrows + 5, W, 3), 7, dtype=dtype, device="cuda")
+            sc.render_frames(out, row0=row0, nrows=nrows)
+            kern = sc.last_kernel
+            for f in range(3):
+                assert torch.equal(out[f, :nrows], want), (dtype, row0, nrows, f, kern)
+                assert bool((out[f, nrows:] == 7).all())
+            assert kern.startswith("rtx_jit_render_") == (jit == "1" and name != "NovelScene1"), kern
+    # overlapping frames (stride below one frame's bytes) are refused
+    import ctypes as C
+    from rtx import _native as N
+    buf = torch.empty((8, W, 3), dtype=torch.uint8, device="cuda")
+    with pytest.raises(N.RtxError):
+        N.call("rtx_render_frames", sc._native.h, 0, 4, C.c_void_p(buf.data_ptr()), 1, 2, 4 * W * 3 - 1, None,
+               C.c_void_p(torch.cuda.current_stream().cuda_stream))
