@@ -212,6 +212,9 @@ int rtx_render_groups_rgb8(rtx_scene* scene, int32_t phase, int32_t stride, uint
  * 1/N-of-a-frame launch per rank leaves partly idle at N = 8. 1 <= nframes <= 65535. */
 int rtx_render_frames(rtx_scene* scene, int32_t row0, int32_t nrows, void* out_dev, int32_t rgb8, int32_t nframes,
                       int64_t frame_stride_bytes, uint64_t* counters_dev, void* hip_stream);
+/* The same for rtx_render_groups / rtx_render_groups_rgb8 (interleaved 8-row groups). */
+int rtx_render_groups_frames(rtx_scene* scene, int32_t phase, int32_t stride, void* out_dev, int32_t rgb8,
+                             int32_t nframes, int64_t frame_stride_bytes, uint64_t* counters_dev, void* hip_stream);
 
 /* Rows rtx_render_groups writes for an image of `height` rows (-1: bad arguments). */
 int32_t rtx_group_rows(int32_t height, int32_t phase, int32_t stride);

@@ -1603,11 +1603,14 @@ int render_rows(const char* fn, rtx_scene* s, int32_t row0, int32_t nrows, void*
 }
 
 int render_groups(const char* fn, rtx_scene* s, int32_t phase, int32_t stride, void* out_dev, uint64_t* counters_dev,
-                  void* stream, bool out8) {
+                  void* stream, bool out8, int32_t nframes = 1, int64_t fstride = 0) {
     if (!s) return fail(RTX_ERR_INVALID, std::string(fn) + ": null scene");
     if (!s->cam_set) return fail(RTX_ERR_STATE, std::string(fn) + ": rtx_camera_set was not called");
     const int32_t nrows = rtx_group_rows(s->kp.height, phase, stride);
     if (nrows < 0) return fail(RTX_ERR_INVALID, std::string(fn) + ": need 0 <= phase < stride");
+    const int64_t block_bytes = (int64_t)nrows * s->kp.ncols * 3 * (out8 ? 1 : 4);
+    if (nframes < 1 || nframes > 65535 || (nframes > 1 && fstride < block_bytes) || (!out8 && fstride % 4))
+        return fail(RTX_ERR_INVALID, std::string(fn) + ": need 1 <= nframes <= 65535 and frames that do not overlap");
     if (nrows == 0) return RTX_OK;
     if (!out_dev) return fail(RTX_ERR_INVALID, std::string(fn) + ": null framebuffer");
     Launch L;
@@ -1616,8 +1619,8 @@ int render_groups(const char* fn, rtx_scene* s, int32_t phase, int32_t stride, v
     L.nrows = nrows;
     L.gphase = phase;
     L.gstride = stride;
-    L.fstride = 0;
-    return render_launch(s, L, counters_dev, stream, out8);
+    L.fstride = nframes > 1 ? fstride : 0;
+    return render_launch(s, L, counters_dev, stream, out8, nframes);
 }
 }  // namespace
 
@@ -1634,6 +1637,12 @@ int rtx_render_frames(rtx_scene* s, int32_t row0, int32_t nrows, void* out_dev, 
                       int64_t frame_stride_bytes, uint64_t* counters_dev, void* stream) {
     return render_rows("rtx_render_frames", s, row0, nrows, out_dev, counters_dev, stream, rgb8 != 0, nframes,
                        frame_stride_bytes);
+}
+
+int rtx_render_groups_frames(rtx_scene* s, int32_t phase, int32_t stride, void* out_dev, int32_t rgb8,
+                             int32_t nframes, int64_t frame_stride_bytes, uint64_t* counters_dev, void* stream) {
+    return render_groups("rtx_render_groups_frames", s, phase, stride, out_dev, counters_dev, stream, rgb8 != 0,
+                         nframes, frame_stride_bytes);
 }
 
 int32_t rtx_group_rows(int32_t height, int32_t phase, int32_t stride) {

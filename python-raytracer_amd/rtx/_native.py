@@ -87,7 +87,8 @@ _lib = None
 
 EXPORTS = ["rtx_abi_version", "rtx_last_error", "rtx_scene_create", "rtx_scene_destroy", "rtx_camera_set",
            "rtx_render", "rtx_render_groups", "rtx_group_rows", "rtx_intersect", "rtx_occluded", "rtx_fb_to_rgb8",
-           "rtx_render_rgb8", "rtx_render_groups_rgb8", "rtx_last_kernel", "rtx_render_frames"]
+           "rtx_render_rgb8", "rtx_render_groups_rgb8", "rtx_last_kernel", "rtx_render_frames",
+           "rtx_render_groups_frames"]
 
 
 def load():
@@ -111,6 +112,8 @@ def load():
         lib.rtx_render_rgb8.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp]
         lib.rtx_render_groups_rgb8.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp]
         lib.rtx_render_frames.argtypes = [vp, C.c_int32, C.c_int32, vp, C.c_int32, C.c_int32, C.c_int64, vp, vp]
+        lib.rtx_render_groups_frames.argtypes = [vp, C.c_int32, C.c_int32, vp, C.c_int32, C.c_int32, C.c_int64, vp,
+                                                 vp]
         lib.rtx_group_rows.argtypes = [C.c_int32, C.c_int32, C.c_int32]
         lib.rtx_group_rows.restype = C.c_int32
         lib.rtx_intersect.argtypes = [vp, C.c_int64, vp, vp, C.c_double, vp, vp, vp, vp, vp, vp]

@@ -221,11 +221,9 @@ class FrameExchange:
     receive buffer (block partitions) valid until that buffer's next exchange, two groups
     later."""
 
-    def __init__(self, scene, rank, world, group=None, device=None, render_block=None, interleave=None, graph=False):
+    def __init__(self, scene, rank, world, group=None, device=None, render_block=None, interleave=True, graph=False):
         H, W = scene.vc.height, scene.vc.width
         device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-        if interleave is None:
-            interleave = scene.samples_per_pixel > 1
         self.rank, self.world, self.group, self.interleave = rank, world, group, interleave
         self.rows_all = [rank_rows(H, world, r, interleave) for r in range(world)]
         self.rows = self.rows_all[rank]
@@ -239,12 +237,17 @@ class FrameExchange:
         for r, rws in enumerate(self.rows_all):
             src[rws] = r * self.maxrows + np.arange(len(rws))
         self.index = torch.as_tensor(src, device=device)
-        # the default renderer on row blocks renders a group in ONE launch (rtx_render_frames)
+        # the default renderer renders a group in ONE launch (rtx_render_frames /
+        # rtx_render_groups_frames)
         self.render_frames = None
         if render_block is None:
             if interleave:
                 def render_block(out, rows, k):
                     scene.render_device(groups=(rank, world), out=out)
+
+                def render_frames(out):
+                    scene.render_frames(out, groups=(rank, world))
+                self.render_frames = render_frames
             else:
                 r0, n = row_block(H, world, rank)
 

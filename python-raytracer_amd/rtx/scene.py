@@ -250,12 +250,17 @@ class Scene:
                    C.c_void_p(st.cuda_stream))
         return out
 
-    def render_frames(self, out, row0=0, nrows=None, stream=None):
-        """render_device(row0=row0, nrows=nrows) into out[f, :nrows] for every frame slot f
-        of a contiguous uint8 or float32 CUDA tensor out [nframes, >= nrows, W, 3], in ONE
-        launch (rtx_render_frames: the frames of one scene state, e.g. a group of
+    def render_frames(self, out, row0=0, nrows=None, stream=None, groups=None):
+        """render_device(row0=row0, nrows=nrows) -- or render_device(groups=groups) -- into
+        out[f, :nrows] for every frame slot f of a contiguous uint8 or float32 CUDA tensor
+        out [nframes, >= nrows, W, 3], in ONE launch (rtx_render_frames /
+        rtx_render_groups_frames: the frames of one scene state, e.g. a group of
         rtx.distributed.FrameExchange)."""
         t = self._set_camera(0, 1)
+        if groups is not None:
+            nrows = int(N.load().rtx_group_rows(self.vc.height, int(groups[0]), int(groups[1])))
+            if nrows < 0:
+                raise ValueError("groups=(k, n) needs 0 <= k < n")
         if nrows is None:
             nrows = self.vc.height - row0
         if out.dim() != 4 or out.shape[1] < nrows or tuple(out.shape[2:]) != (t["ncols"], 3) \
@@ -263,9 +268,9 @@ class Scene:
             raise ValueError("out must be a contiguous float32 or uint8 CUDA tensor [frames, >= %d, %d, 3]"
                              % (nrows, t["ncols"]))
         st = stream if stream is not None else torch.cuda.current_stream()
-        N.call("rtx_render_frames", self._native.h, int(row0), int(nrows), C.c_void_p(out.data_ptr()),
-               int(out.dtype == torch.uint8), int(out.shape[0]), int(out.stride(0) * out.element_size()), None,
-               C.c_void_p(st.cuda_stream))
+        fn, a, b = ("rtx_render_frames", row0, nrows) if groups is None else ("rtx_render_groups_frames",) + tuple(groups)
+        N.call(fn, self._native.h, int(a), int(b), C.c_void_p(out.data_ptr()), int(out.dtype == torch.uint8),
+               int(out.shape[0]), int(out.stride(0) * out.element_size()), None, C.c_void_p(st.cuda_stream))
         return out
 
     def render(self, subimage: int = 0, tasks: int = 1) -> np.ndarray:

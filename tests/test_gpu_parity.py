@@ -553,6 +553,15 @@ def test_render_frames_equals_per_frame_renders(name, res, edits, jit, monkeypat
                 assert torch.equal(out[f, :nrows], want), (dtype, row0, nrows, f, kern)
                 assert bool((out[f, nrows:] == 7).all())
             assert kern.startswith("rtx_jit_render_") == (jit == "1" and name != "NovelScene1"), kern
+        for k, n in ((0, 1), (1, 3), (2, 3)):  # interleaved 8-row groups (rtx_render_groups_frames)
+            want = sc.render_device(groups=(k, n), rgb8=dtype == torch.uint8)
+            if dtype == torch.float32:
+                want = sc.render_device(groups=(k, n))
+            out = torch.full((2, want.shape[0] + 3, W, 3), 7, dtype=dtype, device="cuda")
+            sc.render_frames(out, groups=(k, n))
+            for f in range(2):
+                assert torch.equal(out[f, :want.shape[0]], want), (dtype, k, n, f, sc.last_kernel)
+                assert bool((out[f, want.shape[0]:] == 7).all())
     # overlapping frames (stride below one frame's bytes) are refused
     import ctypes as C
     from rtx import _native as N
