@@ -6,10 +6,10 @@ The unit is the reference's: primary samples W*H*aa*dof*|times| per second (its 
 provided/scene.py:45,71). One step = one 1920x1080 1-spp frame of TwoSpheresPlane.
 N = 1: the frame is rendered into the fp32 framebuffer on one GPU.
 N > 1 (north star, "scaling": "strong"): every frame is split across the ranks — each
-renders its rows straight to uint8 on its GPU (row blocks for 1-spp frames, interleaved
-8-row groups otherwise) — and gathered to ONE rank over RCCL: frame k to rank k mod N
-(rtx.distributed.FrameExchange), the gathers of N consecutive frames issued as one
-all_to_all that overlaps the next N renders. Reported beside it: every frame gathered to
+renders its interleaved 8-row groups straight to uint8 on its GPU — and gathered to ONE
+rank over RCCL: frame k to rank k mod N (rtx.distributed.FrameExchange), the N frames of a
+group rendered in one batched launch and their gathers issued as one all_to_all that
+overlaps the next group's renders. Reported beside it: every frame gathered to
 rank 0 (rtx.distributed.FramePipeline, "gather_to_rank0", bounded by rank 0's ingress)
 and the frame-parallel rate (each rank its own frame, "weak_scaling").
 
@@ -387,7 +387,8 @@ def main():
                           if ex.interleave else "np.array_split row blocks (rtx_render_rgb8), received in image order"),
             "collective": "frame k gathered to rank k mod N; the gathers of N consecutive frames are one "
                           "torch.distributed.all_to_all_single (RCCL), double-buffered",
-            "launch": "eager" if a.no_graph else "one HIP graph of the group's N renders per group",
+            "launch": ("one batched launch per group of N frames (rtx_render_groups_frames)" if ex.render_frames
+                       else "eager" if a.no_graph else "one HIP graph of the group's N renders per group"),
             "gather_to_rank0": {"frame_ms": round(rank0_s * 1e3 / a.steps, 5),
                                 "Mrays_s": round(W * H * spp * a.steps / rank0_s / 1e6, 3),
                                 "note": "FramePipeline: every frame gathered to rank 0 (its ingress bounds the rate)"},
