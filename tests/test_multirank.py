@@ -135,7 +135,8 @@ def _exchange_worker(rank, world, port, name, res, nframes, interleave, out_q):
 
 @pytest.mark.parametrize("world,res,interleave,nframes", [(2, (40, 23), True, 5), (3, (33, 26), True, 7),
                                                           (2, (40, 24), False, 4), (3, (20, 13), False, 2),
-                                                          (4, (24, 20), False, 9), (4, (24, 41), True, 8)])
+                                                          (4, (24, 20), False, 9), (4, (24, 41), True, 8),
+                                                          (4, (16, 20), True, 6)])  # rank 3 has no rows
 def test_frame_exchange_delivers_every_frame_to_its_owner(world, res, interleave, nframes):
     from common import oracle_render
     from oracle import oracle as O
