@@ -1188,6 +1188,8 @@ hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& k
                                      "-DRTX_FIXED_DIVPOW2=" + std::to_string(kp.div_pow2)};
     if (uniform_hard >= 0) opts.push_back("-DRTX_FIXED_HARD=" + std::to_string(uniform_hard));
     if (out8) opts.push_back("-DRTX_OUT8=1");  // uint8 framebuffer (rtx_render_rgb8)
+    // secondary-ray frames keep their material index in a register: 3 LDS words per frame
+    if (sec && v.n_mats <= 64) opts.push_back("-DRTX_FRAME_MATBITS=6");
     opts.push_back(std::string("-DRTX_PRIMARY_BINS=") + (kp.S.bins_on ? "1" : "0"));
     opts.push_back(std::string("-DRTX_LIGHT_GRIDS=") + (v.lgrid_on ? "1" : "0"));
     if (!ext && !spp) {  // experiment: per-lane object / material gathers from LDS (RTX_LDS_RECORDS=1)

@@ -1996,19 +1996,29 @@ RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const 
 // the per-level clamp: colour = clamp(L * tint + child * (1 - tint)). Frames live in a
 // caller-provided store: LDS on the device ([frame][word][thread], conflict-free), a
 // local array in the host emulation.
+// RTX_FRAME_MATBITS > 0 (scene-specialized kernels of scenes with at most
+// 2^RTX_FRAME_MATBITS materials): a frame's material index lives in a register instead,
+// RTX_FRAME_MATBITS bits per level of one 64-bit word, and LDS holds 3 words per frame --
+// 30 instead of 40 KB per 256-thread block, so 5 blocks (20 waves) fit a CU's 160 KB
+// instead of 4.
+#ifndef RTX_FRAME_MATBITS
+#define RTX_FRAME_MATBITS 0
+#endif
+static_assert(RTX_FRAME_MATBITS * kMaxDepth <= 64, "frame materials must fit one 64-bit word");
+constexpr int kFrameWords = RTX_FRAME_MATBITS ? 3 : 4;
 struct FrameStack {
     float* base;
     int stride;
     RTX_HD void put(int k, f3 L, int32_t mat) const {
-        float* p = base + k * 4 * stride;
+        float* p = base + k * kFrameWords * stride;
         p[0] = L.x;
         p[stride] = L.y;
         p[2 * stride] = L.z;
-        p[3 * stride] = __builtin_bit_cast(float, mat);
+        if (!RTX_FRAME_MATBITS) p[3 * stride] = __builtin_bit_cast(float, mat);
     }
     RTX_HD f3 get(int k, int32_t& mat) const {
-        const float* p = base + k * 4 * stride;
-        mat = __builtin_bit_cast(int32_t, p[3 * stride]);
+        const float* p = base + k * kFrameWords * stride;
+        if (!RTX_FRAME_MATBITS) mat = __builtin_bit_cast(int32_t, p[3 * stride]);
         return f3{p[0], p[stride], p[2 * stride]};
     }
 };
@@ -2017,6 +2027,7 @@ template <bool MESH, bool SEC, bool X, bool COUNT>
 RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const FrameStack& fs, const HStack& hs,
                    int32_t bin = -1) {
     int nfr = 0;
+    uint64_t fmats = 0;  // RTX_FRAME_MATBITS: the frames' material indices
     f3 tail = mk(0.0f, 0.0f, 0.0f);
     bool in_shape = false;
     for (int level = 0; level < (SEC ? kMaxDepth : 1); ++level) {
@@ -2053,6 +2064,7 @@ RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const 
             break;
         }
         fs.put(nfr, L, sf.mat);
+        if (RTX_FRAME_MATBITS) fmats |= (uint64_t)(uint32_t)sf.mat << (nfr * RTX_FRAME_MATBITS);
         ++nfr;
         if (tir) break;
         in_shape = m.type == MAT_REFRACTIVE ? !in_shape : false;
@@ -2063,6 +2075,8 @@ RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const 
         for (int k = nfr - 1; k >= 0; --k) {
             int32_t mi;
             const f3 L = fs.get(k, mi);
+            if (RTX_FRAME_MATBITS)
+                mi = (int32_t)((fmats >> (k * RTX_FRAME_MATBITS)) & ((1ull << (RTX_FRAME_MATBITS % 64)) - 1));
             const DMat m = RTX_MAT(S, mi);
             tail = clamp01(add(scale(L, m.tint), scale(tail, m.omt)));
         }
