@@ -292,7 +292,7 @@ __device__ __forceinline__ void render_body(const KParams* __restrict__ Pp, cons
     Tally tl = {};
     // secondary-ray frames: [frame][word][thread] in LDS (40 KB per 256-thread block; 30 KB
     // with RTX_FRAME_MATBITS)
-    __shared__ float frames[SEC ? kMaxDepth * kFrameWords * B : 1];
+    __shared__ float frames[SEC ? kFrameLds * kFrameWords * B : 1];
     extern __shared__ float hstack[];  // X: [level][9][thread] (dynamic size)
     const FrameStack fs{frames + threadIdx.x, B};
     const HStack hs{hstack + threadIdx.x, B};
@@ -343,7 +343,7 @@ __device__ __forceinline__ void render_body_spp(const KParams* __restrict__ Pp, 
     const int rounds = (PPB * S + B - 1) / B;
     const float rS = 1.0f / (float)S, rT = 1.0f / (float)nt, rA = 1.0f / (float)na;
     Tally tl = {};
-    __shared__ float frames[SEC ? kMaxDepth * kFrameWords * B : 1];
+    __shared__ float frames[SEC ? kFrameLds * kFrameWords * B : 1];
     __shared__ float sbuf[3 * B];
     extern __shared__ float hstack[];  // X: [level][9][thread] (dynamic size)
     const FrameStack fs{frames + threadIdx.x, B};

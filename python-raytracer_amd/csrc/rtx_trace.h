@@ -2006,6 +2006,15 @@ RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const 
 #endif
 static_assert(RTX_FRAME_MATBITS * kMaxDepth <= 64, "frame materials must fit one 64-bit word");
 constexpr int kFrameWords = RTX_FRAME_MATBITS ? 3 : 4;
+// Frames kept in LDS; deeper levels of a chain (rare) go to a per-lane private array
+// (scratch), so a smaller LDS stack lets more blocks share a CU. Experiment knob: 8 levels
+// give MirrorRefraction 6 instead of 5 waves/SIMD but measured equal (51.3 vs 50.4-51.1 us,
+// profiles/r02/s19/), so every level stays in LDS.
+#ifndef RTX_FRAME_LDS_LEVELS
+#define RTX_FRAME_LDS_LEVELS kMaxDepth
+#endif
+constexpr int kFrameLds = RTX_FRAME_LDS_LEVELS;
+static_assert(kFrameLds >= 1 && kFrameLds <= kMaxDepth, "RTX_FRAME_LDS_LEVELS out of range");
 struct FrameStack {
     float* base;
     int stride;
@@ -2028,6 +2037,8 @@ RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const 
                    int32_t bin = -1) {
     int nfr = 0;
     uint64_t fmats = 0;  // RTX_FRAME_MATBITS: the frames' material indices
+    f3 deep[kMaxDepth - kFrameLds > 0 ? kMaxDepth - kFrameLds : 1];  // frames kFrameLds.. (private)
+    int32_t deep_mat[kMaxDepth - kFrameLds > 0 ? kMaxDepth - kFrameLds : 1];
     f3 tail = mk(0.0f, 0.0f, 0.0f);
     bool in_shape = false;
     for (int level = 0; level < (SEC ? kMaxDepth : 1); ++level) {
@@ -2063,7 +2074,12 @@ RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const 
             tail = clamp01(L);
             break;
         }
-        fs.put(nfr, L, sf.mat);
+        if (kFrameLds == kMaxDepth || nfr < kFrameLds) {
+            fs.put(nfr, L, sf.mat);
+        } else {
+            deep[nfr - kFrameLds] = L;
+            deep_mat[nfr - kFrameLds] = sf.mat;
+        }
         if (RTX_FRAME_MATBITS) fmats |= (uint64_t)(uint32_t)sf.mat << (nfr * RTX_FRAME_MATBITS);
         ++nfr;
         if (tir) break;
@@ -2074,7 +2090,13 @@ RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const 
     if (SEC) {
         for (int k = nfr - 1; k >= 0; --k) {
             int32_t mi;
-            const f3 L = fs.get(k, mi);
+            f3 L;
+            if (kFrameLds == kMaxDepth || k < kFrameLds) {
+                L = fs.get(k, mi);
+            } else {
+                L = deep[k - kFrameLds];
+                mi = deep_mat[k - kFrameLds];
+            }
             if (RTX_FRAME_MATBITS)
                 mi = (int32_t)((fmats >> (k * RTX_FRAME_MATBITS)) & ((1ull << (RTX_FRAME_MATBITS % 64)) - 1));
             const DMat m = RTX_MAT(S, mi);
