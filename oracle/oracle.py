@@ -74,6 +74,9 @@ def lib():
         _lib.oracle_closest_batch.argtypes = [C.POINTER(_SceneIn), C.c_double, C.c_int, _f, _f,
                                               _d, _i, _i, _i, _f, _f]
         _lib.oracle_shadow_batch.argtypes = [C.POINTER(_SceneIn), C.c_double, C.c_int, _f, _f, _d, _i]
+        _lib.oracle_object_shadow_batch.argtypes = [C.POINTER(_SceneIn), C.c_int, C.c_double, C.c_int, _f, _f,
+                                                    _d, _i]
+        _lib.oracle_object_inside_batch.argtypes = [C.POINTER(_SceneIn), C.c_int, C.c_double, C.c_int, _f, _i]
     return _lib
 
 
@@ -410,6 +413,33 @@ class OracleScene:
         lib().oracle_shadow_batch(C.byref(self.s), float(time), len(o), o.ctypes.data_as(_f),
                                   d.ctypes.data_as(_f), tm.ctypes.data_as(_d), occ.ctypes.data_as(_i))
         return occ
+
+
+    @property
+    def roots(self):
+        """Record indices of the top-level objects (Scene.objects order)."""
+        return [i for i, r in enumerate(self.records) if r["parent"] == -1]
+
+    def object_shadow(self, obj, time, o, d, t_max):
+        """obj.shadow_intersect(ray_i, t_max_i) for n rays (record index obj)."""
+        o = np.ascontiguousarray(o, np.float32).reshape(-1, 3); d = np.ascontiguousarray(d, np.float32).reshape(-1, 3)
+        tm = np.ascontiguousarray(np.broadcast_to(np.asarray(t_max, np.float64), (len(o),)))
+        occ = np.zeros(len(o), np.int32)
+        rc = lib().oracle_object_shadow_batch(C.byref(self.s), obj, float(time), len(o), o.ctypes.data_as(_f),
+                                              d.ctypes.data_as(_f), tm.ctypes.data_as(_d), occ.ctypes.data_as(_i))
+        if rc != 0:
+            raise IndexError("object %d" % obj)
+        return occ.astype(bool)
+
+    def object_inside(self, obj, time, p):
+        """obj.is_inside(p_i) for n points (record index obj)."""
+        p = np.ascontiguousarray(p, np.float32).reshape(-1, 3)
+        out = np.zeros(len(p), np.int32)
+        rc = lib().oracle_object_inside_batch(C.byref(self.s), obj, float(time), len(p), p.ctypes.data_as(_f),
+                                              out.ctypes.data_as(_i))
+        if rc != 0:
+            raise IndexError("object %d" % obj)
+        return out.astype(bool)
 
 
 def to_png_array(image):

@@ -1323,4 +1323,33 @@ int oracle_shadow_batch(const oracle_scene_in* in, double time, int n, const flo
     return 0;
 }
 
+/* Geometry.shadow_intersect / Geometry.is_inside of ONE object (KAT vectors), n rays /
+ * points at one motion time: occluded[i] = obj.shadow_intersect(ray_i, t_max[i]),
+ * inside[i] = obj.is_inside(p_i) (geometry/__init__.py:50-54, simple_geometry.py,
+ * mesh.py, hierarchy.py). */
+int oracle_object_shadow_batch(const oracle_scene_in* in, int obj, double time, int n, const float* o,
+                               const float* d, const double* t_max, int* occluded) {
+    scene_t* sc = scene_build(in);
+    if (obj < 0 || obj >= sc->n_objs) { scene_free(sc); return -1; }
+    sc->current_time = time;
+    for (int i = 0; i < n; i++) {
+        ray_t ray;
+        ray.origin = V3(o[3 * i], o[3 * i + 1], o[3 * i + 2]);
+        ray.direction = V3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
+        occluded[i] = obj_shadow(sc, obj, &ray, t_max[i]) ? 1 : 0;
+    }
+    scene_free(sc);
+    return 0;
+}
+
+int oracle_object_inside_batch(const oracle_scene_in* in, int obj, double time, int n, const float* p,
+                               int* inside) {
+    scene_t* sc = scene_build(in);
+    if (obj < 0 || obj >= sc->n_objs) { scene_free(sc); return -1; }
+    sc->current_time = time;
+    for (int i = 0; i < n; i++) inside[i] = obj_is_inside(sc, obj, V3(p[3 * i], p[3 * i + 1], p[3 * i + 2])) ? 1 : 0;
+    scene_free(sc);
+    return 0;
+}
+
 int oracle_abi_version(void) { return 1; }

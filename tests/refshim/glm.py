@@ -1,10 +1,15 @@
 """Test-only stand-in for PyGLM (not installed in this image), so the reference's own
 Python modules can be imported in this container to build reference-shaped objects
 (tests/golden/make_refobjects.py). float32 components, GLM operation order:
-dot = (x*x + y*y) + z*z, normalize = v * (1 / sqrt(dot(v, v))). Only what
-/root/reference/provided calls at scene-construction time is needed to be exact; the
-render-time functions are included so the modules import and run.
+dot = (x*x + y*y) + z*z, normalize = v * (1 / sqrt(dot(v, v))). Every function the
+reference calls is restated from GLM 0.9.9's generic code (which PyGLM wraps) with its
+operation order, so the reference can also RENDER here to produce golden vectors
+(tests/golden/make_refvectors.py): vec/mat arithmetic componentwise in fp32, mat4 * vec4
+as (m0 x + m1 y) + (m2 z + m3 w), vec4 dot as (x*x + y*y) + (z*z + w*w), rotate with
+libm cosf/sinf of the float angle, inverse by cofactors.
 """
+import ctypes
+import ctypes.util
 import math
 
 import numpy as np
@@ -100,6 +105,9 @@ class vec4(_Vec):
 
 
 class mat4:
+    """GLM mat4 (float). ``m`` holds the matrix row-major as numpy float32: GLM's column
+    c, component k is m[k, c]."""
+
     def __init__(self, diag=1.0):
         self.m = np.eye(4, dtype=f32) * f32(diag)
 
@@ -110,14 +118,21 @@ class mat4:
         return o
 
     def __mul__(self, o):
-        if isinstance(o, mat4):
-            return mat4._wrap(self.m @ o.m)
-        return vec4._wrap(self.m @ o.a)
+        m = self.m
+        if isinstance(o, mat4):  # Result[i] = ((m1[0] * m2[i][0] + m1[1] * m2[i][1]) + m1[2] * m2[i][2]) + m1[3] * m2[i][3]
+            r = np.empty((4, 4), f32)
+            for i in range(4):
+                b = o.m[:, i]
+                r[:, i] = ((m[:, 0] * b[0] + m[:, 1] * b[1]) + m[:, 2] * b[2]) + m[:, 3] * b[3]
+            return mat4._wrap(r)
+        v = o.a  # GLM mat4 * vec4: (m[0] * v.x + m[1] * v.y) + (m[2] * v.z + m[3] * v.w)
+        return vec4._wrap((m[:, 0] * v[0] + m[:, 1] * v[1]) + (m[:, 2] * v[2] + m[:, 3] * v[3]))
 
 
 def dot(a, b):
+    """GLM compute_dot: vec3 (x + y) + z, vec4 (x + y) + (z + w), in fp32."""
     p = a.a * b.a
-    return float((p[0] + p[1]) + p[2]) if len(p) == 3 else float(((p[0] + p[1]) + p[2]) + p[3])
+    return float((p[0] + p[1]) + p[2]) if len(p) == 3 else float((p[0] + p[1]) + (p[2] + p[3]))
 
 
 def cross(a, b):
@@ -155,12 +170,14 @@ def tan(x):
 
 
 def translate(m, v):
+    """GLM translate: Result[3] = ((m[0] * v[0] + m[1] * v[1]) + m[2] * v[2]) + m[3]."""
     r = m.m.copy()
-    r[:, 3] = m.m[:, 0] * v.a[0] + m.m[:, 1] * v.a[1] + m.m[:, 2] * v.a[2] + m.m[:, 3]
+    r[:, 3] = ((m.m[:, 0] * v.a[0] + m.m[:, 1] * v.a[1]) + m.m[:, 2] * v.a[2]) + m.m[:, 3]
     return mat4._wrap(r)
 
 
 def scale(m, v):
+    """GLM scale: Result[i] = m[i] * v[i] for i < 3, Result[3] = m[3]."""
     r = m.m.copy()
     r[:, 0] *= v.a[0]
     r[:, 1] *= v.a[1]
@@ -168,19 +185,69 @@ def scale(m, v):
     return mat4._wrap(r)
 
 
+_libm = ctypes.CDLL(ctypes.util.find_library("m"))
+_libm.cosf.restype = _libm.sinf.restype = ctypes.c_float
+_libm.cosf.argtypes = _libm.sinf.argtypes = [ctypes.c_float]
+
+
 def rotate(m, angle, axis):
-    c, s = math.cos(angle), math.sin(angle)
-    a = axis.a / np.linalg.norm(axis.a)
-    t = (1 - c) * a
-    r = np.eye(4, dtype=f32)
-    r[0, 0], r[1, 0], r[2, 0] = c + t[0] * a[0], t[0] * a[1] + s * a[2], t[0] * a[2] - s * a[1]
-    r[0, 1], r[1, 1], r[2, 1] = t[1] * a[0] - s * a[2], c + t[1] * a[1], t[1] * a[2] + s * a[0]
-    r[0, 2], r[1, 2], r[2, 2] = t[2] * a[0] + s * a[1], t[2] * a[1] - s * a[0], c + t[2] * a[2]
-    return mat4._wrap(m.m @ r)
+    """GLM 0.9.9 rotate(m, angle, v) with T = float: c = cos(a), s = sin(a) on the float
+    angle (libm cosf / sinf), axis = normalize(v), temp = (1 - c) * axis, and
+    Result[i] = (m[0] * R[i][0] + m[1] * R[i][1]) + m[2] * R[i][2]."""
+    a = f32(angle)
+    c, s = f32(_libm.cosf(a)), f32(_libm.sinf(a))
+    ax = normalize(axis).a
+    t = (f32(1) - c) * ax
+    R = [[c + t[0] * ax[0], t[0] * ax[1] + s * ax[2], t[0] * ax[2] - s * ax[1]],
+         [t[1] * ax[0] - s * ax[2], c + t[1] * ax[1], t[1] * ax[2] + s * ax[0]],
+         [t[2] * ax[0] + s * ax[1], t[2] * ax[1] - s * ax[0], c + t[2] * ax[2]]]
+    r = m.m.copy()
+    for i in range(3):
+        r[:, i] = (m.m[:, 0] * R[i][0] + m.m[:, 1] * R[i][1]) + m.m[:, 2] * R[i][2]
+    return mat4._wrap(r)
 
 
 def inverse(m):
-    return mat4._wrap(np.linalg.inv(m.m.astype(np.float64)))
+    """GLM 0.9.9 compute_inverse<4, 4> (cofactors, then * (1 / determinant)), in fp32."""
+    g = [[f32(m.m[k, c]) for k in range(4)] for c in range(4)]  # g[column][component]
+    c00 = g[2][2] * g[3][3] - g[3][2] * g[2][3]
+    c02 = g[1][2] * g[3][3] - g[3][2] * g[1][3]
+    c03 = g[1][2] * g[2][3] - g[2][2] * g[1][3]
+    c04 = g[2][1] * g[3][3] - g[3][1] * g[2][3]
+    c06 = g[1][1] * g[3][3] - g[3][1] * g[1][3]
+    c07 = g[1][1] * g[2][3] - g[2][1] * g[1][3]
+    c08 = g[2][1] * g[3][2] - g[3][1] * g[2][2]
+    c10 = g[1][1] * g[3][2] - g[3][1] * g[1][2]
+    c11 = g[1][1] * g[2][2] - g[2][1] * g[1][2]
+    c12 = g[2][0] * g[3][3] - g[3][0] * g[2][3]
+    c14 = g[1][0] * g[3][3] - g[3][0] * g[1][3]
+    c15 = g[1][0] * g[2][3] - g[2][0] * g[1][3]
+    c16 = g[2][0] * g[3][2] - g[3][0] * g[2][2]
+    c18 = g[1][0] * g[3][2] - g[3][0] * g[1][2]
+    c19 = g[1][0] * g[2][2] - g[2][0] * g[1][2]
+    c20 = g[2][0] * g[3][1] - g[3][0] * g[2][1]
+    c22 = g[1][0] * g[3][1] - g[3][0] * g[1][1]
+    c23 = g[1][0] * g[2][1] - g[2][0] * g[1][1]
+    f0, f1, f2 = [c00, c00, c02, c03], [c04, c04, c06, c07], [c08, c08, c10, c11]
+    f3, f4, f5 = [c12, c12, c14, c15], [c16, c16, c18, c19], [c20, c20, c22, c23]
+    v0 = [g[1][0], g[0][0], g[0][0], g[0][0]]
+    v1 = [g[1][1], g[0][1], g[0][1], g[0][1]]
+    v2 = [g[1][2], g[0][2], g[0][2], g[0][2]]
+    v3 = [g[1][3], g[0][3], g[0][3], g[0][3]]
+    sa, sb = [f32(1), f32(-1), f32(1), f32(-1)], [f32(-1), f32(1), f32(-1), f32(1)]
+    inv = [[None] * 4 for _ in range(4)]
+    for k in range(4):
+        inv[0][k] = ((v1[k] * f0[k] - v2[k] * f1[k]) + v3[k] * f2[k]) * sa[k]
+        inv[1][k] = ((v0[k] * f0[k] - v2[k] * f3[k]) + v3[k] * f4[k]) * sb[k]
+        inv[2][k] = ((v0[k] * f1[k] - v1[k] * f3[k]) + v3[k] * f5[k]) * sa[k]
+        inv[3][k] = ((v0[k] * f2[k] - v1[k] * f4[k]) + v2[k] * f5[k]) * sb[k]
+    d = [g[0][k] * inv[k][0] for k in range(4)]
+    one_over = f32(1) / ((d[0] + d[1]) + (d[2] + d[3]))
+    r = np.empty((4, 4), f32)
+    for c in range(4):
+        for k in range(4):
+            r[k, c] = inv[c][k] * one_over
+    return mat4._wrap(r)
 
 
 def transpose(m):
