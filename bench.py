@@ -356,6 +356,23 @@ def main():
             pipe.step()
         pipe.flush()
         rank0_s = run_frames(pipe, a.steps)
+        # one frame at a time (no batching across frames, no overlap): this rank's rows of
+        # the frame, uint8 (fused), then the gather to rank 0, awaited -- the latency of one
+        # sharded frame
+        from rtx.distributed import FrameGather
+        single = FrameGather(H, W, 3, world, rank, torch.uint8, torch.device("cuda", local), interleave=True, dst=0)
+
+        def one_frame():
+            if single.nrows:
+                sc.render_device(groups=(rank, world), out=single.block, stream=stream)
+            w = single.start(async_op=True)
+            if w is not None:
+                w.wait()
+            if rank == 0:
+                single.frame()
+        for _ in range(a.warmup):
+            one_frame()
+        single_s = timed(one_frame, a.steps, use_dist)
         # breakdown (outside the timed region): this rank's render + uint8 conversion, and
         # one group exchange alone, each from HIP events on the launch stream
         rank_fb = torch.empty((ex.nrows, W, 3), dtype=torch.float32, device="cuda")
@@ -392,6 +409,15 @@ def main():
             "gather_to_rank0": {"frame_ms": round(rank0_s * 1e3 / a.steps, 5),
                                 "Mrays_s": round(W * H * spp * a.steps / rank0_s / 1e6, 3),
                                 "note": "FramePipeline: every frame gathered to rank 0 (its ingress bounds the rate)"},
+            "single_frame": {"frame_ms": round(single_s * 1e3 / a.steps, 5),
+                             "Mrays_s": round(W * H * spp * a.steps / single_s / 1e6, 3),
+                             "note": "latency of ONE sharded frame: each rank renders its interleaved rows (uint8, "
+                                     "fused) and the frame is gathered to rank 0, awaited, frame by frame (no "
+                                     "batching across frames, no overlap)"},
+            "headline": "frame-stream throughput of one static scene state: frame k sharded over the N ranks and "
+                        "gathered to rank k mod N; a group of N frames is rendered in ONE batched launch per rank "
+                        "and exchanged by one all_to_all, overlapped with the next group (see single_frame for "
+                        "one frame's latency)",
         }
         # secondary: weak scaling (each rank renders its own whole frame per step)
         for _ in range(3):

@@ -1185,7 +1185,8 @@ hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& k
                                      "-DRTX_FIXED_STATIC=" + std::to_string(any_speed ? 0 : 1),
                                      "-DRTX_FIXED_LDIR=" + std::to_string(ldir) + "u",
                                      "-DRTX_FIXED_POWBITS=" + std::to_string(v.pow_bits),
-                                     "-DRTX_FIXED_DIVPOW2=" + std::to_string(kp.div_pow2)};
+                                     "-DRTX_FIXED_DIVPOW2=" + std::to_string(kp.div_pow2),
+                                     "-DRTX_FIXED_JMODE=" + std::to_string(kp.jitter)};
     if (uniform_hard >= 0) opts.push_back("-DRTX_FIXED_HARD=" + std::to_string(uniform_hard));
     if (out8) opts.push_back("-DRTX_OUT8=1");  // uint8 framebuffer (rtx_render_rgb8)
     // secondary-ray frames keep their material index in a register: 3 LDS words per frame

@@ -70,22 +70,52 @@ RTX_HD f3 pixel_focal(const KParams& P, int32_t cc, int j) {
     return add(ld3(P.pos), scale(bdir, P.focal));  // scene.py:55
 }
 
-// scene.py:60-65: the origin of AA sample ka of DOF sample kd, jittered (JIT).
+#ifdef RTX_FIXED_JMODE  // scene-specialized kernels pin the jitter mode
+#define RTX_JMODE(P) RTX_FIXED_JMODE
+#else
+#define RTX_JMODE(P) (P).jitter
+#endif
+
+// Production jitter (RTX_JITTER_PHILOX): sample s = kd * n_aa + ka of pixel (column
+// col0 + cc, reference row j) takes half s & 1 of one Philox4x32-10 block with counter
+// (col0 + cc, j, s >> 1, 0) and the scene's seed: 128 bits -> 6 uniforms of 21 bits,
+// three per sample (half 0: the top 21 bits of words 0-2; half 1: their low 11 bits
+// joined with 10-bit pieces of word 3). Consecutive samples share a block, so a pixel's
+// samples cost half a Philox evaluation each (the render loops keep the block).
+RTX_HD void jitter_block(const KParams& P, int32_t cc, int j, int pair, uint32_t w[4]) {
+    w[0] = (uint32_t)(P.col0 + cc);
+    w[1] = (uint32_t)j;
+    w[2] = (uint32_t)pair;
+    w[3] = 0u;
+    philox4x32(w, P.seed_lo, P.seed_hi);
+}
+RTX_HD f3 jitter_rnd(const uint32_t w[4], int half) {
+    const uint32_t a = half ? ((w[0] & 0x7FFu) | ((w[3] & 0x3FFu) << 11)) : w[0] >> 11;
+    const uint32_t b = half ? ((w[1] & 0x7FFu) | (((w[3] >> 10) & 0x3FFu) << 11)) : w[1] >> 11;
+    const uint32_t c = half ? ((w[2] & 0x7FFu) | (((w[3] >> 20) & 0x3FFu) << 11)) : w[2] >> 11;
+    return mk((float)a * 0x1p-21f, (float)b * 0x1p-21f, (float)c * 0x1p-21f);
+}
+
+// scene.py:60-65: the origin of AA sample ka of DOF sample kd, jittered (JIT). jr: this
+// sample's Philox uniforms when the caller has them (render_pixel keeps the odd sample's
+// from the pair's block), else they are computed here.
 template <bool JIT>
-RTX_HD f3 sample_origin(const KParams& P, int32_t cc, int j, int kd, int ka) {
+RTX_HD f3 sample_origin(const KParams& P, int32_t cc, int j, int kd, int ka, const f3* jr = nullptr) {
     f3 o = ld3(P.aa_o + 3 * (kd * RTX_NAA(P) + ka));
     if (JIT) {  // scene.py:63-65
         f3 rnd;
-        if (P.jitter == RTX_JITTER_REPLAY) {
+        if (RTX_JMODE(P) == RTX_JITTER_REPLAY) {
             const int64_t idx = (((int64_t)cc * P.height + j) * RTX_NDOF(P) + kd) * RTX_NAA(P) + ka;
             rnd = ld3(P.noise + 3 * idx);
         } else if (RTX_ABLATE == 15) {  // cost probe only: no RNG
             rnd = mk(0.25f + 0.001f * (float)ka, 0.5f, 0.75f + 0.001f * (float)kd);
+        } else if (jr != nullptr) {
+            rnd = *jr;
         } else {
-            uint32_t ctr[4] = {(uint32_t)(P.col0 + cc), (uint32_t)j, (uint32_t)(kd * RTX_NAA(P) + ka), 0u};
-            philox4x32(ctr, P.seed_lo, P.seed_hi);
-            rnd = mk((float)(ctr[0] >> 8) * 0x1p-24f, (float)(ctr[1] >> 8) * 0x1p-24f,
-                     (float)(ctr[2] >> 8) * 0x1p-24f);
+            const int s = kd * RTX_NAA(P) + ka;
+            uint32_t w[4];
+            jitter_block(P, cc, j, s >> 1, w);
+            rnd = jitter_rnd(w, s & 1);
         }
         o = add(o, scale(normalize(rnd), P.jscale));
     }
@@ -115,42 +145,100 @@ RTX_HD void put_channel(float* fb, int64_t i, float v) {
         fb[i] = v;
 }
 
+// Multi-sample kernels re-read the scene records in every sample instead of keeping
+// them live across the sample loops: the compiler otherwise hoists every record load and
+// its loop-invariant VALU conversions (fp64 box bounds, padded culling boxes) out of the
+// loops, where they occupy SGPRs and VGPRs for the kernel's whole life and spill (the
+// DepthOfField kernel: 54 SGPRs into VGPR lanes and 176 B/lane of scratch, written once
+// per pixel = 1.46 GB per 4K frame). Re-reads are scalar-cache hits, once per sample.
+#ifndef RTX_RELOAD_RECORDS
+#if defined(RTX_FIXED_SAMPLES)
+#define RTX_RELOAD_RECORDS (RTX_FIXED_NDOF * RTX_FIXED_NAA * RTX_FIXED_NTIMES > 1)
+#else
+#define RTX_RELOAD_RECORDS 1
+#endif
+#endif
+// A wave-uniform pointer the compiler cannot prove loop-invariant (its halves pass through
+// readfirstlane, a no-op on a uniform value, and an empty asm that "redefines" them).
+template <class T>
+__device__ __forceinline__ cptr<T> opaque_uniform(cptr<T> p) {
+    const uint64_t v = (uint64_t)p;
+    uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    asm volatile("" : "+s"(lo), "+s"(hi));
+    return (cptr<T>)(((uint64_t)hi << 32) | lo);
+}
+// (flat-scene kernels only: the hierarchy/texture kernels keep the loaded records)
+template <bool X>
+RTX_HD SceneView sample_scene(const SceneView& S0) {
+    SceneView S = S0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (RTX_RELOAD_RECORDS && !X) {  // opaque to loop-invariant code motion
+        S.objs = opaque_uniform(S.objs);
+        if (RTX_RELOAD_RECORDS > 1) {
+            S.mats = opaque_uniform(S.mats);
+            S.lights = opaque_uniform(S.lights);
+        }
+    }
+#endif
+    return S;
+}
+
 // scene.py:47-79 for pixel p of the output block (host/device: the tests-only host
 // emulation runs the same body).
 template <bool MESH, bool SEC, bool X, bool COUNT, bool JIT>
 RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, int32_t cc, Tally& tl,
                          const FrameStack& fs, const HStack& hs, int32_t bin = -1) {
-    const int64_t p = (int64_t)rr * P.ncols + cc;
     if (RTX_ABLATE == 14) {  // cost probe only: store a constant (launch + framebuffer write)
+        const int64_t p = (int64_t)rr * P.ncols + cc;
         put_channel(fb, 3 * p, 0.5f); put_channel(fb, 3 * p + 1, 0.25f); put_channel(fb, 3 * p + 2, 0.125f);
         return;
     }
     const int j = P.height - 1 - (row0 + rr);  // reference row index (y grows upward)
-    const f3 focal = pixel_focal(P, cc, j);
     f3 colour = mk(0.0f, 0.0f, 0.0f);
+    f3 jr_odd = mk(0.0f, 0.0f, 0.0f);  // the odd sample's jitter uniforms of the current pair
     // pinned counts must not unroll the loops (one cast_ray body per sample)
 #pragma unroll 1
     for (int kd = 0; kd < RTX_NDOF(P); ++kd) {
+        // the focal point is recomputed per DOF sample (the same fp32 operations) rather
+        // than kept live across the loops (RTX_RELOAD_RECORDS)
+        int32_t cc_k = cc, j_k = j;
+#if defined(__HIP_DEVICE_COMPILE__)
+        if (RTX_RELOAD_RECORDS) asm volatile("" : "+v"(cc_k), "+v"(j_k));
+#endif
+        const f3 focal = pixel_focal(P, cc_k, j_k);
         const f3 ddir = normalize(sub(focal, ld3(P.dof_o + 3 * kd)));  // scene.py:58
 #pragma unroll 1
         for (int ka = 0; ka < RTX_NAA(P); ++ka) {
-            const f3 o = sample_origin<JIT>(P, cc, j, kd, ka);
+            // the Philox block of samples (2m, 2m + 1), computed at the even one; the odd
+            // one's uniforms wait in jr
+            const bool philox = JIT && RTX_JMODE(P) == RTX_JITTER_PHILOX && RTX_ABLATE != 15;
+            const bool odd = ((kd * RTX_NAA(P) + ka) & 1) != 0;
+            f3 jr = jr_odd;
+            if (philox && !odd) {
+                uint32_t w[4];
+                jitter_block(P, cc, j, (kd * RTX_NAA(P) + ka) >> 1, w);
+                jr = jitter_rnd(w, 0);
+                jr_odd = jitter_rnd(w, 1);
+            }
+            const f3 o = sample_origin<JIT>(P, cc, j, kd, ka, philox ? &jr : nullptr);
 #pragma unroll 1
             for (int kt = 0; kt < RTX_NTIMES(P); ++kt)
-                colour = add(colour, cast_ray<MESH, SEC, X, COUNT>(P.S, o, ddir, P.times[kt], tl, fs, hs, bin));
+                colour = add(colour, cast_ray<MESH, SEC, X, COUNT>(sample_scene<X>(P.S), o, ddir, P.times[kt], tl, fs, hs,
+                                                                   bin));
         }
     }
     colour = mk(sample_mean(P, colour.x), sample_mean(P, colour.y), sample_mean(P, colour.z));
 #if RTX_ABLATE == 11 && defined(__HIP_DEVICE_COMPILE__)
     {  // cost probe only: RTX_PAD extra VALU instructions per pixel in 4 independent chains
-        float c0 = colour.x, c1 = colour.y, c2 = colour.z, c3 = focal.x;
+        float c0 = colour.x, c1 = colour.y, c2 = colour.z, c3 = (float)cc;
 #pragma unroll
         for (int k = 0; k < RTX_PAD / 4; ++k)
             asm volatile("v_add_f32 %0, %4, %0\n v_add_f32 %1, %4, %1\n v_add_f32 %2, %4, %2\n v_add_f32 %3, %4, %3"
-                         : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3) : "v"(focal.y));
+                         : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3) : "v"((float)j));
         colour = mk(c0, c1, c2 + c3 * 0.0f);
     }
 #endif
+    const int64_t p = (int64_t)rr * P.ncols + cc;
     put_channel(fb, 3 * p, colour.x);
     put_channel(fb, 3 * p + 1, colour.y);
     put_channel(fb, 3 * p + 2, colour.z);

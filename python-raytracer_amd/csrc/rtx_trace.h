@@ -552,6 +552,27 @@ RTX_HD bool box_slabs(f3 o, f3 d, f3 mn, f3 mx, double& start, int& label, doubl
     return true;
 }
 
+RTX_HD float rcp_approx(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(x);
+#else
+    return 1.0f / x;
+#endif
+}
+// Per-ray reciprocals of the direction (v_rcp_f32), shared by the conservative box and
+// cluster tests and the fp32 slab intervals.
+struct RayInv {
+    f3 inv;
+    float pad_rel;
+};
+RTX_HD RayInv ray_inv(f3 o, f3 d) {
+    auto safe = [](float v) { return fabsf(v) < 1e-30f ? copysignf(1e-30f, v) : v; };
+    RayInv r;
+    // v_rcp_f32 (1 ulp): its error moves a slab by <= 2^-23 |bound - o|, far inside the pad
+    r.inv = f3{rcp_approx(safe(d.x)), rcp_approx(safe(d.y)), rcp_approx(safe(d.z))};
+    r.pad_rel = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
+    return r;
+}
 // The same slabs decided in fp32, with box_slabs as the fallback. Each reference quotient
 // t = fl64((bound - o) / d) is estimated as q = fl32(bound - o) * rcp(d): three fp32
 // roundings and v_rcp_f32's 1 ulp give |q - t| <= 2^-22 |q|, so q +- (2^-20 |q| + 2^-100)
@@ -565,18 +586,14 @@ struct SlabIv {
     bool reject;  // certain: a d == 0 slab does not contain the origin (exact comparison)
     bool sure;    // the intervals and the label hold
 };
-RTX_HD float rcp_approx(float x) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    return __builtin_amdgcn_rcpf(x);
-#else
-    return 1.0f / x;
-#endif
-}
-RTX_HD SlabIv box_slabs_iv(f3 o, f3 d, f3 mn, f3 mx) {
+// ri: the ray's reciprocals when the caller has them (the same v_rcp_f32 of every |d| >=
+// 1e-30; smaller slabs are undecided anyway), else they are computed here.
+RTX_HD SlabIv box_slabs_iv(f3 o, f3 d, f3 mn, f3 mx, const RayInv* ri = nullptr) {
     const float ro[3] = {o.x, o.y, o.z};
     const float rd[3] = {d.x, d.y, d.z};
     const float lo[3] = {mn.x, mn.y, mn.z};
     const float hi[3] = {mx.x, mx.y, mx.z};
+    const float rr[3] = {ri ? ri->inv.x : 0.0f, ri ? ri->inv.y : 0.0f, ri ? ri->inv.z : 0.0f};
     float sc[3], ec[3], w[3];
     SlabIv r;
     r.reject = false;
@@ -589,7 +606,7 @@ RTX_HD SlabIv box_slabs_iv(f3 o, f3 d, f3 mn, f3 mx) {
             ec[k] = INFINITY;
             w[k] = 0.0f;
         } else {
-            const float rc = rcp_approx(rd[k]);
+            const float rc = ri ? rr[k] : rcp_approx(rd[k]);
             const float q1 = (lo[k] - ro[k]) * rc, q2 = (hi[k] - ro[k]) * rc;
             sc[k] = fminf(q1, q2);
             ec[k] = fmaxf(q1, q2);
@@ -624,8 +641,8 @@ RTX_HD double slab_start64(f3 o, f3 d, f3 mn, f3 mx, int k) {
 // Box entry as the closest-hit test needs it (simple_geometry.py:188-226: valid iff no
 // zero-direction slab rejects, start <= end and start >= 0): fp32 decision, one fp64
 // division for the entry t, the full fp64 slabs for undecided lanes.
-RTX_HD bool box_entry(f3 o, f3 d, f3 mn, f3 mx, bool live, double& start, int& label) {
-    const SlabIv iv = box_slabs_iv(o, d, mn, mx);
+RTX_HD bool box_entry(f3 o, f3 d, f3 mn, f3 mx, bool live, double& start, int& label, const RayInv* ri = nullptr) {
+    const SlabIv iv = box_slabs_iv(o, d, mn, mx, ri);
     const bool yes = live && iv.sure && !iv.reject && iv.s_hi < iv.e_lo && iv.s_lo > 0.0f;
     const bool no = !live || iv.reject || (iv.sure && (iv.s_lo > iv.e_hi || iv.s_hi < 0.0f));
     label = iv.label;
@@ -642,8 +659,8 @@ RTX_HD bool box_entry(f3 o, f3 d, f3 mn, f3 mx, bool live, double& start, int& l
     return valid;
 }
 // Box shadow test (simple_geometry.py:251-294): 1e-4 < start < t_max and start <= end.
-RTX_HD bool box_shadow(f3 o, f3 d, f3 mn, f3 mx, double t_max) {
-    const SlabIv iv = box_slabs_iv(o, d, mn, mx);
+RTX_HD bool box_shadow(f3 o, f3 d, f3 mn, f3 mx, double t_max, const RayInv* ri = nullptr) {
+    const SlabIv iv = box_slabs_iv(o, d, mn, mx, ri);
     const bool yes = iv.sure && !iv.reject && iv.s_hi < iv.e_lo && iv.s_lo >= kEps4Up && (double)iv.s_hi < t_max;
     const bool no = iv.reject ||
                     (iv.sure && (iv.s_lo > iv.e_hi || iv.s_hi < kEps4Up || (double)iv.s_lo >= t_max));
@@ -684,18 +701,6 @@ RTX_HD bool mesh_bv(const O& ob, f3 o, f3 d) {
 // o + d*t32 inside the triangle up to fp32 rounding, i.e. within ~2^-22 (|o| + cmax) of
 // the cluster box; the box is padded by 2^-16 (|o|_max + cmax) per ray, far above every
 // rounding term, so a cluster is skipped only if none of its faces can pass.
-struct RayInv {
-    f3 inv;
-    float pad_rel;
-};
-RTX_HD RayInv ray_inv(f3 o, f3 d) {
-    auto safe = [](float v) { return fabsf(v) < 1e-30f ? copysignf(1e-30f, v) : v; };
-    RayInv r;
-    // v_rcp_f32 (1 ulp): its error moves a slab by <= 2^-23 |bound - o|, far inside the pad
-    r.inv = f3{rcp_approx(safe(d.x)), rcp_approx(safe(d.y)), rcp_approx(safe(d.z))};
-    r.pad_rel = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
-    return r;
-}
 // tcap: the ray's current best t (closest hit) -- a face beyond it cannot win; the
 // padded box's entry precedes every face hit inside it.
 template <class L_>
@@ -1517,6 +1522,7 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
     Hit h{INFINITY, -1, 0};
     int oi = 0;
     for (int k = 0; k < RTX_NPLANE(S); ++k, ++oi) {  // simple_geometry.py:105-120
+        if (RTX_ABLATE == 18) continue;  // cost probe: no planes in closest_hit
         const DObj ob = S.objs[oi];
         const f3 n = ld3(ob.b);
         const float denom = dot(d, n);
@@ -1556,6 +1562,7 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
     if (RTX_NBOX(S) > 0 || (MESH && RTX_NMESH(S) > 0)) ri = ray_inv(o, d);
     for (int k = 0; k < RTX_NBOX(S); ++k, ++oi) {  // simple_geometry.py:188-249 (entry precedes exit)
         if (!((omask >> (16 + (k & 15))) & 1u)) continue;
+        if (RTX_ABLATE == 17) continue;  // cost probe: no boxes in closest_hit
         const DObj ob = S.objs[oi];
         const f3 mn = moved(ob, ob.a, time), mx = moved(ob, ob.b, time);
         // the fp64 slabs only where some lane's ray may hit the box before its best t
@@ -1563,7 +1570,7 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
         if (!RTX_ANY(maybe)) continue;
         double start = 0.0;
         int label = 0;
-        const bool valid = box_entry(o, d, mn, mx, maybe, start, label);
+        const bool valid = box_entry(o, d, mn, mx, maybe, start, label, &ri);
         offer(S, h, valid, (float)start, oi, label, o, d, time);
     }
     if (MESH) {
@@ -1710,6 +1717,7 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
     bool occ = false;
     int oi = 0;
     for (int k = 0; k < RTX_NPLANE(S); ++k, ++oi) {  // simple_geometry.py:122-131
+        if (RTX_ABLATE == 21) continue;  // cost probe: planes never occlude
         const DObj ob = S.objs[oi];
         const f3 n = ld3(ob.b);
         const float denom = dot(d, n);
@@ -1747,6 +1755,7 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
     }
     if (RTX_ALL(occ)) return true;
     for (int k = 0; k < RTX_NSPHERE(S); ++k, ++oi) {  // simple_geometry.py:48-72 (shadow_epsilon 1e-3)
+        if (RTX_ABLATE == 19) continue;  // cost probe: spheres never occlude
         const DObj ob = S.objs[oi];
         const f3 ctr = moved(ob, ob.a, time);
 #ifdef RTX_FIXED_COUNTS
@@ -1779,11 +1788,12 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
     RayInv ri{};
     if (RTX_NBOX(S) > 0) ri = ray_inv(o, d);  // meshes: only once a lane passes a bounding volume
     for (int k = 0; k < RTX_NBOX(S); ++k, ++oi) {  // simple_geometry.py:251-294
+        if (RTX_ABLATE == 20) continue;  // cost probe: boxes never occlude
         const DObj ob = S.objs[oi];
         const f3 mn = moved(ob, ob.a, time), mx = moved(ob, ob.b, time);
         const bool maybe = !occ && box_maybe_hit(mn, mx, o, ri, INFINITY);
         if (!RTX_ANY(maybe)) continue;
-        if (maybe) occ = box_shadow(o, d, mn, mx, t_max);
+        if (maybe) occ = box_shadow(o, d, mn, mx, t_max, &ri);
     }
     if (MESH) {
         for (int k = 0; k < RTX_NMESH(S); ++k, ++oi) {  // mesh.py:121-153 (no t_max test)

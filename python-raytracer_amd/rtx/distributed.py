@@ -35,39 +35,53 @@ def rank_rows(height, world, rank, interleave):
 class FrameGather:
     """The frame's single collective: every rank sends its packed rows (padded to the
     largest rank's count), rank ``dst`` receives them into one buffer and reorders them
-    into the [height, W, C] frame. Buffers are allocated once and reused per frame."""
+    into the [height, W, C] frame. Buffers are allocated once and reused per frame.
+    ``dst`` renders its own rows in place, into its slot of the receive buffer, and hands
+    that very tensor to the gather as its input (the collective's root copy is then a
+    no-op: ``copy_`` of a tensor onto itself); one rank needs no collective at all."""
 
     def __init__(self, height, width, channels, world, rank, dtype, device, interleave=True, dst=0, group=None):
         self.world, self.rank, self.dst, self.group = world, rank, dst, group
         self.rows = [rank_rows(height, world, r, interleave) for r in range(world)]
         self.nrows = len(self.rows[rank])
         self.maxrows = max(len(r) for r in self.rows)
+        self.height = height
         shape = (self.maxrows, width, channels)
-        self.send = torch.zeros(shape, dtype=dtype, device=device)
-        self.block = self.send[:self.nrows]  # this rank renders (or converts) into it
         # contiguous equal blocks (np.array_split with world | height) arrive in image order:
         # the receive buffer IS the frame, no reorder
         self.in_order = not interleave and height == world * self.maxrows
         if rank == dst:
-            self.recv = torch.empty((world,) + shape, dtype=dtype, device=device)
+            self.recv = torch.zeros((world,) + shape, dtype=dtype, device=device)
             self.recv_list = list(self.recv.unbind(0))
+            self.send = self.recv_list[dst]
             src = np.empty(height, np.int64)  # frame row -> row of recv viewed as [world * maxrows]
             for r, rows in enumerate(self.rows):
                 src[rows] = r * self.maxrows + np.arange(len(rows))
+            self.in_order = self.in_order or bool(np.array_equal(src, np.arange(height)))
             self.index = torch.as_tensor(src, device=device)
+        else:
+            self.send = torch.zeros(shape, dtype=dtype, device=device)
+        self.block = self.send[:self.nrows]  # this rank renders (or converts) into it
 
     def frame(self):
-        """The gathered frame [height, W, C] on ``dst`` (after the gather completed)."""
+        """The gathered frame [height, W, C] on ``dst`` (after the gather completed); a view
+        of the receive buffer when the rows arrive in image order (valid until the buffer's
+        next gather), else a new tensor."""
         flat = self.recv.view((self.world * self.maxrows,) + tuple(self.recv.shape[2:]))
-        return flat if self.in_order else torch.index_select(flat, 0, self.index)
+        return flat[:self.height] if self.in_order else torch.index_select(flat, 0, self.index)
+
+    def start(self, async_op=False):
+        """Issue the gather (None at world 1: nothing to move)."""
+        if self.world == 1:
+            return None
+        if self.rank != self.dst:
+            return dist.gather(self.send, dst=self.dst, group=self.group, async_op=async_op)
+        return dist.gather(self.send, gather_list=self.recv_list, dst=self.dst, group=self.group, async_op=async_op)
 
     def __call__(self):
         """Gather the ranks' blocks; returns the frame on ``dst`` and None elsewhere."""
-        if self.rank != self.dst:
-            dist.gather(self.send, dst=self.dst, group=self.group)
-            return None
-        dist.gather(self.send, gather_list=self.recv_list, dst=self.dst, group=self.group)
-        return self.frame()
+        self.start()
+        return self.frame() if self.rank == self.dst else None
 
 
 def gather_rows(block, height, world, rank, dst=0, group=None, interleave=False):
@@ -136,7 +150,9 @@ class FramePipeline:
     N | height arrive in image order (zero-copy frame). Default: interleave when a pixel
     has several samples (render time dominates), blocks for 1-spp frames (the gather
     dominates). ``render_block(out, rows)`` fills this rank's uint8 rows [len(rows), W, 3];
-    the CPU tests inject the host emulation."""
+    the CPU tests inject the host emulation. A returned frame is a view of a slot's
+    receive buffer when its rows arrive in image order (always at N = 1), valid until that
+    slot is gathered again two steps later -- clone it to keep it."""
 
     def __init__(self, scene, rank, world, dst=0, group=None, device=None, render_block=None, interleave=None):
         H, W = scene.vc.height, scene.vc.width
@@ -161,7 +177,8 @@ class FramePipeline:
         self.prev = None  # (work, slot) of the last submitted frame
 
     def _finish(self, work, slot):
-        work.wait()
+        if work is not None:
+            work.wait()
         return slot.frame() if self.rank == self.dst else None
 
     def render(self):
@@ -175,10 +192,7 @@ class FramePipeline:
         """Submit the next frame; returns the previous frame on ``dst`` (None elsewhere and
         on the first step)."""
         slot = self.render()
-        if self.rank == self.dst:
-            work = dist.gather(slot.send, gather_list=slot.recv_list, dst=self.dst, group=self.group, async_op=True)
-        else:
-            work = dist.gather(slot.send, dst=self.dst, group=self.group, async_op=True)
+        work = slot.start(async_op=True)
         prev, self.prev = self.prev, (work, slot)
         self.k += 1
         return self._finish(*prev) if prev is not None else None
@@ -202,41 +216,62 @@ class FrameExchange:
     every xGMI link of the full mesh carries 1 / N of a frame per group and the exchange
     costs ~1 / N of a gather per frame.
 
+    No rank sends anything to itself: its rows of its OWN frame are rendered straight into
+    the place where the owner assembles that frame, and the collective's split sizes are 0
+    for the rank itself. Per group buffer, one allocation Z of 2N - 1 row slots
+    [maxrows, W, 3]:
+
+        Z[0 : N-1]    this rank's rows of the peers' frames, frame j at slot p(j)
+                      (p(j) = j for j < rank, j - 1 above): the collective's input
+        Z[N-1]        this rank's rows of its own frame
+        Z[N : 2N-1]   the peers' rows of this rank's frame, from rank s at N + p(s):
+                      the collective's output
+
+    so Z[N-1 : 2N-1] holds the owner's whole frame ([N * maxrows] rows) and one
+    index_select puts it in image order. At N = 1 there is no collective at all and the
+    frame is Z[0] itself.
+
     Frames are submitted one per ``step``; a group is rendered once its N frames are
-    submitted (this rank's rows of each, uint8, fused, into the group's send buffer), then
-    its exchange starts asynchronously and the previous group's exchange is awaited (a
-    stream wait on RCCL), so an exchange overlaps the next group's renders. Two group
-    buffers. With the default renderer on row blocks a group is ONE launch
-    (``Scene.render_frames``: gridDim.y = frames), which both keeps the host ahead (a
-    Python render call costs ~9 us of host time, a 1/8-frame render ~3.5 us of GPU time)
-    and fills the GPU that one 1/N-frame launch leaves partly idle. Otherwise
+    submitted (this rank's rows of each, uint8, fused), then its exchange starts
+    asynchronously and the previous group's exchange is awaited (a stream wait on RCCL), so
+    an exchange overlaps the next group's renders. Two group buffers. With the default
+    renderer a full group is ONE launch (``Scene.render_frames``: gridDim.y = N frames into
+    Z[0 : N], all of one scene state -- the bench's static frame), which both keeps the
+    host ahead (a Python render call costs ~9 us of host time, a 1/8-frame render ~3.5 us
+    of GPU time) and fills the GPU that one 1/N-frame launch leaves partly idle. Otherwise
     ``graph=True`` records the N renders of each buffer once as a HIP graph and replays it
     per group (needs a render_block that does not depend on k, like the bench's static
-    frame). ``flush`` renders and exchanges a partial last group (uneven splits: no rows
-    for the frames that were not submitted).
+    frame; the scene's camera is re-checked per group and the graphs are re-recorded when
+    its upload or device state changed; scenes that run the generic kernels stay eager). ``flush``
+    renders and exchanges a partial last group (uneven splits: no rows for the frames that
+    were not submitted).
 
     ``render_block(out, rows, k)`` fills this rank's uint8 rows [len(rows), W, 3] of frame
     k (the CPU tests inject the host emulation). ``step`` and ``flush`` return the list
-    of (k, frame [H, W, 3]) this rank owns that completed; a frame is a view of the
-    receive buffer (block partitions) valid until that buffer's next exchange, two groups
-    later."""
+    of (k, frame [H, W, 3]) this rank owns that completed; a frame is a new tensor, except
+    when the rows already arrive in image order (N = 1, or rank 0 of some partitions):
+    then it is a view of a group buffer, valid until that buffer is rendered again (two
+    groups later) -- clone it to keep it."""
 
     def __init__(self, scene, rank, world, group=None, device=None, render_block=None, interleave=True, graph=False):
         H, W = scene.vc.height, scene.vc.width
         device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-        self.rank, self.world, self.group, self.interleave = rank, world, group, interleave
+        self.scene, self.rank, self.world, self.group, self.interleave = scene, rank, world, group, interleave
         self.rows_all = [rank_rows(H, world, r, interleave) for r in range(world)]
         self.rows = self.rows_all[rank]
         self.nrows = len(self.rows)
         self.maxrows = max(len(r) for r in self.rows_all)
-        self.in_order = not interleave and H == world * self.maxrows
-        shape = (world, self.maxrows, W, 3)
-        self.send = [torch.zeros(shape, dtype=torch.uint8, device=device) for _ in range(2)]
-        self.recv = [torch.empty(shape, dtype=torch.uint8, device=device) for _ in range(2)]
-        src = np.empty(H, np.int64)  # frame row -> row of a receive buffer viewed as [N * maxrows]
-        for r, rws in enumerate(self.rows_all):
-            src[rws] = r * self.maxrows + np.arange(len(rws))
-        self.index = torch.as_tensor(src, device=device)
+        N = world
+        self.Z = [torch.zeros((2 * N - 1, self.maxrows, W, 3), dtype=torch.uint8, device=device) for _ in range(2)]
+        pos = np.empty(H, np.int64)  # frame row -> row of Z[N-1:] viewed as [N * maxrows]
+        for s, rws in enumerate(self.rows_all):
+            base = 0 if s == rank else (1 + self._peer(s)) * self.maxrows
+            pos[rws] = base + np.arange(len(rws))
+        # rows already in image order (N = 1, and the first rank of some partitions): the
+        # frame is a view of Z[N-1:]
+        self.identity = bool(np.array_equal(pos, np.arange(H)))
+        self.H = H
+        self.index = torch.as_tensor(pos, device=device)
         # the default renderer renders a group in ONE launch (rtx_render_frames /
         # rtx_render_groups_frames)
         self.render_frames = None
@@ -247,7 +282,6 @@ class FrameExchange:
 
                 def render_frames(out):
                     scene.render_frames(out, groups=(rank, world))
-                self.render_frames = render_frames
             else:
                 r0, n = row_block(H, world, rank)
 
@@ -256,75 +290,104 @@ class FrameExchange:
 
                 def render_frames(out):
                     scene.render_frames(out, row0=r0, nrows=n)
-                self.render_frames = render_frames
+            self.render_frames = render_frames
         self.render_block = render_block
         self.graph = graph and device.type == "cuda" and self.render_frames is None
         self.graphs = [None, None]
-        if self.graph:
-            self.capture()
+        self._graph_state = None
         self.k = 0
         self.pending = None  # (work, buffer, first frame index, frames) of the last exchange
 
+    def _peer(self, j):
+        """Slot of peer j among this rank's N - 1 peer slots."""
+        return j if j < self.rank else j - 1
+
+    def slot(self, buf, j):
+        """Where this rank renders its rows of frame j of a group (uint8 [nrows, W, 3])."""
+        i = self.world - 1 if j == self.rank else self._peer(j)
+        return self.Z[buf][i, :self.nrows]
+
     def render_group(self, buf, first, nframes):
-        """Render this rank's rows of frames first .. first + nframes - 1 into slots
-        0 .. nframes - 1 of buffer ``buf`` (a graph replay for a full group in graph mode)."""
+        """Render this rank's rows of frames first .. first + nframes - 1 of a group into
+        their slots of buffer ``buf`` (a graph replay for a full group in graph mode)."""
         if not self.nrows:
             return
-        if self.render_frames is not None:
-            self.render_frames(self.send[buf][:nframes])
+        if self.render_frames is not None:  # one scene state: N interchangeable frames, one launch
+            self.render_frames(self.Z[buf][:self.world])
             return
         if self.graph and nframes == self.world:
-            if self.graphs[buf] is None:
-                self.capture()
-            self.graphs[buf].replay()
-            return
+            if hasattr(self.scene, "_set_camera"):  # a changed camera is uploaded (new tables) first
+                self.scene._set_camera(0, 1)
+            if self.graphs[buf] is None or self._graph_state != self._state():
+                self.capture(buf)
+            if self.graph:
+                self.graphs[buf].replay()
+                return
         for j in range(nframes):
-            self.render_block(self.send[buf][j, :self.nrows], self.rows, first + j)
+            self.render_block(self.slot(buf, j), self.rows, first + j)
 
-    def capture(self):
-        """Record both buffers' group renders as HIP graphs (graph mode). Done before the
-        first exchange is issued, so no collective is in flight while capturing; the
-        capture is thread-local (the process group's watchdog thread keeps querying its
-        events meanwhile)."""
+    def _state(self):
+        """What a captured graph bakes in: the scene's device handle and camera upload."""
+        sc = self.scene
+        nat = getattr(sc, "_native", None)
+        return (id(nat), getattr(nat, "h", None) and nat.h.value, id(getattr(sc, "_cam_info", None)))
+
+    def capture(self, buf):
+        """Record both buffers' group renders as HIP graphs (graph mode), rendering buffer
+        ``buf`` (the one about to be rendered; the other may hold a frame not yet
+        delivered) eagerly first, which compiles any specialized kernel. The capture is
+        thread-local (the process group's watchdog thread keeps querying its events
+        meanwhile) and records without executing, so an exchange in flight is untouched."""
         if not self.nrows:
             return
-        for buf in (0, 1):
-            for j in range(self.world):  # eager once: compiles any specialized kernel first
-                self.render_block(self.send[buf][j, :self.nrows], self.rows, j)
+        for j in range(self.world):
+            self.render_block(self.slot(buf, j), self.rows, j)
         torch.cuda.synchronize()
+        if not getattr(self.scene, "last_kernel", "rtx_jit_render_").startswith("rtx_jit_render_"):
+            # the generic kernels' uint8 renders stage through a library scratch buffer that
+            # a larger render may reallocate under a recorded graph: stay eager
+            self.graph = False
+            self.graphs = [None, None]
+            return
         for buf in (0, 1):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 for j in range(self.world):
-                    self.render_block(self.send[buf][j, :self.nrows], self.rows, j)
+                    self.render_block(self.slot(buf, j), self.rows, j)
             self.graphs[buf] = g
         torch.cuda.synchronize()
+        self._graph_state = self._state()
 
     def render(self):
         """One frame's render alone (bench.py's breakdown; not part of the frame loop)."""
         if self.nrows:
-            self.render_block(self.send[0][0, :self.nrows], self.rows, 0)
+            self.render_block(self.slot(0, self.rank), self.rows, 0)
 
     def _frame(self, buf):
-        flat = self.recv[buf].view((self.world * self.maxrows,) + tuple(self.recv[buf].shape[2:]))
-        return flat if self.in_order else torch.index_select(flat, 0, self.index)
+        flat = self.Z[buf][self.world - 1:].reshape((self.world * self.maxrows,) + tuple(self.Z[buf].shape[2:]))
+        return flat[:self.H] if self.identity else torch.index_select(flat, 0, self.index)
+
+    def _exchange(self, buf, nframes, async_op=True):
+        """frame j's rows to rank j, for the group's first nframes frames; no self-sends."""
+        N, m = self.world, self.maxrows
+        if N == 1:
+            return None
+        Z = self.Z[buf]
+        ins = [m if (j < nframes and j != self.rank) else 0 for j in range(N)]
+        outs = [m if (self.rank < nframes and s != self.rank) else 0 for s in range(N)]
+        flat = Z.view((Z.shape[0] * m,) + tuple(Z.shape[2:]))
+        send = flat[:sum(ins)]
+        recv = flat[N * m:N * m + sum(outs)]
+        return dist.all_to_all_single(recv, send, output_split_sizes=outs, input_split_sizes=ins, group=self.group,
+                                      async_op=async_op)
 
     def _submit_group(self, nframes):
         """Render the group that ends at frame k - 1 (nframes of it) and start its one
-        collective: frame j's rows to rank j. Returns the previous group's frames."""
+        collective. Returns the previous group's frames."""
         first = self.k - nframes
         buf = (first // self.world) % 2
         self.render_group(buf, first, nframes)
-        send = self.send[buf].view((self.world * self.maxrows,) + tuple(self.send[buf].shape[2:]))
-        recv = self.recv[buf].view(send.shape)
-        if nframes == self.world:
-            work = dist.all_to_all_single(recv, send, group=self.group, async_op=True)
-        else:
-            ins = [self.maxrows if j < nframes else 0 for j in range(self.world)]
-            outs = [self.maxrows if self.rank < nframes else 0] * self.world
-            # split sizes must add up to the tensors' first dimension
-            work = dist.all_to_all_single(recv[:sum(outs)], send[:sum(ins)], output_split_sizes=outs,
-                                          input_split_sizes=ins, group=self.group, async_op=True)
+        work = self._exchange(buf, nframes)
         prev, self.pending = self.pending, (work, buf, first, nframes)
         return self._finish(prev)
 
@@ -332,14 +395,16 @@ class FrameExchange:
         if pending is None:
             return []
         work, buf, first, nframes = pending
-        work.wait()
+        if work is not None:
+            work.wait()
         return [(first + self.rank, self._frame(buf))] if self.rank < nframes else []
 
     def exchange_once(self):
         """One full-group exchange of buffer 0, awaited (a stream wait): its cost alone
-        (bench.py's breakdown; not part of the frame loop)."""
-        send = self.send[0].view((self.world * self.maxrows,) + tuple(self.send[0].shape[2:]))
-        dist.all_to_all_single(self.recv[0].view(send.shape), send, group=self.group, async_op=True).wait()
+        (bench.py's breakdown; not part of the frame loop). Nothing at N = 1."""
+        work = self._exchange(0, self.world)
+        if work is not None:
+            work.wait()
 
     def step(self):
         """Submit the next frame; returns this rank's completed frames (see the class)."""

@@ -66,10 +66,18 @@ def _pipeline_worker(rank, world, port, name, res, nframes, interleave, out_q):
     from rtx.distributed import FramePipeline, to_rgb8
     sc = product_scene(name, res)
 
+    cache, count = {}, [0]
+
     def render_block(out, rows):  # the fused uint8 render, emulated: fp32 rows, then main.py's conversion
-        out.copy_(to_rgb8(torch.from_numpy(hostemu.render_rows(sc, rows, threads=2))))
+        if "rows" not in cache:
+            cache["rows"] = to_rgb8(torch.from_numpy(hostemu.render_rows(sc, rows, threads=2)))
+        out.copy_(cache["rows"] + count[0])  # frame k's rows + k (uint8 wraps): frames differ
+        count[0] += 1
     pipe = FramePipeline(sc, rank, world, device=torch.device("cpu"), render_block=render_block, interleave=interleave)
-    frames = [pipe.step() for _ in range(nframes)] + [pipe.flush()]
+
+    def keep(f):  # a returned frame may be a view of a reused buffer: copy it at once
+        return None if f is None else f.clone()
+    frames = [keep(pipe.step()) for _ in range(nframes)] + [keep(pipe.flush())]
     if rank == 0:
         assert frames[0] is None and all(f is not None for f in frames[1:])
         out_q.put([f.numpy() for f in frames[1:]])
@@ -79,8 +87,8 @@ def _pipeline_worker(rank, world, port, name, res, nframes, interleave, out_q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,res,interleave", [(2, (40, 23), True), (3, (33, 26), True), (2, (40, 24), False),
-                                                  (3, (20, 13), False)])
+@pytest.mark.parametrize("world,res,interleave", [(1, (40, 23), True), (2, (40, 23), True), (3, (33, 26), True),
+                                                  (2, (40, 24), False), (3, (20, 13), False)])
 def test_frame_pipeline_gathers_every_frame(world, res, interleave):
     from common import oracle_render
     from oracle import oracle as O
@@ -97,8 +105,8 @@ def test_frame_pipeline_gathers_every_frame(world, res, interleave):
         assert p.exitcode == 0
     want = O.to_png_array(oracle_render("MirrorRefraction", res))
     assert len(frames) == 3
-    for f in frames:
-        assert np.array_equal(f, want)
+    for k, f in enumerate(frames):
+        assert np.array_equal(f, (want.astype(np.int64) + k).astype(np.uint8)), k
 
 
 def _exchange_worker(rank, world, port, name, res, nframes, interleave, out_q):
@@ -133,7 +141,8 @@ def _exchange_worker(rank, world, port, name, res, nframes, interleave, out_q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,res,interleave,nframes", [(2, (40, 23), True, 5), (3, (33, 26), True, 7),
+@pytest.mark.parametrize("world,res,interleave,nframes", [(1, (40, 23), True, 3), (1, (40, 24), False, 2),
+                                                          (2, (40, 23), True, 5), (3, (33, 26), True, 7),
                                                           (2, (40, 24), False, 4), (3, (20, 13), False, 2),
                                                           (4, (24, 20), False, 9), (4, (24, 41), True, 8),
                                                           (4, (16, 20), True, 6)])  # rank 3 has no rows

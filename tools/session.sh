@@ -1,0 +1,72 @@
+#!/bin/bash
+# One parametrized GPU session (replaces the per-session one-off scripts). Every GPU step
+# has its own time limit, and the script stops at the first failure (pytest: exit >= 2 on
+# a crash; a failing assertion stops it too unless KEEP_GOING=1).
+#
+#   TAG=name STEPS="tests smoke bench configs ab pmc rocprof pipeline" bash tools/session.sh
+#
+# tests     python -m pytest tests -m gpu (TESTS="tests/x.py ..." narrows it)
+# smoke     __graft_entry__.smoke()
+# bench     the default bench line (N = 1, with CPU baselines unless CPU=0)
+# configs   bench.py --config C for C in CONFIGS (CPU=1 adds the CPU legs to each line)
+# ab        tools/ab_jitflags.sh: VARIANTS="name=jit flags;..." over CONFIGS
+# pmc       rocprofv3 counter passes (FETCH_SIZE, WRITE_SIZE, instruction mix) per CONFIGS
+#           -> $OUT/pmc_<config>.json
+# rocprof   rocprofv3 --kernel-trace --stats of the default bench
+# pipeline  the multi-GPU frame loop over RCCL with one rank (PIPE_CONFIGS)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${TAG:-session}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+CFGS=${CONFIGS:-tsp1080 tm1080 mr1080 dof4k}
+step() {  # step NAME SECONDS CMD...
+  local name=$1 secs=$2; shift 2
+  echo "== $name"; date +%T
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "rc=$rc"; tail -3 "$OUT/$name.log"
+  return $rc
+}
+cpu_flag() { [ "${CPU:-1}" = 1 ] && echo "--cpu-seconds ${CPU_SECONDS:-10}" || echo "--no-cpu-baseline"; }
+for s in ${STEPS:-tests smoke bench rocprof}; do
+  case $s in
+    tests)
+      step pytest_gpu 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -q -p no:cacheprovider --timeout 120 \
+        --timeout-method thread
+      rc=$?; [ $rc -eq 0 ] || [ "${KEEP_GOING:-0}" = 1 -a $rc -eq 1 ] || exit 1 ;;
+    smoke)
+      step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
+    bench)
+      step bench_default 400 python bench.py $(cpu_flag) || exit 1
+      grep '^{' "$OUT/bench_default.log" > "$OUT/bench_default.json" ;;
+    configs)
+      for c in $CFGS; do
+        pj=""; [ -f "$OUT/pmc_$c.json" ] && pj="--pmc-json $OUT/pmc_$c.json"
+        step bench_$c 600 python bench.py --config $c --steps ${BSTEPS:-20} --warmup 3 $(cpu_flag) $pj || exit 1
+        grep '^{' "$OUT/bench_$c.log" > "$OUT/bench_$c.json"
+      done ;;
+    ab)
+      CONFIGS="$CFGS" bash tools/ab_jitflags.sh > "$OUT/ab.log" 2>&1 || { tail "$OUT/ab.log"; exit 1; }
+      cat "$OUT/ab.log"; mkdir -p "$OUT/ab"; cp gpurun_out/abj/*.json "$OUT/ab/" ;;
+    pmc)
+      for c in $CFGS; do
+        CFG=$c TAG="${OUT#gpurun_out/}/pmc_$c" bash tools/pmc_session.sh > "$OUT/pmc_$c.log" 2>&1 || { tail "$OUT/pmc_$c.log"; exit 1; }
+        python tools/pmc_summary.py "$OUT/pmc_$c" $c > "$OUT/pmc_$c.json" || exit 1
+        python -c "import json;d=json.load(open('$OUT/pmc_$c.json'));c=d['counters_per_dispatch'];print('$c', d['kernel'], 'WRITE_KiB', c.get('WRITE_SIZE'), 'FETCH_KiB', c.get('FETCH_SIZE'), 'hbm_B', d.get('hbm_bytes_per_launch'), 'valu/wave', d.get('valu_insts_per_wave'))"
+      done ;;
+    rocprof)
+      step rocprof 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py \
+        --steps 100 --warmup 10 --no-cpu-baseline || exit 1 ;;
+    pipeline)
+      for c in ${PIPE_CONFIGS:-tsp1080 dof4k}; do
+        st=200; [ $c = dof4k ] && st=20
+        step pipeline1_$c 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+          --master-port 29533 bench.py --gpus 1 --force-dist --pipeline --config $c --steps $st --warmup 5 \
+          --no-cpu-baseline || exit 1
+        grep '^{' "$OUT/pipeline1_$c.log" > "$OUT/pipeline1_$c.json"
+      done ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo SESSION_DONE
