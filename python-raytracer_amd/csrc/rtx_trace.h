@@ -573,6 +573,15 @@ RTX_HD RayInv ray_inv(f3 o, f3 d) {
     r.pad_rel = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
     return r;
 }
+// The fp64 slabs as the rare fallback of the fp32 decisions below, out of line: inlined,
+// the compiler hoists their loop-invariant fp64 numerators (bound - origin) out of the
+// shading loops, where they hold VGPRs for the whole kernel (TorusMesh: 40 B/lane of
+// spills for its bounding volume's six numerators).
+__host__ __device__ __attribute__((noinline)) inline bool box_slabs_far(f3 o, f3 d, f3 mn, f3 mx, double& start,
+                                                                       int& label, double& end) {
+    return box_slabs(o, d, mn, mx, start, label, end);
+}
+
 // The same slabs decided in fp32, with box_slabs as the fallback. Each reference quotient
 // t = fl64((bound - o) / d) is estimated as q = fl32(bound - o) * rcp(d): three fp32
 // roundings and v_rcp_f32's 1 ulp give |q - t| <= 2^-22 |q|, so q +- (2^-20 |q| + 2^-100)
@@ -641,8 +650,7 @@ RTX_HD double slab_start64(f3 o, f3 d, f3 mn, f3 mx, int k) {
 // Box entry as the closest-hit test needs it (simple_geometry.py:188-226: valid iff no
 // zero-direction slab rejects, start <= end and start >= 0): fp32 decision, one fp64
 // division for the entry t, the full fp64 slabs for undecided lanes.
-RTX_HD bool box_entry(f3 o, f3 d, f3 mn, f3 mx, bool live, double& start, int& label, const RayInv* ri = nullptr) {
-    const SlabIv iv = box_slabs_iv(o, d, mn, mx, ri);
+RTX_HD bool box_entry_iv(f3 o, f3 d, f3 mn, f3 mx, const SlabIv& iv, bool live, double& start, int& label) {
     const bool yes = live && iv.sure && !iv.reject && iv.s_hi < iv.e_lo && iv.s_lo > 0.0f;
     const bool no = !live || iv.reject || (iv.sure && (iv.s_lo > iv.e_hi || iv.s_hi < 0.0f));
     label = iv.label;
@@ -653,14 +661,30 @@ RTX_HD bool box_entry(f3 o, f3 d, f3 mn, f3 mx, bool live, double& start, int& l
     if (RTX_ANY(und)) {
         if (und) {
             double e = 0.0;
-            valid = box_slabs(o, d, mn, mx, start, label, e) && !(start > e || start < 0.0);
+            valid = box_slabs_far(o, d, mn, mx, start, label, e) && !(start > e || start < 0.0);
         }
     }
     return valid;
 }
+RTX_HD bool box_entry(f3 o, f3 d, f3 mn, f3 mx, bool live, double& start, int& label, const RayInv* ri = nullptr) {
+    return box_entry_iv(o, d, mn, mx, box_slabs_iv(o, d, mn, mx, ri), live, start, label);
+}
+// From the fp32 intervals alone: the lane's ray certainly misses the box, or enters it
+// only after tcap (its start cannot win or tie against a best hit whose fp32 proxy is
+// tcap: start >= s_lo > tcap gives fl32(start) > tcap).
+RTX_HD bool box_iv_out(const SlabIv& iv, float tcap) {
+    return iv.reject || (iv.sure && (iv.s_lo > iv.e_hi || iv.s_hi < 0.0f || iv.s_lo > tcap));
+}
+// Experiment knob: 1 drops the padded pre-test and lets the slab intervals (which share
+// its reciprocals and quotients) decide which lanes go on. Measured slower (DepthOfField 4K
+// 7.06 -> 7.85 ms, profiles/r03/box_iv/): the cheap pre-test culls most lanes -- rays
+// already ending on the floor in front of a box, tiles that miss it -- before any
+// interval is needed.
+#ifndef RTX_BOX_IV_CULL
+#define RTX_BOX_IV_CULL 0
+#endif
 // Box shadow test (simple_geometry.py:251-294): 1e-4 < start < t_max and start <= end.
-RTX_HD bool box_shadow(f3 o, f3 d, f3 mn, f3 mx, double t_max, const RayInv* ri = nullptr) {
-    const SlabIv iv = box_slabs_iv(o, d, mn, mx, ri);
+RTX_HD bool box_shadow_iv(f3 o, f3 d, f3 mn, f3 mx, const SlabIv& iv, double t_max) {
     const bool yes = iv.sure && !iv.reject && iv.s_hi < iv.e_lo && iv.s_lo >= kEps4Up && (double)iv.s_hi < t_max;
     const bool no = iv.reject ||
                     (iv.sure && (iv.s_lo > iv.e_hi || iv.s_hi < kEps4Up || (double)iv.s_lo >= t_max));
@@ -670,10 +694,13 @@ RTX_HD bool box_shadow(f3 o, f3 d, f3 mn, f3 mx, double t_max, const RayInv* ri 
         if (und) {
             double start, end;
             int label;
-            occ = box_slabs(o, d, mn, mx, start, label, end) && !(start > end) && 1e-4 < start && start < t_max;
+            occ = box_slabs_far(o, d, mn, mx, start, label, end) && !(start > end) && 1e-4 < start && start < t_max;
         }
     }
     return occ;
+}
+RTX_HD bool box_shadow(f3 o, f3 d, f3 mn, f3 mx, double t_max, const RayInv* ri = nullptr) {
+    return box_shadow_iv(o, d, mn, mx, box_slabs_iv(o, d, mn, mx, ri), t_max);
 }
 
 // Mesh bounding volume (bounding_volumes.py:18-37 sphere, :49-83 AABB).
@@ -688,7 +715,7 @@ RTX_HD bool mesh_bv(const O& ob, f3 o, f3 d) {
         if (yes || no) return yes;
         double start, end;
         int label;
-        if (!box_slabs(o, d, mn, mx, start, label, end)) return false;
+        if (!box_slabs_far(o, d, mn, mx, start, label, end)) return false;
         return !(start > end || start < 0.0);
     }
     double b, s, two_a;
@@ -1565,12 +1592,20 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
         if (RTX_ABLATE == 17) continue;  // cost probe: no boxes in closest_hit
         const DObj ob = S.objs[oi];
         const f3 mn = moved(ob, ob.a, time), mx = moved(ob, ob.b, time);
-        // the fp64 slabs only where some lane's ray may hit the box before its best t
-        const bool maybe = box_maybe_hit(mn, mx, o, ri, h.t32);
-        if (!RTX_ANY(maybe)) continue;
         double start = 0.0;
         int label = 0;
-        const bool valid = box_entry(o, d, mn, mx, maybe, start, label, &ri);
+        bool valid;
+        if (RTX_BOX_IV_CULL) {  // the intervals decide which lanes may hit before their best t
+            const SlabIv iv = box_slabs_iv(o, d, mn, mx, &ri);
+            const bool maybe = !box_iv_out(iv, h.t32);
+            if (!RTX_ANY(maybe)) continue;
+            valid = box_entry_iv(o, d, mn, mx, iv, maybe, start, label);
+        } else {
+            // the fp64 slabs only where some lane's ray may hit the box before its best t
+            const bool maybe = box_maybe_hit(mn, mx, o, ri, h.t32);
+            if (!RTX_ANY(maybe)) continue;
+            valid = box_entry(o, d, mn, mx, maybe, start, label, &ri);
+        }
         offer(S, h, valid, (float)start, oi, label, o, d, time);
     }
     if (MESH) {
@@ -1791,9 +1826,17 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
         if (RTX_ABLATE == 20) continue;  // cost probe: boxes never occlude
         const DObj ob = S.objs[oi];
         const f3 mn = moved(ob, ob.a, time), mx = moved(ob, ob.b, time);
-        const bool maybe = !occ && box_maybe_hit(mn, mx, o, ri, INFINITY);
-        if (!RTX_ANY(maybe)) continue;
-        if (maybe) occ = box_shadow(o, d, mn, mx, t_max, &ri);
+        if (RTX_BOX_IV_CULL) {
+            if (RTX_ALL(occ)) break;
+            const SlabIv iv = box_slabs_iv(o, d, mn, mx, &ri);
+            const bool maybe = !occ && !box_iv_out(iv, INFINITY);
+            if (!RTX_ANY(maybe)) continue;
+            if (maybe) occ = box_shadow_iv(o, d, mn, mx, iv, t_max);
+        } else {
+            const bool maybe = !occ && box_maybe_hit(mn, mx, o, ri, INFINITY);
+            if (!RTX_ANY(maybe)) continue;
+            if (maybe) occ = box_shadow(o, d, mn, mx, t_max, &ri);
+        }
     }
     if (MESH) {
         for (int k = 0; k < RTX_NMESH(S); ++k, ++oi) {  // mesh.py:121-153 (no t_max test)
