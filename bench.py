@@ -297,11 +297,40 @@ def main():
     import rtx  # noqa: F401
     from rtx.distributed import FrameExchange, FramePipeline
 
+    # setup cost, outside the timed region (the reference re-parses and re-renders per
+    # main.py run, provided/main.py:25-34): host parse, rtx_scene_create (records, mesh
+    # BVH, light grids), rtx_camera_set (tables, primary-ray bins) and the first frame
+    # (scene-specialized kernel: hiprtc compile, or a load from the on-disk cache)
+    jit_dir = os.environ.get("RTX_JIT_CACHE") or "/tmp/rtx_jit_%d" % os.getuid()
+
+    def n_cached():
+        try:
+            return len(os.listdir(jit_dir))
+        except OSError:
+            return 0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
     sc = make_scene(a.config)
+    t1 = time.perf_counter()
+    sc.native()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    sc._set_camera(0, 1)
+    torch.cuda.synchronize()
+    t3 = time.perf_counter()
     W, H = sc.vc.width, sc.vc.height
     spp = sc.samples_per_pixel
     stream = torch.cuda.current_stream()
     fb = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    cached0 = n_cached()
+    t4 = time.perf_counter()
+    sc.render_device(out=fb)
+    torch.cuda.synchronize()
+    t5 = time.perf_counter()
+    setup = {"parse_ms": round((t1 - t0) * 1e3, 3), "scene_create_ms": round((t2 - t1) * 1e3, 3),
+             "camera_set_ms": round((t3 - t2) * 1e3, 3), "first_frame_ms": round((t5 - t4) * 1e3, 3),
+             "first_frame_jit": "compiled (hiprtc)" if n_cached() > cached0 else "code object from the disk cache",
+             "note": "outside the timed region; first_frame_ms includes one render"}
 
     # ray-segment census for the algorithmic byte model (separate counting launch)
     cnt = torch.zeros(16, dtype=torch.int64, device="cuda")
@@ -470,6 +499,7 @@ def main():
                            "unit": "G wave64-instructions/s", "frac": round(ach / VALU_PEAK_GINST_S, 4),
                            "issue_floor_us": round(v / VALU_PEAK_GINST_S / 1e3, 3), "source": traffic_src}
             roof["limiter"] = "VALU issue + per-wave latency (see valu); measured HBM traffic is frac_measured"
+        out["setup_ms"] = setup
         out.update(extra)
         out.update(cpu)
         print(json.dumps(out), flush=True)

@@ -762,9 +762,23 @@ bool primary_bins(const HostScene& H, const rtx_camera_desc* c, std::vector<int3
         c->dof_origins[2] != c->position[2])
         return false;
     const double o[3] = {c->aa_origins[0], c->aa_origins[1], c->aa_origins[2]};
-    const double dx = (double)c->xs[1] - (double)c->xs[0], dy = (double)c->ys[1] - (double)c->ys[0];
-    if (!(dx > 0.0) || !(dy > 0.0)) return false;
     const int32_t W = c->ncols, Hh = c->height;
+    const double dx = ((double)c->xs[W - 1] - (double)c->xs[0]) / (W - 1);
+    const double dy = ((double)c->ys[Hh - 1] - (double)c->ys[0]) / (Hh - 1);
+    if (!(dx > 0.0) || !(dy > 0.0)) return false;
+    for (int32_t i = 1; i < W; ++i)
+        if (!(c->xs[i] > c->xs[i - 1])) return false;
+    for (int32_t j = 1; j < Hh; ++j)
+        if (!(c->ys[j] > c->ys[j - 1])) return false;
+    // fractional index of a screen coordinate in the camera's own (fp32) pixel table: the
+    // rays use those very values, so no spacing estimate accumulates error across the image
+    auto table_pos = [](const float* t, int32_t n, double x) {
+        if (x <= (double)t[0]) return (x - (double)t[0]) / ((double)t[1] - (double)t[0]);
+        if (x >= (double)t[n - 1]) return (n - 1) + (x - (double)t[n - 1]) / ((double)t[n - 1] - (double)t[n - 2]);
+        const int32_t k = (int32_t)(std::upper_bound(t, t + n, (float)x) - t);  // t[k-1] <= fl(x) < t[k]
+        const int32_t k1 = std::min(std::max(k, 1), n - 1);
+        return (k1 - 1) + (x - (double)t[k1 - 1]) / ((double)t[k1] - (double)t[k1 - 1]);
+    };
     bins_x = (W + 7) / 8;
     const int32_t bins_y = (Hh + 7) / 8;
     const size_t nb = (size_t)bins_x * bins_y;
@@ -780,8 +794,8 @@ bool primary_bins(const HostScene& H, const rtx_camera_desc* c, std::vector<int3
         }
         depth = -pw;
         if (!(depth > 1e-3 * std::sqrt(len2)) || !(depth > 1e-9)) return false;
-        col = (c->d * pu / depth - (double)c->xs[0]) / dx;
-        row = (double)(Hh - 1) - (c->d * pv / depth - (double)c->ys[0]) / dy;
+        col = table_pos(c->xs, W, c->d * pu / depth);
+        row = (double)(Hh - 1) - table_pos(c->ys, Hh, c->d * pv / depth);
         return true;
     };
     struct Rect { int32_t c0, c1, r0, r1; };

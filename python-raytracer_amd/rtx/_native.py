@@ -119,8 +119,9 @@ def load():
         lib.rtx_intersect.argtypes = [vp, C.c_int64, vp, vp, C.c_double, vp, vp, vp, vp, vp, vp]
         lib.rtx_occluded.argtypes = [vp, C.c_int64, vp, vp, vp, C.c_double, vp, vp]
         lib.rtx_fb_to_rgb8.argtypes = [vp, vp, C.c_int64, vp]
-        for fn in EXPORTS[2:-1]:
-            getattr(lib, fn).restype = C.c_int
+        for fn in EXPORTS:  # every status-returning entry point (not the string / count ones)
+            if fn not in ("rtx_abi_version", "rtx_last_error", "rtx_last_kernel", "rtx_group_rows"):
+                getattr(lib, fn).restype = C.c_int
         lib.rtx_last_kernel.argtypes = [vp]
         lib.rtx_last_kernel.restype = C.c_char_p
         v = lib.rtx_abi_version()

@@ -116,6 +116,7 @@ class Scene:
             self._native.close()
         self._native = None
         self._cam_key = None
+        self._noise_src = None
 
     @property
     def last_kernel(self):
@@ -195,8 +196,13 @@ class Scene:
         vecs = b"".join(np.asarray(v, np.float32).tobytes() for v in (vc.position, vc.u, vc.v, vc.w))
         noise = None
         if self.jitter and self.jitter_noise is not None:
-            a = np.ascontiguousarray(np.asarray(self.jitter_noise, np.float64))
-            noise = (a.size, hashlib.blake2b(a.tobytes(), digest_size=16).digest())
+            # the digest of a replayed stream is cached per array object (a new stream is a
+            # new array; mutate one in place and call invalidate())
+            src = self.jitter_noise
+            if getattr(self, "_noise_src", None) is not src:
+                a = np.ascontiguousarray(np.asarray(src, np.float64))
+                self._noise_src, self._noise_digest = src, (a.size, hashlib.blake2b(a.tobytes(), digest_size=16).digest())
+            noise = self._noise_digest
         return (subimage, tasks, vc.width, vc.height, vc.left, vc.right, vc.top, vc.bottom, vecs, vc.d,
                 vc.focal_length, vc.aperture, vc.dof_samples, tuple(vc.motion_times), self.samples, self.jitter,
                 self.seed, noise)

@@ -111,6 +111,9 @@ def render_cases():
                                seed=5),
         "dof_strip": dict(scene=_bundle("DepthOfField", resolution=[96, 64], AA={"jitter": True, "samples": 1}),
                           seed=11, subimage=5, tasks=8),
+        # BASELINE config 1: TwoSpheresPlane 256x256 1 spp on the reference's CPU path
+        "tsp256_config1": dict(scene=_bundle("TwoSpheresPlane", resolution=[256, 256],
+                                             AA={"jitter": False, "samples": 1})),
         "tsp_aa3_jitter": dict(scene=_bundle("TwoSpheresPlane", resolution=[48, 36],
                                              AA={"jitter": True, "samples": 3}), seed=7),
         "motionblur": dict(scene=_bundle("MotionBlur", resolution=[48, 40])),

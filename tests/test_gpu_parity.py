@@ -569,3 +569,18 @@ def test_render_frames_equals_per_frame_renders(name, res, edits, jit, monkeypat
     with pytest.raises(N.RtxError):
         N.call("rtx_render_frames", sc._native.h, 0, 4, C.c_void_p(buf.data_ptr()), 1, 2, 4 * W * 3 - 1, None,
                C.c_void_p(torch.cuda.current_stream().cuda_stream))
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_primary_bins_wide_frame(seed, monkeypatch):
+    """Primary-ray bins at 7680 pixels across (the tables, not a spacing estimate, map a
+    projected point to its column): binned == walk == oracle on the last column strip."""
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import bins_scene
+    d = bins_scene(seed, res=(7680, 16))
+    a = product_scene_dict(d).render(7, 8)
+    monkeypatch.setenv("RTX_BINS", "0")
+    b = product_scene_dict(d).render(7, 8)
+    monkeypatch.delenv("RTX_BINS")
+    assert np.array_equal(a, b)
+    assert_parity(a, oracle_render_dict(d, 7, 8), "wide bins seed %d" % seed)

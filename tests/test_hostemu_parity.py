@@ -412,3 +412,31 @@ def test_hostemu_plane_shadow_stress():
     osc = O.OracleScene(dd, base)
     for tmax in (1.0, np.inf, 0.7):
         assert np.array_equal(hostemu.occluded(sc, o, d, tmax, 0.0), osc.shadow(0.0, o, d, tmax).astype(bool)), tmax
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_hostemu_primary_bins_wide_frame(seed, monkeypatch):
+    """Bins at 7680 pixels across: a tile's objects come from projecting through the camera's
+    own fp32 pixel tables (rtx_api.hip primary_bins), not from a spacing estimate whose
+    error grows with the column index -- binned == walk == oracle on the first and last of
+    eight column strips, with tiny spheres strung along the frame's width."""
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import bins_scene
+    d = bins_scene(seed, res=(7680, 16))
+    cam = np.array(d["camera"]["position"])
+    look = np.array(d["camera"]["lookAt"])
+    fwd = (look - cam) / np.linalg.norm(look - cam)
+    side = np.cross(fwd, [0.0, 1.0, 0.0])
+    side /= np.linalg.norm(side)
+    for k, s in enumerate(np.linspace(-1.0, 1.0, 9)):
+        c = cam + fwd * 20.0 + side * s * 20.0 * np.tan(np.radians(d["camera"]["fov"] / 2)) * 1.2
+        d["objects"].append({"name": "tiny%d" % k, "type": "sphere", "radius": 0.02,
+                             "position": np.round(c, 4).tolist(), "materials": [k % 4]})
+    sc = product_scene_dict(d)
+    for k in (0, 7):
+        img, _ = hostemu.render(sc, k, 8)
+        monkeypatch.setenv("RTX_BINS", "0")
+        walk, _ = hostemu.render(product_scene_dict(d), k, 8)
+        monkeypatch.delenv("RTX_BINS")
+        assert np.array_equal(img, walk), k
+        assert_parity(img, oracle_render_dict(d, k, 8), "wide bins seed %d strip %d" % (seed, k))

@@ -54,3 +54,24 @@ def test_pyloop_refuses_hierarchies():
     d, base = O.load_bundle("NovelScene1", resolution=[8, 4])
     with pytest.raises(NotImplementedError):
         P.PyLoopScene(O.OracleScene(d, base))
+
+
+def _config1_strip(k):
+    d, base = O.load_bundle("TwoSpheresPlane", resolution=[256, 256], AA={"jitter": False, "samples": 1})
+    return P.PyLoopScene(O.OracleScene(d, base)).render(k, 4)
+
+
+def test_config1_tsp256_python_loop_equals_reference():
+    """BASELINE config 1 (TwoSpheresPlane 256x256, 1 spp, the reference's CPU path) at its
+    stated size: the Python loop, run as 4 column-strip processes like render.nu, glued,
+    equals the reference's own render (tests/golden/refvectors/render_tsp256_config1.npz)
+    and the C oracle, bit for bit."""
+    from multiprocessing import get_context
+
+    import refvectors as R
+    with get_context("fork").Pool(4) as pool:
+        img = np.concatenate(pool.map(_config1_strip, range(4)), axis=0)
+    fx = R.load("render", "tsp256_config1")
+    assert np.array_equal(img, fx["image"])
+    d, base = O.load_bundle("TwoSpheresPlane", resolution=[256, 256], AA={"jitter": False, "samples": 1})
+    assert np.array_equal(O.OracleScene(d, base).render(), fx["image"])
