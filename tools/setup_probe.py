@@ -1,0 +1,53 @@
+"""Setup cost of a render (outside bench.py's timed region), each step three times:
+host parse, rtx_scene_create, rtx_camera_set and the first frame, with a cold on-disk JIT
+cache (a fresh RTX_JIT_CACHE directory) and then warm. usage: python tools/setup_probe.py [config]"""
+import json
+import os
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "python-raytracer_amd")]
+os.environ["RTX_JIT_CACHE"] = tempfile.mkdtemp(prefix="rtx_jit_probe_")
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def ms(t0):
+    torch.cuda.synchronize()
+    return round((time.perf_counter() - t0) * 1e3, 3)
+
+
+def main():
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "tsp1080"
+    torch.cuda.set_device(0)
+    torch.zeros(1, device="cuda")
+    rows = []
+    for rep in range(3):
+        t = time.perf_counter()
+        sc = bench.make_scene(cfg)
+        parse = ms(t)
+        t = time.perf_counter()
+        sc.native()
+        create = ms(t)
+        t = time.perf_counter()
+        sc._set_camera(0, 1)
+        cam = ms(t)
+        fb = torch.empty((sc.vc.height, sc.vc.width, 3), dtype=torch.float32, device="cuda")
+        t = time.perf_counter()
+        sc.render_device(out=fb)
+        first = ms(t)
+        t = time.perf_counter()
+        sc.render_device(out=fb)
+        second = ms(t)
+        rows.append({"rep": rep, "parse_ms": parse, "scene_create_ms": create, "camera_set_ms": cam,
+                     "first_frame_ms": first, "next_frame_ms": second, "kernel": sc.last_kernel})
+        sc.invalidate()
+    print(json.dumps({"config": cfg, "runs": rows}))
+
+
+if __name__ == "__main__":
+    main()
