@@ -114,6 +114,16 @@ def render_cases():
         # BASELINE config 1: TwoSpheresPlane 256x256 1 spp on the reference's CPU path
         "tsp256_config1": dict(scene=_bundle("TwoSpheresPlane", resolution=[256, 256],
                                              AA={"jitter": False, "samples": 1})),
+        # BASELINE configs 2-5 at their stated sizes: column strips (np.array_split) of the
+        # full frames, the columns crossing the objects
+        "config2_tsp1080_cols": dict(scene=_bundle("TwoSpheresPlane", resolution=[1920, 1080],
+                                                   AA={"jitter": False, "samples": 1}), subimage=37, tasks=96),
+        "config3_tm1080_cols": dict(scene=_bundle("TorusMesh", resolution=[1920, 1080],
+                                                  AA={"jitter": False, "samples": 1}), subimage=125, tasks=240),
+        "config4_mr1080_cols": dict(scene=_bundle("MirrorRefraction", resolution=[1920, 1080],
+                                                  AA={"jitter": False, "samples": 1}), subimage=52, tasks=96),
+        "config5_dof4k_col": dict(scene=_bundle("DepthOfField", resolution=[3840, 2160],
+                                                AA={"jitter": True, "samples": 2}), seed=29, subimage=3000, tasks=3840),
         "tsp_aa3_jitter": dict(scene=_bundle("TwoSpheresPlane", resolution=[48, 36],
                                              AA={"jitter": True, "samples": 3}), seed=7),
         "motionblur": dict(scene=_bundle("MotionBlur", resolution=[48, 40])),
