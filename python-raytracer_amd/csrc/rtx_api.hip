@@ -1201,6 +1201,13 @@ hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& k
                                      "-DRTX_FIXED_POWBITS=" + std::to_string(v.pow_bits),
                                      "-DRTX_FIXED_DIVPOW2=" + std::to_string(kp.div_pow2),
                                      "-DRTX_FIXED_JMODE=" + std::to_string(kp.jitter)};
+    // the strip width too: the tile index arithmetic becomes multiplications by constants
+    // (TSP 1080p 27.85 -> 27.37 us, profiles/r03/ncols/; one compile per strip width).
+    // RTX_JIT_NCOLS=0 leaves it a run-time value.
+    {
+        const char* e = getenv("RTX_JIT_NCOLS");
+        if (!spp && !(e && e[0] == '0')) opts.push_back("-DRTX_FIXED_NCOLS=" + std::to_string(kp.ncols));
+    }
     if (uniform_hard >= 0) opts.push_back("-DRTX_FIXED_HARD=" + std::to_string(uniform_hard));
     if (out8) opts.push_back("-DRTX_OUT8=1");  // uint8 framebuffer (rtx_render_rgb8)
     // secondary-ray frames keep their material index in a register: 3 LDS words per frame

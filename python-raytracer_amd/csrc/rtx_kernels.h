@@ -376,7 +376,11 @@ __device__ __forceinline__ void render_body(const KParams* __restrict__ Pp, cons
     constexpr int B = kBlock<X>;
     if (MESH) stage_mesh_lds(Pp->S);
     stage_records_lds(Pp->S);
+#ifdef RTX_FIXED_NCOLS  // scene-specialized kernels pin the strip width (tile index math by constants)
+    const int32_t ncols = RTX_FIXED_NCOLS;
+#else
     const int32_t ncols = Pp->ncols;
+#endif
     Tally tl = {};
     // secondary-ray frames: [frame][word][thread] in LDS (40 KB per 256-thread block; 30 KB
     // with RTX_FRAME_MATBITS)
