@@ -168,9 +168,25 @@ __device__ __forceinline__ cptr<T> opaque_uniform(cptr<T> p) {
     return (cptr<T>)(((uint64_t)hi << 32) | lo);
 }
 // (flat-scene kernels only: the hierarchy/texture kernels keep the loaded records)
+//
+// One-sample scene-specialized kernels built with RTX_BAKED_RECORDS carry the scene's object,
+// material and light records in the code object (rtx_api.hip jit_baked_records: constant
+// arrays rtx_baked::kObjs / kMats / kLights, defined ahead of this header). Reads at a
+// compile-time index -- the unrolled object and light loops -- fold to literals, so no
+// dependent scalar load precedes a wave's first ray; per-lane reads (the hit object, its
+// material) load from the code object's read-only data. The values are the same bytes
+// rtx_scene_create uploads, so the arithmetic is unchanged.
 template <bool X>
 RTX_HD SceneView sample_scene(const SceneView& S0) {
     SceneView S = S0;
+#if defined(RTX_BAKED_RECORDS) && defined(__HIP_DEVICE_COMPILE__)
+    if (!X) {
+        S.objs = (cptr<DObj>)rtx_baked::kObjs;
+        S.mats = (cptr<DMat>)rtx_baked::kMats;
+        S.lights = (cptr<DLight>)rtx_baked::kLights;
+        return S;
+    }
+#endif
 #if defined(__HIP_DEVICE_COMPILE__)
     if (RTX_RELOAD_RECORDS && !X) {  // opaque to loop-invariant code motion
         S.objs = opaque_uniform(S.objs);

@@ -110,3 +110,18 @@ def occluded_light(scene, o, light, grids):
         return None
     _chk(rc)
     return occ.astype(bool), cells
+
+
+def jit_baked(scene):
+    """The scene-record prelude librtx.so hands its scene-specialized kernels
+    (rtx_api.hip jit_baked_records), as a string."""
+    sd = scene.scene_desc()
+    f = lib().rtx_hostemu_jit_baked
+    f.argtypes = [C.c_void_p, C.c_char_p, C.c_int64]
+    f.restype = C.c_int64
+    n = f(C.addressof(sd), None, 0)
+    if n < 0:
+        raise RuntimeError("hostemu jit_baked failed: %s" % lib().rtx_hostemu_last_error().decode())
+    buf = C.create_string_buffer(int(n) + 1)
+    f(C.addressof(sd), buf, n + 1)
+    return buf.value.decode()

@@ -339,3 +339,18 @@ extern "C" int64_t rtx_hostemu_sizeof(int which) {
     }
     return -1;
 }
+
+// The scene-record prelude of the scene-specialized kernels (rtx_api.hip
+// jit_baked_records) for a scene, so tests and tools/jit_isa.sh can inspect it offline.
+// Returns the string's length; writes at most cap bytes (NUL-terminated) into out.
+extern "C" int64_t rtx_hostemu_jit_baked(const rtx_scene_desc* sd, char* out, int64_t cap) {
+    HostScene H;
+    if (convert_scene(sd, H)) return -1;
+    const std::string s = jit_baked_records(H.objs, H.mats, H.lights);
+    if (out && cap > 0) {
+        const size_t n = std::min((size_t)cap - 1, s.size());
+        memcpy(out, s.data(), n);
+        out[n] = '\0';
+    }
+    return (int64_t)s.size();
+}

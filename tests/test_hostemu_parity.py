@@ -440,3 +440,28 @@ def test_hostemu_primary_bins_wide_frame(seed, monkeypatch):
         monkeypatch.delenv("RTX_BINS")
         assert np.array_equal(img, walk), k
         assert_parity(img, oracle_render_dict(d, k, 8), "wide bins seed %d strip %d" % (seed, k))
+
+
+@pytest.mark.parametrize("name", ["TwoSpheresPlane", "MirrorRefraction", "TorusMesh", "DepthOfField"])
+def test_jit_baked_records_are_the_scene_records(name):
+    """The prelude of the one-sample scene-specialized kernels (rtx_api.hip
+    jit_baked_records) holds exactly the object, material and light records the scene
+    uploads: one DObj (56 words), DMat (20) and DLight (20) per record, objects grouped
+    by type (planes, spheres, boxes, meshes) and materials' diffuse colours in f32."""
+    import re
+    sc = product_scene(name, (64, 48))
+    src = hostemu.jit_baked(sc)
+    assert src.rstrip().endswith("#define RTX_BAKED_RECORDS 1")
+    arrays = {m.group(1): [int(w, 16) for w in re.findall(r"0x([0-9a-f]+)u", m.group(2))]
+              for m in re.finditer(r"static constexpr unsigned (\w+)\[\] = \{([^}]*)\}", src)}
+    objs, mats, lights = arrays["kObjs"], arrays["kMats"], arrays["kLights"]
+    assert len(objs) == 56 * len(sc.objects)
+    assert len(mats) == 20 * len(sc.materials)
+    assert len(lights) == 20 * len(sc.lights)
+    kinds = [objs[56 * i] for i in range(len(sc.objects))]  # DObj::type: sphere 0, plane 1, box 2, mesh 3
+    assert kinds == sorted(kinds, key=lambda k: [1, 0, 2, 3].index(k))
+    want = sorted({"sphere": 0, "plane": 1, "box": 2, "mesh": 3}[o.gtype] for o in sc.objects)
+    assert sorted(kinds) == want
+    for i, m in enumerate(sc.materials):
+        got = np.array(mats[20 * i:20 * i + 3], np.uint32).view(np.float32)
+        assert np.array_equal(got, np.asarray(m.diffuse, np.float32)), (i, got, m.diffuse)
