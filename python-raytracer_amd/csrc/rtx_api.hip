@@ -19,6 +19,7 @@
 #include <fstream>
 #include <functional>
 #include <map>
+#include <numeric>
 #include <mutex>
 #include <sstream>
 #include <string>
@@ -1766,6 +1767,13 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
     };
     int64_t nblocks = blocks(spp_mode);
     if (nblocks > 0x7fffffff || blocks(false) > 0x7fffffff) return fail(RTX_ERR_INVALID, "rtx_render: launch too large");
+    {  // RTX_TILE_ORDER 2 (experiment): a multiplier coprime to the launch's wave count
+        const uint64_t T = (uint64_t)nblocks * (blk / 64) * RTX_PPL;
+        uint64_t m = std::max<uint64_t>(1, (uint64_t)((double)T * 0.6180339887498949));
+        while (T > 1 && std::gcd(m, T) != 1) ++m;
+        L.perm = (uint32_t)(T > 1 ? m % T : 1);
+        L.pad0 = 0;
+    }
     rtx_scene::Resolved& rs = s->resolved[(out8 ? 8 : 0) | (cnt ? 4 : 0) | (jit ? 2 : 0) | (spp_mode ? 1 : 0)];
     if (!rs.done) {
         rs.fn = jit_render_kernel(s->device, s->view, s->kp, s->fc_mode, s->any_speed, s->light_dir_mask,

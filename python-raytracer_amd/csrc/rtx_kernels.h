@@ -271,6 +271,7 @@ struct Launch {
     int32_t gphase, gstride;
     // rtx_render_frames: blockIdx.y renders frame y of a batch into fb + y * fstride bytes
     int64_t fstride;
+    uint32_t perm, pad0;  // RTX_TILE_ORDER 2: the wave permutation's multiplier
 };
 
 // This block's framebuffer (frame blockIdx.y of a batched launch; the only frame otherwise).
@@ -319,10 +320,20 @@ __host__ __device__ inline int32_t primary_bin(const SceneView& S, int32_t row, 
 struct PixelRC {
     int32_t r, c;
 };
-__device__ __forceinline__ PixelRC pixel_rc(int32_t ncols, int sub) {
+// The order in which a launch's waves visit the tiles (experiments): 0 row-major from the
+// top, 1 reversed (bottom rows first), 2 a stride permutation w -> w * perm mod T (the
+// host picks perm coprime to the launch's T waves, near T / golden ratio), so each
+// stretch of the dispatch samples the whole image.
+#ifndef RTX_TILE_ORDER
+#define RTX_TILE_ORDER 0
+#endif
+__device__ __forceinline__ PixelRC pixel_rc(int32_t ncols, int sub, uint32_t perm = 1) {
     const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(
+    int wave = __builtin_amdgcn_readfirstlane(
         (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RTX_PPL + sub));
+    const uint32_t T = gridDim.x * (blockDim.x >> 6) * RTX_PPL;
+    if (RTX_TILE_ORDER == 1) wave = (int)T - 1 - wave;
+    if (RTX_TILE_ORDER == 2) wave = (int)(((uint64_t)(uint32_t)wave * perm) % T);
     if (RTX_TILE == 0) {
         const int64_t p = (int64_t)wave * 64 + lane;
         const int32_t r = (int32_t)(p / ncols);
@@ -406,7 +417,7 @@ __device__ __forceinline__ void render_body(const KParams* __restrict__ Pp, cons
     const HStack hs{hstack + threadIdx.x, B};
     bool any_active = false;
     for (int sub = 0; sub < RTX_PPL; ++sub) {
-        const PixelRC px = pixel_rc(ncols, sub);
+        const PixelRC px = pixel_rc(ncols, sub, L.perm);
         const bool active = px.r < L.nrows && px.c < ncols;
         any_active = any_active || active;
         // primary-ray face bin of the wave's 8x8 tile (its top-left pixel)

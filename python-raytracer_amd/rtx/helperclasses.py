@@ -74,10 +74,46 @@ class AAInterval:
         self.label = label
 
 
+class _Times(list):
+    """ViewportCamera.motion_times: a list that counts its owner's version up on every
+    in-place change (it still compares equal to a plain list)."""
+
+    def __init__(self, values, owner):
+        super().__init__(values)
+        self._owner = owner
+
+    def _changed(self):
+        self._owner._bump()
+
+
+def _tracked(name):
+    def method(self, *args, **kwargs):
+        r = getattr(list, name)(self, *args, **kwargs)
+        self._changed()
+        return self if name == "__iadd__" or name == "__imul__" else r
+    method.__name__ = name
+    return method
+
+
+for _m in ("__setitem__", "__delitem__", "__iadd__", "__imul__", "append", "extend", "insert", "pop", "remove",
+           "clear", "sort", "reverse"):
+    setattr(_Times, _m, _tracked(_m))
+
+
 class ViewportCamera:
-    """helperclasses.py:69-108: viewport, camera basis, lens and motion samples."""
+    """helperclasses.py:69-108: viewport, camera basis, lens and motion samples.
+
+    Every attribute assignment counts ``_version`` up, so a Scene re-uploads its camera
+    tables only after a change (Scene._set_camera). The basis vectors are kept as
+    read-only fp32 copies (assign a new vector to move the camera) and motion_times as a
+    list that reports in-place edits; a vector of another type (e.g. a PyGLM vec3 set
+    by hand) makes the scene compare every camera value per render instead."""
+
+    _VECS = ("position", "u", "v", "w")
 
     def __init__(self):
+        object.__setattr__(self, "_version", 0)
+        object.__setattr__(self, "_untracked", False)
         self.focal_length = 1.0
         self.aperture = 0.0
         self.dof_samples = 1
@@ -108,6 +144,21 @@ class ViewportCamera:
         self.aperture = aperture
         self.dof_samples = dof_samples
         return self
+
+    def __setattr__(self, name, value):
+        if name in self._VECS:
+            if isinstance(value, np.ndarray):
+                value = value.copy()
+                value.setflags(write=False)
+            else:
+                object.__setattr__(self, "_untracked", True)
+        elif name == "motion_times" and isinstance(value, list):
+            value = _Times(value, self)
+        object.__setattr__(self, name, value)
+        self._bump()
+
+    def _bump(self):
+        object.__setattr__(self, "_version", self._version + 1)
 
     def set_motion(self, time, motion_samples, motion_final):
         dt = time / motion_samples

@@ -191,21 +191,29 @@ class Scene:
 
     def _camera_key(self, subimage, tasks):
         """Every value camera_tables / camera_desc read, so a moved camera, new lens,
-        motion or sample settings, or a new noise stream re-uploads the tables."""
+        motion or sample settings, or a new noise stream re-uploads the tables. A
+        version-tracked camera (rtx.helperclasses.ViewportCamera) stands for its values
+        by (identity, version); other camera objects (the reference's own, bound by
+        Scene.from_reference) are compared value by value."""
         vc = self.vc
+        noise = self._noise_key()
+        if getattr(vc, "_untracked", True) is False:
+            return (subimage, tasks, vc, vc._version, self.samples, self.jitter, self.seed, noise)
         vecs = b"".join(np.asarray(v, np.float32).tobytes() for v in (vc.position, vc.u, vc.v, vc.w))
-        noise = None
-        if self.jitter and self.jitter_noise is not None:
-            # the digest of a replayed stream is cached per array object (a new stream is a
-            # new array; mutate one in place and call invalidate())
-            src = self.jitter_noise
-            if getattr(self, "_noise_src", None) is not src:
-                a = np.ascontiguousarray(np.asarray(src, np.float64))
-                self._noise_src, self._noise_digest = src, (a.size, hashlib.blake2b(a.tobytes(), digest_size=16).digest())
-            noise = self._noise_digest
         return (subimage, tasks, vc.width, vc.height, vc.left, vc.right, vc.top, vc.bottom, vecs, vc.d,
                 vc.focal_length, vc.aperture, vc.dof_samples, tuple(vc.motion_times), self.samples, self.jitter,
                 self.seed, noise)
+
+    def _noise_key(self):
+        if not (self.jitter and self.jitter_noise is not None):
+            return None
+        # the digest of a replayed stream is cached per array object (a new stream is a
+        # new array; mutate one in place and call invalidate())
+        src = self.jitter_noise
+        if getattr(self, "_noise_src", None) is not src:
+            a = np.ascontiguousarray(np.asarray(src, np.float64))
+            self._noise_src, self._noise_digest = src, (a.size, hashlib.blake2b(a.tobytes(), digest_size=16).digest())
+        return self._noise_digest
 
     def _set_camera(self, subimage, tasks):
         key = self._camera_key(subimage, tasks)

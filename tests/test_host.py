@@ -202,3 +202,46 @@ def test_f32_helpers_follow_glm_order():
     assert F.dot(a, b) == np.float32(np.float32(1e8 + np.float32(1.0)) - np.float32(1e8))
     v = F.normalize(np.array([3, 4, 0], np.float32))
     assert v.dtype == np.float32 and abs(float(F.length(v)) - 1) < 1e-6
+
+
+def test_camera_key_follows_every_camera_change():
+    """Scene._camera_key (which decides when rtx_camera_set re-uploads the tables) is
+    cached by the camera's version: equal while nothing changes, new after an attribute
+    assignment, an in-place edit of motion_times, or a scene sample setting; the basis
+    vectors are read-only, so they change only by assignment."""
+    import pytest
+    import rtx
+    from rtx import f32 as F
+    sc = rtx.load_bundled_scene("TwoSpheresPlane", resolution=(64, 48))
+    vc = sc.vc
+    seen = [sc._camera_key(0, 1)]
+    assert sc._camera_key(0, 1) == seen[0]
+
+    def changed():
+        k = sc._camera_key(0, 1)
+        assert all(k != s for s in seen)
+        seen.append(k)
+
+    vc.set_camera(F.vec3(0.0, 2.0, 7.0), F.vec3(0.0, 0.0, 0.0), F.vec3(0.0, 1.0, 0.0), 40.0)
+    changed()
+    vc.motion_times.append(0.5)
+    changed()
+    vc.motion_times[1] = 0.25
+    changed()
+    vc.motion_times += [1.0]
+    changed()
+    vc.aperture = 0.1
+    changed()
+    sc.samples = 2
+    changed()
+    sc.seed = 7
+    changed()
+    assert sc._camera_key(1, 2) != sc._camera_key(0, 1)
+    with pytest.raises(ValueError):
+        vc.position[0] = 1.0  # read-only: move the camera by assigning a vector
+    assert vc.motion_times == [0, 0.25, 1.0]
+    # a camera vector of another type: every render compares the values themselves
+    vc.position = [0.0, 2.0, 7.5]
+    k1 = sc._camera_key(0, 1)
+    vc.position[2] = 8.0
+    assert sc._camera_key(0, 1) != k1
