@@ -67,6 +67,30 @@ RTX_HD float dot(f3 a, f3 b) {
 RTX_HD f3 cross(f3 a, f3 b) {
     return f3{a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y};
 }
+// Wave votes as one ballot of the predicate's lane mask (no bool -> int -> compare round
+// trip through a VGPR): true if the predicate holds in ANY / ALL active lanes; the host
+// emulation runs a single lane.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RTX_ANY(p) (__builtin_amdgcn_ballot_w64((bool)(p)) != 0)
+#define RTX_ALL(p) (__builtin_amdgcn_ballot_w64((bool)(p)) == __builtin_amdgcn_ballot_w64(true))
+#else
+#define RTX_ANY(p) ((bool)(p))
+#define RTX_ALL(p) ((bool)(p))
+#endif
+
+// Marks the start of a rarely taken wave-uniform branch: an asm statement cannot be
+// speculated, so the compiler keeps the block behind the branch instead of computing it
+// in every wave and selecting (if-conversion of the IEEE normalize fallback and of the
+// spheres' second roots cost TwoSpheresPlane 4 %, DepthOfField 3 %).
+#ifndef RTX_NORM_BRANCH
+#define RTX_NORM_BRANCH 1
+#endif
+RTX_HD void unspeculated() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (RTX_NORM_BRANCH) asm volatile("");
+#endif
+}
+
 // glm::normalize = v * inversesqrt(dot(v, v)), inversesqrt(x) = 1 / sqrt(x)
 RTX_HD f3 normalize(f3 v) {
     const float q = dot(v, v);
@@ -77,7 +101,8 @@ RTX_HD f3 normalize(f3 v) {
     // the same IEEE results from the hardware approximations (rtx_fastmath.h) when every
     // active lane's dot is in range -- the common case; the compiler's sequence otherwise
     const bool fast = q >= fm::kLo && q < fm::kHi;  // false for NaN
-    if (__all((int)fast)) return scale(v, fm::rcp_rn(fm::sqrt_rn(q)));
+    if (RTX_ALL(fast)) return scale(v, fm::rcp_rn(fm::sqrt_rn(q)));
+    unspeculated();
 #endif
     float inv = 1.0f / sqrtf(q);
 #endif
@@ -392,15 +417,7 @@ constexpr float kEps4Up = 0x1.a36e3p-14f;      // smallest float > 1e-4
 constexpr float kEps4Near = 1e-4f;             // fl32(1e-4) (< 1e-4)
 constexpr float kEps3Near = 1e-3f;             // fl32(1e-3)
 
-// Wave-uniform predicates: true if the predicate holds in ANY / ALL active lanes (one
-// ballot on the device); the host emulation runs a single lane.
-#if defined(__HIP_DEVICE_COMPILE__)
-#define RTX_ANY(p) (__any((int)(p)) != 0)
-#define RTX_ALL(p) (__all((int)(p)) != 0)
-#else
-#define RTX_ANY(p) ((bool)(p))
-#define RTX_ALL(p) ((bool)(p))
-#endif
+// Wave-uniform predicates: RTX_ANY / RTX_ALL (defined with normalize above).
 
 // A value every active lane holds, as a wave-uniform (scalar) value.
 RTX_HD int32_t wave_uniform(int32_t x) {
@@ -1578,7 +1595,12 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
             double b, s, two_a;
             if (sphere_roots(o, d, ctr, ob.r2, b, s, two_a)) {
                 double t = (-b - s) / two_a;
-                if (!(t > 0.0)) { t = (-b + s) / two_a; root = 1; }
+                const bool near = t > 0.0;
+                // the far root only where some lane needs it (a ray from inside the sphere)
+                if (RTX_ANY(!near)) {
+                    unspeculated();
+                    if (!near) { t = (-b + s) / two_a; root = 1; }
+                }
                 valid = t > 0.0;
                 t32 = (float)t;
             }
@@ -1811,9 +1833,12 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
                                 : sphere_roots_oc(d, oc, q, ob.r2, b, s, two_a)) {
                 const double t1 = (-b - s) / two_a;
                 bool hit = 1e-3 < t1 && t1 < t_max;
-                if (!hit) {
-                    const double t2 = (-b + s) / two_a;
-                    hit = 1e-3 < t2 && t2 < t_max;
+                if (RTX_ANY(!hit)) {  // the second root only where some lane needs it
+                    unspeculated();
+                    if (!hit) {
+                        const double t2 = (-b + s) / two_a;
+                        hit = 1e-3 < t2 && t2 < t_max;
+                    }
                 }
                 occ = hit;
             }
@@ -1978,7 +2003,7 @@ RTX_HD double spec_pow(double x, const DMat& m, int pow_bits) {
         double r = 1.0, b = x;
         for (int k = 0; k < pow_bits; ++k) {
 #if defined(__HIP_DEVICE_COMPILE__)
-            if (!__any(n >> k)) break;  // wave-uniform exit once no lane has bits left
+            if (!RTX_ANY(n >> k)) break;  // wave-uniform exit once no lane has bits left
 #endif
             const double rb = r * b;
             r = ((n >> k) & 1) ? rb : r;
