@@ -372,6 +372,7 @@ RTX_HD int32_t floor_diff(float a, float b) {
     const float d = a - b;
     const float f = floorf(d);
     if (fabsf(d) < 0x1p23f && d != f) return (int32_t)f;
+    unspeculated();
     return (int32_t)(int64_t)floor((double)a - (double)b);
 }
 
@@ -440,10 +441,12 @@ struct Hit {
 // t64 > T for t64 = fl64(num / den), with T32 = fl32(T).
 RTX_HD bool quot_gt(float t32, float num, float den, double T, float T32) {
     if (t32 != T32) return t32 > T32;
+    unspeculated();  // (the fp64 quotient only for lanes at the threshold's float)
     return (double)num / (double)den > T;
 }
 RTX_HD bool quot_lt(float t32, float num, float den, double T, float T32) {
     if (t32 != T32) return t32 < T32;
+    unspeculated();
     return (double)num / (double)den < T;
 }
 // t64 >= 0 and t64 < 0 for t64 = fl64(num / den), den != 0, from t32 = fl32(num / den):
@@ -1799,6 +1802,7 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
             if (above >= 0 && below >= 0) {
                 hit = above == 1 && below == 1;
             } else {
+                unspeculated();  // (the correctly rounded quotient only near a threshold)
                 const float t32 = num / denom;
                 hit = quot_gt(t32, num, denom, 1e-4, kEps4Near) && quot_lt(t32, num, denom, t_max, tmax32);
             }
@@ -1985,6 +1989,9 @@ RTX_HD Surface resolve_hit(const SceneView& S, const Hit& h, const HHit& hh, f3 
 // scenes never use.
 __host__ __device__ __attribute__((noinline)) inline double pow_general(double x, double y) { return pow(x, y); }
 
+#ifndef RTX_SPEC_UNIFORM
+#define RTX_SPEC_UNIFORM 1
+#endif
 // `x ** hardness` (CPython float_pow -> pow) in fp64. Integer exponents use binary
 // exponentiation; the fp32 cast that follows makes it equal to libm pow except when the
 // exact value lies within a few fp64 ulps of an fp32 rounding boundary. The loop runs a
@@ -1999,6 +2006,22 @@ RTX_HD double spec_pow(double x, const DMat& m, int pow_bits) {
 #else
     if (m.hard_is_int) {
         const int n = m.hard_int;
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(RTX_FIXED_HARD)
+        // every lane shading the same exponent (the common case: a tile of one material):
+        // a scalar loop performs only the multiplications of the set bits, in the same order
+        if (RTX_SPEC_UNIFORM) {
+            const int n0 = __builtin_amdgcn_readfirstlane(n);
+            if (RTX_ALL(n == n0)) {
+                double r = 1.0, b = x;
+                for (int k = 0; k < pow_bits && (n0 >> k) != 0; ++k) {
+                    if ((n0 >> k) & 1) r = r * b;
+                    if ((n0 >> (k + 1)) != 0) b = b * b;  // (the last square is never used)
+                }
+                return r;
+            }
+            unspeculated();
+        }
 #endif
         double r = 1.0, b = x;
         for (int k = 0; k < pow_bits; ++k) {
