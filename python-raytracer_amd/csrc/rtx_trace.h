@@ -1989,9 +1989,6 @@ RTX_HD Surface resolve_hit(const SceneView& S, const Hit& h, const HHit& hh, f3 
 // scenes never use.
 __host__ __device__ __attribute__((noinline)) inline double pow_general(double x, double y) { return pow(x, y); }
 
-#ifndef RTX_SPEC_UNIFORM
-#define RTX_SPEC_UNIFORM 1
-#endif
 // `x ** hardness` (CPython float_pow -> pow) in fp64. Integer exponents use binary
 // exponentiation; the fp32 cast that follows makes it equal to libm pow except when the
 // exact value lies within a few fp64 ulps of an fp32 rounding boundary. The loop runs a
@@ -2006,22 +2003,6 @@ RTX_HD double spec_pow(double x, const DMat& m, int pow_bits) {
 #else
     if (m.hard_is_int) {
         const int n = m.hard_int;
-#endif
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(RTX_FIXED_HARD)
-        // every lane shading the same exponent (the common case: a tile of one material):
-        // a scalar loop performs only the multiplications of the set bits, in the same order
-        if (RTX_SPEC_UNIFORM) {
-            const int n0 = __builtin_amdgcn_readfirstlane(n);
-            if (RTX_ALL(n == n0)) {
-                double r = 1.0, b = x;
-                for (int k = 0; k < pow_bits && (n0 >> k) != 0; ++k) {
-                    if ((n0 >> k) & 1) r = r * b;
-                    if ((n0 >> (k + 1)) != 0) b = b * b;  // (the last square is never used)
-                }
-                return r;
-            }
-            unspeculated();
-        }
 #endif
         double r = 1.0, b = x;
         for (int k = 0; k < pow_bits; ++k) {
