@@ -969,31 +969,37 @@ RTX_HD f3 box_normal(int label, f3 d) {
 
 // Every hit of one leaf, in the reference's list order, with fp64 t (leaves of
 // hierarchies are few: no fp32 proxies). emit(t64, position, normal, material).
+// Spheres, planes and boxes emit through ONE call site (a loop over their <= 2 hits), so
+// the walk-up the caller's emit inlines is compiled once per leaf_hits, not once per hit
+// kind.
 template <bool MESH, class O, class Emit>
 RTX_HD void leaf_hits(const SceneView& S, const O& ob, f3 o, f3 d, float time, Emit&& emit) {
+    double th[2];
+    int nh = 0;
+    f3 c = mk(0.0f, 0.0f, 0.0f), nb = mk(0.0f, 0.0f, 0.0f);
     if (ob.type == OBJ_SPHERE) {  // simple_geometry.py:20-46
-        const f3 c = moved(ob, ob.a, time);
+        c = moved(ob, ob.a, time);
         double b, s, two_a;
         if (!sphere_roots(o, d, c, ob.r2, b, s, two_a)) return;
         const double t1 = (-b - s) / two_a, t2 = (-b + s) / two_a;
-        if (t1 > 0.0) { const f3 p = get_point(o, d, t1); emit(t1, p, normalize(sub(p, c)), ob.mat0); }
-        if (t2 > 0.0) { const f3 p = get_point(o, d, t2); emit(t2, p, normalize(sub(p, c)), ob.mat0); }
+        if (t1 > 0.0) th[nh++] = t1;
+        if (t2 > 0.0) th[nh++] = t2;
     } else if (ob.type == OBJ_PLANE) {  // :105-120
-        const f3 n = ld3(ob.b);
-        const float den = dot(d, n);
+        nb = ld3(ob.b);
+        const float den = dot(d, nb);
         if (!(fabsf(den) >= kEps4Up)) return;
-        const double t = (double)dot(sub(moved(ob, ob.a, time), o), n) / (double)den;
+        const double t = (double)dot(sub(moved(ob, ob.a, time), o), nb) / (double)den;
         if (!(t >= 0.0)) return;
-        const f3 p = get_point(o, d, t);
-        emit(t, p, n, plane_material(ob, p, time));
+        th[nh++] = t;
     } else if (ob.type == OBJ_BOX) {  // :188-249 (entry, then exit, both with the entry normal)
         double start, end;
         int label;
         if (!box_slabs(o, d, moved(ob, ob.a, time), moved(ob, ob.b, time), start, label, end)) return;
         if (start > end || start < 0.0) return;
-        const f3 nb = box_normal(label, d);
-        emit(start, get_point(o, d, start), nb, ob.mat0);
-        emit(end, get_point(o, d, end), nb, ob.mat0);
+        nb = box_normal(label, d);
+        th[0] = start;
+        th[1] = end;
+        nh = 2;
     } else if (MESH && ob.type == OBJ_MESH) {  // mesh.py:72-119, faces in OBJ order
         if (!mesh_bv(ob, o, d)) return;
         for (int f = 0; f < ob.tri_count; ++f) {
@@ -1009,6 +1015,15 @@ RTX_HD void leaf_hits(const SceneView& S, const O& ob, f3 o, f3 d, float time, E
                 dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n) >= 0.0f)
                 emit(t, p, ob.flat ? n : smooth_normal(T, (DTriN)S.trins[ob.tri_begin + f], p), ob.mat0);
         }
+        return;
+    }
+#pragma unroll 1
+    for (int k = 0; k < nh; ++k) {
+        const double t = k ? th[1] : th[0];
+        const f3 p = get_point(o, d, t);
+        f3 nrm = nb;
+        if (ob.type == OBJ_SPHERE) nrm = normalize(sub(p, c));
+        emit(t, p, nrm, ob.type == OBJ_PLANE ? plane_material(ob, p, time) : ob.mat0);
     }
 }
 
@@ -1147,11 +1162,18 @@ RTX_HD bool pt_in(const float RTX_CONST* lo, const float RTX_CONST* hi, f3 p) {
     return lo[0] <= p.x && p.x <= hi[0] && lo[1] <= p.y && p.y <= hi[1] && lo[2] <= p.z && p.z <= hi[2];
 }
 
-// Inlining of the rarely-divergent CSG helpers (experiment knob; see tools/ablate.sh).
-// 2: everything inlined; 1: is_inside / get_material / walk_up out of line; 0: also
-// hier_closest / hier_shadow.
+// Inlining of the CSG helpers. 2 (default): everything inlined; 1: is_inside /
+// get_material / walk_up out of line; 0: also hier_closest / hier_shadow. Each helper has
+// ONE call site per enumeration (leaf_hits emits through one site, diff_shadow enumerates
+// both children through one hier_enum, hier_shadow reaches every difference node through
+// one diff_shadow, walk_up tests siblings through one is_inside), so inlining no longer
+// multiplies them: the NovelScene1 kernel went from 110 call sites (50 walk_up, 40
+// is_inside), 230 VGPRs and 961 SGPR spills to 195 VGPRs and 262 SGPR spills with no
+// hierarchy calls; NovelScene1 29.0 -> 27.9 ms, NovelScene2 155 -> 143 ms (same box,
+// profiles/r03/csg_inline/). Out of line (1) the restructured code measured 30.3 ms, and
+// occupancy bounds of 3 and 4 waves/SIMD spill (29.6, 36.9 ms).
 #ifndef RTX_HIER_INLINE
-#define RTX_HIER_INLINE 1
+#define RTX_HIER_INLINE 2
 #endif
 #if RTX_HIER_INLINE >= 2
 #define RTX_HX RTX_HD
@@ -1227,15 +1249,18 @@ RTX_HX bool walk_up(const SceneView& S, const HStack& hs, int cur, int stop, flo
         cref<DNodeHot> c = S.nodes[cur];
         const int a = c.parent;
         cref<DNodeHot> A = S.nodes[a];
-        if (A.kind == HN_INTER) {
-            for (int j = a + 1; j < A.end; j = S.nodes[j].end)
-                if (j != cur && !is_inside(S, hs, j, pos, time)) return false;
-        } else if (A.kind == HN_DIFF) {
+        if (A.kind == HN_INTER || A.kind == HN_DIFF) {
+            // intersection: every other child must contain the hit; difference: child 1 must
+            // not contain a child-0 hit, child 0 must contain a child-1 hit (one is_inside site)
+            const bool inter = A.kind == HN_INTER;
             const int c0 = a + 1, c1 = S.nodes[c0].end;
-            if (c.cidx == 0) {
-                if (is_inside(S, hs, c1, pos, time)) return false;
-            } else {
-                if (!is_inside(S, hs, c0, pos, time)) return false;
+            const bool keep = inter || c.cidx != 0;  // the is_inside answer that keeps the hit
+            for (int j = inter ? c0 : (c.cidx == 0 ? c1 : c0); j < A.end; j = S.nodes[j].end) {
+                if (j == cur) continue;
+                if (is_inside(S, hs, j, pos, time) != keep) return false;
+                if (!inter) break;
+            }
+            if (!inter && c.cidx != 0) {
                 mat = get_material(S, hs, c0, pos, time);
                 n = neg(n);
             }
@@ -1261,31 +1286,26 @@ RTX_HD void hier_enum(const SceneView& S, const HStack& hs, int s, float time, W
     };
     cref<DNodeHot> root = S.nodes[s];
     if (culled(s, root.depth)) return;
-    auto visit_leaf = [&](int li, int32_t depth, int32_t obj) {
-        f3 lo, ld;
-        hs.get_ray(depth, lo, ld);
-        cref<DObj> ob = S.objs[obj];
-        leaf_hits<MESH>(S, ob, lo, ld, time, [&](double t, f3 pos, f3 n, int32_t mat) {
-            if (!want(t)) return;
-            if (walk_up(S, hs, li, s, time, pos, n, mat)) take(t, pos, n, mat, obj);
-        });
-    };
-    if (root.kind == HN_LEAF) { visit_leaf(s, root.depth, root.obj); return; }
     if (root.kind == HN_OTHER) return;  // unknown hierarchy_type: no hits
-    {
-        f3 ro, rd;
-        hs.get_ray(root.depth, ro, rd);
-        hs.put_ray(root.depth + 1, xform(S.nmat[s].Minv, ro, 1.0f), xform(S.nmat[s].Minv, rd, 0.0f));
-    }
-    for (int i = s + 1; i < root.end;) {
+    // preorder from s itself (a leaf root is visited once), one leaf visit site
+    for (int i = s; i < root.end;) {
         cref<DNodeHot> c = S.nodes[i];
-        if (c.pkind == HN_DIFF && c.cidx >= 2) { i = c.end; continue; }  // difference reads children 0, 1
-        if (culled(i, c.depth)) { i = c.end; continue; }
-        if (c.kind == HN_LEAF) { visit_leaf(i, c.depth, c.obj); ++i; continue; }
-        if (c.kind == HN_OTHER) { i = c.end; continue; }
+        if (i != s) {
+            if (c.pkind == HN_DIFF && c.cidx >= 2) { i = c.end; continue; }  // difference reads children 0, 1
+            if (culled(i, c.depth)) { i = c.end; continue; }
+            if (c.kind == HN_OTHER) { i = c.end; continue; }
+        }
         f3 ro, rd;
         hs.get_ray(c.depth, ro, rd);
-        hs.put_ray(c.depth + 1, xform(S.nmat[i].Minv, ro, 1.0f), xform(S.nmat[i].Minv, rd, 0.0f));
+        if (c.kind == HN_LEAF) {
+            const int32_t obj = c.obj, li = i;
+            leaf_hits<MESH>(S, S.objs[obj], ro, rd, time, [&](double t, f3 pos, f3 n, int32_t mat) {
+                if (!want(t)) return;
+                if (walk_up(S, hs, li, s, time, pos, n, mat)) take(t, pos, n, mat, obj);
+            });
+        } else {
+            hs.put_ray(c.depth + 1, xform(S.nmat[i].Minv, ro, 1.0f), xform(S.nmat[i].Minv, rd, 0.0f));
+        }
         ++i;
     }
 }
@@ -1304,10 +1324,13 @@ RTX_HD bool diff_shadow(const SceneView& S, const HStack& hs, int x, float time)
     bool found = false;
     auto want = [&](double t) { return !found && t > 1e-4; };
     auto cap = [&]() { return found ? -1.0f : INFINITY; };
-    auto take0 = [&](double, f3 pos, f3, int32_t, int32_t) { found = !is_inside(S, hs, c1, pos, time); };
-    hier_enum<MESH>(S, hs, c0, time, want, take0, cap);
-    auto take1 = [&](double, f3 pos, f3, int32_t, int32_t) { found = is_inside(S, hs, c0, pos, time); };
-    hier_enum<MESH>(S, hs, c1, time, want, take1, cap);
+    // child 0's hits count outside child 1, child 1's inside child 0 (one enumeration site)
+#pragma unroll 1
+    for (int k = 0; k < 2; ++k) {
+        const int mine = k ? c1 : c0, other = k ? c0 : c1;
+        auto take = [&](double, f3 pos, f3, int32_t, int32_t) { found = is_inside(S, hs, other, pos, time) == (k != 0); };
+        hier_enum<MESH>(S, hs, mine, time, want, take, cap);
+    }
     return found;
 }
 
@@ -1324,13 +1347,29 @@ RTX_HY bool hier_shadow(const SceneView& S, const HStack& hs, int r, f3 o, f3 d,
     if (!RTX_ANY(ray_meets(S.sbox[r].lo, S.sbox[r].hi, o, d, INFINITY))) return false;
     cref<DNodeHot> R = S.nodes[r];
     if (R.kind == HN_OTHER) return false;
-    if (R.kind == HN_DIFF) return diff_shadow<MESH>(S, hs, r, time);
-    hs.put_ray(1, xform(S.nmat[r].Minv, o, 1.0f), xform(S.nmat[r].Minv, d, 0.0f));
-    uint32_t acc = hinit(0u, R.kind, 0);
+    // difference nodes (the root or inner ones) are evaluated at ONE diff_shadow site: dx
+    // is the pending node (wave-uniform), dlive whether this lane's ray meets its box
+    const bool root_diff = R.kind == HN_DIFF;
+    int dx = root_diff ? r : -1, dend = 0;
+    int32_t dcidx = 0;
+    bool dlive = true;
+    uint32_t acc = 0u;
+    if (!root_diff) {
+        hs.put_ray(1, xform(S.nmat[r].Minv, o, 1.0f), xform(S.nmat[r].Minv, d, 0.0f));
+        acc = hinit(0u, R.kind, 0);
+    }
     int open = r;
     int32_t okind = R.kind, odepth = R.depth, oend = R.end, oparent = R.parent, ocidx = R.cidx;
     int i = r + 1;
     for (;;) {
+        if (dx >= 0) {
+            bool v = false;
+            if (dlive) v = diff_shadow<MESH>(S, hs, dx, time);
+            if (root_diff) return v;
+            acc = hfold(acc, okind, odepth, dcidx, v);
+            i = dend;
+            dx = -1;
+        }
         while (i >= oend) {
             const bool v = ((acc >> odepth) & 1u) != 0u;
             if (open == r) return v;
@@ -1359,8 +1398,10 @@ RTX_HY bool hier_shadow(const SceneView& S, const HStack& hs, int r, f3 o, f3 d,
             acc = hfold(acc, okind, odepth, c.cidx, false);
             i = c.end;
         } else if (c.kind == HN_DIFF) {
-            acc = hfold(acc, okind, odepth, c.cidx, live && diff_shadow<MESH>(S, hs, i, time));
-            i = c.end;
+            dx = i;
+            dlive = live;
+            dcidx = c.cidx;
+            dend = c.end;
         } else {
             f3 ro, rd;
             hs.get_ray(c.depth, ro, rd);
@@ -1371,6 +1412,18 @@ RTX_HY bool hier_shadow(const SceneView& S, const HStack& hs, int r, f3 o, f3 d,
             ++i;
         }
     }
+}
+
+// The shadow rays of every hierarchy root, for the lanes not yet occluded. (Out of line,
+// with hier_closest too, the kernel measured 247 VGPRs against 195 inlined: the calls cost
+// more registers than they isolate.)
+template <bool MESH>
+RTX_HD bool hier_occluded(const SceneView& S, const HStack& hs, f3 o, f3 d, double t_max, float time, bool occ) {
+    for (int r = 0; r < S.n_nodes; r = S.nodes[r].end) {
+        if (RTX_ALL(occ)) break;
+        if (!occ) occ = hier_shadow<MESH>(S, hs, r, o, d, t_max, time);
+    }
+    return occ;
 }
 
 // Best hierarchy hit: the surface the walk-up produced (world frame).
@@ -1936,12 +1989,7 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
             }
         }
     }
-    if (X && RTX_ABLATE != 10) {  // hierarchies (hierarchy.py:80-109)
-        for (int r = 0; r < S.n_nodes; r = S.nodes[r].end) {
-            if (RTX_ALL(occ)) break;
-            if (!occ) occ = hier_shadow<MESH>(S, hs, r, o, d, t_max, time);
-        }
-    }
+    if (X && RTX_ABLATE != 10) occ = hier_occluded<MESH>(S, hs, o, d, t_max, time, occ);  // hierarchy.py:80-109
     return occ;
 }
 
