@@ -545,6 +545,15 @@ int convert_scene(const rtx_scene_desc* desc, HostScene& H) {
                 break;
             }
             case RTX_BOX:
+                // the padded pre-test's inputs of a static box (rtx_trace.h box_maybe_hit_obj):
+                // sorted corners in c / e, max |coordinate| in c[3], as the kernel forms them
+                for (int k = 0; k < 3; ++k) {
+                    d.c[k] = std::fmin(d.a[k], d.b[k]);
+                    d.e[k] = std::fmax(d.a[k], d.b[k]);
+                }
+                d.c[3] = std::fmax(std::fmax(std::fmax(std::fabs(d.a[0]), std::fabs(d.a[1])),
+                                             std::fmax(std::fabs(d.a[2]), std::fabs(d.b[0]))),
+                                   std::fmax(std::fabs(d.b[1]), std::fabs(d.b[2])));
                 break;
             case RTX_MESH:
                 if (o.tri_begin < 0 || o.tri_count < 0 || (int64_t)o.tri_begin + o.tri_count > desc->n_triangles)
@@ -558,6 +567,14 @@ int convert_scene(const rtx_scene_desc* desc, HostScene& H) {
                 d.flat = o.flat ? 1 : 0;
                 set3(d.bv_a, o.bv_a);
                 set3(d.bv_b, o.bv_b);
+                // the bounding box's padded pre-test inputs (rtx_trace.h bv_maybe), as for boxes
+                for (int k = 0; k < 3; ++k) {
+                    d.c[k] = std::fmin(d.bv_a[k], d.bv_b[k]);
+                    d.e[k] = std::fmax(d.bv_a[k], d.bv_b[k]);
+                }
+                d.c[3] = std::fmax(std::fmax(std::fmax(std::fabs(d.bv_a[0]), std::fabs(d.bv_a[1])),
+                                             std::fmax(std::fabs(d.bv_a[2]), std::fabs(d.bv_b[0]))),
+                                   std::fmax(std::fabs(d.bv_b[1]), std::fabs(d.bv_b[2])));
                 d.bv_r2 = std::pow(o.bv_radius, 2.0);  // BoundingSphere: self.radius ** 2
                 break;
             default:

@@ -786,13 +786,28 @@ RTX_HD bool box_maybe_hit(f3 mn, f3 mx, f3 o, const RayInv& ri, float tcap) {
     return leaf_maybe_hit(B, o, ri, cm, tcap);
 }
 
+// The same pre-test from a box's record: a static box carries its sorted corners and max
+// |coordinate| (rtx_api.hip convert_scene: c = lo, e = hi, c[3] = max), so the per-ray test
+// skips the wave-uniform min / max / abs work (VALU on scalar values); a moving box forms
+// them from its moved corners.
+template <class O>
+RTX_HD bool box_maybe_hit_obj(const O& ob, f3 mn, f3 mx, f3 o, const RayInv& ri, float tcap) {
+#if !(defined(RTX_FIXED_STATIC) && RTX_FIXED_STATIC)
+    if (ob.has_speed) return box_maybe_hit(mn, mx, o, ri, tcap);
+#endif
+    const Box3 B{{ob.c[0], ob.c[1], ob.c[2]}, {ob.e[0], ob.e[1], ob.e[2]}};
+    return leaf_maybe_hit(B, o, ri, ob.c[3], tcap);
+}
+
 // Conservative pre-test of a mesh's bounding volume: false only when the exact test
 // (mesh_bv) cannot pass with an entry at or before tcap. An AABB volume passes only rays
 // that enter it at start >= 0, and every face hit inside it lies beyond that entry, so the
 // padded box of the clusters' bound (box_maybe_hit) decides; sphere volumes always pass.
 template <class O>
 RTX_HD bool bv_maybe(const O& ob, f3 o, const RayInv& ri, float tcap) {
-    return ob.bv_type != BV_AABB || box_maybe_hit(ld3(ob.bv_a), ld3(ob.bv_b), o, ri, tcap);
+    // (the record carries the sorted corners and max |coordinate|, as for boxes)
+    return ob.bv_type != BV_AABB ||
+           leaf_maybe_hit(Box3{{ob.c[0], ob.c[1], ob.c[2]}, {ob.e[0], ob.e[1], ob.e[2]}}, o, ri, ob.c[3], tcap);
 }
 
 // Exact fp64 t of a candidate, recomputed from the object exactly as during its test
@@ -1680,7 +1695,7 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
             valid = box_entry_iv(o, d, mn, mx, iv, maybe, start, label);
         } else {
             // the fp64 slabs only where some lane's ray may hit the box before its best t
-            const bool maybe = box_maybe_hit(mn, mx, o, ri, h.t32);
+            const bool maybe = box_maybe_hit_obj(ob, mn, mx, o, ri, h.t32);
             if (!RTX_ANY(maybe)) continue;
             valid = box_entry(o, d, mn, mx, maybe, start, label, &ri);
         }
@@ -1915,7 +1930,7 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
             if (!RTX_ANY(maybe)) continue;
             if (maybe) occ = box_shadow_iv(o, d, mn, mx, iv, t_max);
         } else {
-            const bool maybe = !occ && box_maybe_hit(mn, mx, o, ri, INFINITY);
+            const bool maybe = !occ && box_maybe_hit_obj(ob, mn, mx, o, ri, INFINITY);
             if (!RTX_ANY(maybe)) continue;
             if (maybe) occ = box_shadow(o, d, mn, mx, t_max, &ri);
         }
