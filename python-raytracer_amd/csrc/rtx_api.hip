@@ -216,7 +216,13 @@ void hb_store(const HBox& b, float* lo, float* hi) {
         if ((double)lo[k] > b.lo[k]) lo[k] = std::nextafter(lo[k], -INFINITY);
         if ((double)hi[k] < b.hi[k]) hi[k] = std::nextafter(hi[k], INFINITY);
     }
-    lo[3] = hi[3] = 0.0f;
+    // lo[3]: the culling test's max |coordinate| (rtx_trace.h ray_meets), -inf for an empty
+    // box (lo > hi on some axis, or NaN)
+    const bool nonempty = lo[0] <= hi[0] && lo[1] <= hi[1] && lo[2] <= hi[2];
+    lo[3] = nonempty ? std::fmax(std::fmax(std::fmax(std::fabs(lo[0]), std::fabs(lo[1])), std::fmax(std::fabs(lo[2]), std::fabs(hi[0]))),
+                                 std::fmax(std::fabs(hi[1]), std::fabs(hi[2])))
+                     : -INFINITY;
+    hi[3] = 0.0f;
 }
 
 struct NodeBoxes {
@@ -528,6 +534,7 @@ int convert_scene(const rtx_scene_desc* desc, HostScene& H) {
         switch (o.type) {
             case RTX_SPHERE:
                 d.r2 = std::pow(o.radius, 2.0);  // self.radius ** 2
+                d.r2f = (float)d.r2;
                 d.radius = o.radius;
                 break;
             case RTX_PLANE: {

@@ -137,7 +137,9 @@ struct alignas(16) DObj {
     int32_t has_speed, tri_begin, tri_count, bv_type;
     int32_t flat, oid, leaf_begin, leaf_count;   // mesh: BVH nodes (DLeaf range, preorder)
     float cmax;                                  // mesh: max |vertex coordinate|
-    int32_t face_cull, pad4, pad5;               // mesh: test each face's box before its exact test
+    int32_t face_cull;                           // mesh: test each face's box before its exact test
+    float r2f;                                   // sphere: (float)(radius ** 2), the fp32 filters' input
+    int32_t pad5;
     float a[4];       // sphere centre | plane point | box minpos
     float b[4];       // plane normal | box maxpos
     float c[4];       // plane width axis
@@ -1133,10 +1135,11 @@ RTX_HD bool ray_meets(const float RTX_CONST* lo, const float RTX_CONST* hi, f3 o
 #if defined(RTX_NO_CULL)
     return true;
 #endif
-    if (!box_nonempty(lo, hi)) return false;
+    // lo[3]: the box's max |coordinate|, or -inf when it is empty (rtx_api.hip hb_store), so
+    // no lane spends VALU on the wave-uniform emptiness test and maximum
+    const float bm = lo[3];
+    if (!(bm >= 0.0f)) return false;
     const float om = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
-    const float bm = fmaxf(fmaxf(fmaxf(fabsf(lo[0]), fabsf(lo[1])), fmaxf(fabsf(lo[2]), fabsf(hi[0]))),
-                           fmaxf(fabsf(hi[1]), fabsf(hi[2])));
     const float pad = 0x1p-8f * (om + bm);
     // v_rcp (1 ulp): its error moves an entry by ~2^-23 of (|box| + |o|) |1/d|, far
     // inside the pad's 2^-8 (|o| + |box|) |1/d|
@@ -1662,7 +1665,7 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
         bool valid = false;
         float t32 = INFINITY;
         int32_t root = 0;
-        if (sphere_disc_sign(o, d, ctr, (float)ob.r2) >= 0) {  // fp64 only where a hit is possible
+        if (sphere_disc_sign(o, d, ctr, ob.r2f) >= 0) {  // fp64 only where a hit is possible
             double b, s, two_a;
             if (sphere_roots(o, d, ctr, ob.r2, b, s, two_a)) {
                 double t = (-b - s) / two_a;
@@ -1896,10 +1899,10 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
 #endif
         int dec = -1;
         if (RTX_SHADOW_F32 && RTX_ABLATE != 4) {
-            dec = sphere_shadow_f32(d, oc, q, (float)ob.r2, tmax_dn, tmax_up);
+            dec = sphere_shadow_f32(d, oc, q, ob.r2f, tmax_dn, tmax_up);
             if (!occ && dec >= 0) occ = dec == 1;
         }
-        if (!occ && dec < 0 && sphere_disc_sign_oc(d, oc, q, (float)ob.r2) >= 0) {
+        if (!occ && dec < 0 && sphere_disc_sign_oc(d, oc, q, ob.r2f) >= 0) {
             double b, s, two_a;
             if (RTX_ABLATE == 4 ? sphere_roots(o, d, ctr, ob.r2, b, s, two_a)
                                 : sphere_roots_oc(d, oc, q, ob.r2, b, s, two_a)) {
