@@ -1293,12 +1293,15 @@ hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& k
     const char* lm = getenv("RTX_JIT_LIBMACROS");  // experiment: 0 = do not forward them
     if (!(lm && lm[0] == '0'))
         for (const char* m : kLibMacros) opts.push_back(m);
-    if (mesh && !sec && !ext && fc_mode == 1) {
-        // small meshes (every face box-culled): 5 waves/SIMD beat the mesh kernels' 4
-        // despite a 48 B/lane spill (TorusMesh 1080p 70.2 -> 66.2 us; the 81,920-face
-        // mesh, which has no face boxes, measured 1.4 % slower at 5)
+    if (!sec && !ext && (!mesh || fc_mode == 1)) {
+        // flat scenes and small meshes (every face box-culled): 6 waves/SIMD. With the
+        // host-side box precomputes the DepthOfField kernel fits 80 VGPRs with no more
+        // scratch than at 5: DepthOfField 4K 6.60 -> 6.28 ms, TorusMesh 1080p 54.6 -> 52.1 us,
+        // twice on one box; 8 waves are slower (6.89 ms, 57.8 us; profiles/r03/lb6/). (Round 2:
+        // small meshes 4 -> 5 waves, 70.2 -> 66.2 us.) The 81,920-face mesh, which has no face
+        // boxes, keeps the mesh kernels' 4 (1.4 % slower at 5).
         opts.push_back("-URTX_LB_WAVES");
-        opts.push_back("-DRTX_LB_WAVES(MESH,SEC)=5");
+        opts.push_back("-DRTX_LB_WAVES(MESH,SEC)=6");
     }
     if (const char* extra = getenv("RTX_JIT_FLAGS")) {  // experiments (tools/ablate.sh); part of the cache key
         std::istringstream is(extra);
