@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU session: NovelScene1 under library variants (tools/ab_lib.sh), then the default
 # configs with RTX_JIT_DUMP=1 (the specialized kernels' hiprtc options and source, for
-# offline ISA work with tools/jit_isa.sh).
+# offline ISA work with tools/jit_offline.py).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/${TAG:-r03s3}; mkdir -p $O
