@@ -1297,7 +1297,7 @@ hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& k
         // flat scenes and small meshes (every face box-culled): 6 waves/SIMD. With the
         // host-side box precomputes the DepthOfField kernel fits 80 VGPRs with no more
         // scratch than at 5: DepthOfField 4K 6.60 -> 6.28 ms, TorusMesh 1080p 54.6 -> 52.1 us,
-        // twice on one box; 8 waves are slower (6.89 ms, 57.8 us; profiles/r03/lb6/). (Round 2:
+        // twice on one box; 7 and 8 waves are slower (6.60 / 6.89 ms; profiles/r03/lb6/). (Round 2:
         // small meshes 4 -> 5 waves, 70.2 -> 66.2 us.) The 81,920-face mesh, which has no face
         // boxes, keeps the mesh kernels' 4 (1.4 % slower at 5).
         opts.push_back("-URTX_LB_WAVES");
