@@ -5,13 +5,14 @@ TwoSpheresPlane 1920x1080 @1/2/4/8 GPUs).
 The unit is the reference's: primary samples W*H*aa*dof*|times| per second (its tqdm bar,
 provided/scene.py:45,71). One step = one 1920x1080 1-spp frame of TwoSpheresPlane.
 N = 1: the frame is rendered into the fp32 framebuffer on one GPU.
-N > 1 (north star, "scaling": "strong"): every frame is split across the ranks — each
-renders its interleaved 8-row groups straight to uint8 on its GPU — and gathered to ONE
-rank over RCCL: frame k to rank k mod N (rtx.distributed.FrameExchange), the N frames of a
-group rendered in one batched launch and their gathers issued as one all_to_all that
-overlaps the next group's renders. Reported beside it: every frame gathered to
-rank 0 (rtx.distributed.FramePipeline, "gather_to_rank0", bounded by rank 0's ingress)
-and the frame-parallel rate (each rank its own frame, "weak_scaling").
+N > 1 ("scaling": "strong", the north star's 1 -> 8-GPU tile scaling): ONE frame per step,
+sharded across the ranks -- each renders its interleaved 8-row groups straight to uint8
+on its GPU -- and gathered to rank 0 by one RCCL gather, awaited before the next frame
+(measure_sharded). Reported beside it: the frame-stream throughput of one static scene
+state (rtx.distributed.FrameExchange, "throughput"), every frame gathered to rank 0 in a
+double-buffered stream ("gather_to_rank0") and the frame-parallel rate (each rank its own
+frame, "weak_scaling"). DepthOfField 4K (--config dof4k) is the render-bound scaling
+config; the TwoSpheresPlane 1080p frame is the metric's.
 
 Launch: python bench.py [--steps K --warmup W]          (N = 1)
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -267,28 +268,157 @@ def clock_warmup(fn, seconds, sync):
     return n, time.perf_counter() - t0
 
 
-def max_over_ranks(x, use_dist):
-    t = torch.tensor([float(x)], dtype=torch.float64, device="cuda")
+def max_over_ranks(x, use_dist, device="cuda"):
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     if use_dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
-def timed(fn, steps, use_dist):
+def cuda_sync():
+    torch.cuda.synchronize()
+
+
+def timed(fn, steps, use_dist, sync=cuda_sync, device="cuda"):
     """Wall time of `steps` calls of fn, bracketed by barrier + synchronize on both sides;
     the max over ranks is the job's time. Each rank's clock stops when its own work is done;
     the closing barrier keeps every rank inside the bracket."""
     if use_dist:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(steps):
         fn()
-    torch.cuda.synchronize()
+    sync()
     t1 = time.perf_counter()
     if use_dist:
         dist.barrier()
-    return max_over_ranks(t1 - t0, use_dist)
+    return max_over_ranks(t1 - t0, use_dist, device)
+
+
+def measure_sharded(sc, rank, world, steps, warmup, use_dist, device, sync=cuda_sync, stream=None,
+                    render_rows=None, render_block=None, render_block_k=None, graph=True):
+    """The N > 1 measurements (bench.py's multi-GPU leg; at N = 1 with --pipeline a
+    rehearsal). Renderers default to the HIP kernels on this rank's GPU; the CPU tests
+    inject the host emulation (tests/test_bench_multirank.py).
+
+    - value: ONE frame sharded over the ranks, frame by frame. Every step renders this
+      rank's interleaved 8-row groups of the frame straight to uint8 (fused
+      rtx_render_groups_rgb8, one launch per frame) and gathers them to rank 0 (one RCCL
+      gather), awaited before the next frame starts; rank 0 puts the rows in image order.
+      No batching and no overlap across frames: the latency of one frame, the reference's
+      one-frame-per-run strip render + glue (render.nu:10-15, provided/glue.py:17-27).
+    - throughput: the frame stream of one static scene state (rtx.distributed.FrameExchange:
+      frame k to rank k mod N, N frames per batched launch and per all_to_all, overlapped).
+    - gather_to_rank0: the same stream with every frame gathered to rank 0 (FramePipeline).
+    Returns a dict (times are the max over ranks) and, on rank 0, the last frame of the
+    value loop ([H, W, 3] uint8)."""
+    from rtx.distributed import FrameExchange, FrameGather, FramePipeline
+    H, W = sc.vc.height, sc.vc.width
+    spp = sc.samples_per_pixel
+    single = FrameGather(H, W, 3, world, rank, torch.uint8, device, interleave=True, dst=0)
+    if render_rows is None:
+        def render_rows(out):
+            sc.render_device(groups=(rank, world), out=out, stream=stream)
+    last = [None]
+
+    def one_frame():
+        if single.nrows:
+            render_rows(single.block)
+        w = single.start(async_op=True)
+        if w is not None:
+            w.wait()
+        if rank == 0:
+            last[0] = single.frame()
+    for _ in range(warmup):
+        one_frame()
+    sync()
+    frame_s = timed(one_frame, steps, use_dist, sync, device)
+
+    def run_frames(loop, n):
+        if use_dist:
+            dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            loop.step()
+        loop.flush()
+        sync()
+        t1 = time.perf_counter()
+        if use_dist:
+            dist.barrier()
+        return max_over_ranks(t1 - t0, use_dist, device)
+    ex = FrameExchange(sc, rank, world, device=device, render_block=render_block_k, graph=graph)
+    for _ in range(warmup):
+        ex.step()
+    ex.flush()
+    sync()
+    stream_s = run_frames(ex, steps)
+    pipe = FramePipeline(sc, rank, world, device=device, render_block=render_block)
+    for _ in range(warmup):
+        pipe.step()
+    pipe.flush()
+    rank0_s = run_frames(pipe, steps)
+    nrows = [len(r) for r in ex.rows_all]
+
+    def rate(s):
+        return round(W * H * spp * steps / s / 1e6, 3)
+    out = {
+        "frame_s": frame_s,
+        "frame_ms": round(frame_s * 1e3 / steps, 5),
+        "rows_per_rank": [min(nrows), max(nrows)],
+        "partition": "interleaved 8-row groups r, r+N, ... (rtx_render_groups_rgb8), reordered by rank 0",
+        "collective": "one torch.distributed.gather (RCCL) of the ranks' uint8 rows to rank 0 per frame, awaited",
+        "throughput": {
+            "frame_ms": round(stream_s * 1e3 / steps, 5), "Mrays_s": rate(stream_s),
+            "launch": ("one batched launch per group of N frames (rtx_render_groups_frames)" if ex.render_frames
+                       else "one HIP graph of the group's N renders per group" if ex.graph else "eager"),
+            "note": "frame-stream throughput of one static scene state (rtx.distributed.FrameExchange): frame k "
+                    "sharded over the N ranks and gathered to rank k mod N; a group of N frames rendered in ONE "
+                    "batched launch per rank and exchanged by one all_to_all, overlapped with the next group"},
+        "gather_to_rank0": {
+            "frame_ms": round(rank0_s * 1e3 / steps, 5), "Mrays_s": rate(rank0_s),
+            "note": "FramePipeline: every frame gathered to rank 0, double-buffered (its ingress bounds the rate)"},
+        "headline": "value = ONE frame sharded over the N ranks (uint8 rows, fused) and gathered to rank 0, "
+                    "frame by frame, awaited: no batching or overlap across frames",
+    }
+    return out, last[0]
+
+
+def roofline(bytes_alg, kern_ms, rows_frac, pmc_path):
+    """The dominant kernel's roofline. The bound is VALU issue: the megakernel keeps its rays
+    in registers and moves little more than its framebuffer, so the counters show issue,
+    not HBM, as the limiter. achieved = SQ_INSTS_VALU per launch
+    (rocprofv3 PMC pass of the same kernel, committed under profiles/) / the kernel's
+    average duration; peak = 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction
+    (MI355X_MICROARCH.md). Every instruction is priced at that 2-cycle rate, so frac <= 1
+    (fp64, transcendental and VOP3 forms take longer). Beside it: the measured HBM bytes
+    (2 x FETCH_SIZE + WRITE_SIZE) against 8 TB/s (frac_hbm), and SURVEY.md 8(d)'s
+    algorithmic byte model (model_frac: SoA ray records this kernel never stores)."""
+    secs = kern_ms * 1e-3
+    traffic, src = pmc_traffic(pmc_path)
+    valu = pmc_valu(pmc_path) if src else None
+    if src:
+        src = os.path.relpath(src, REPO)
+    roof = {"bound": "valu", "achieved": None, "peak": VALU_PEAK_GINST_S, "unit": "G wave64 VALU instructions/s",
+            "frac": None, "traffic": None,
+            "traffic_unit": "HBM bytes/launch (rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE)", "source": src,
+            "model_bytes_per_launch": int(bytes_alg),
+            "model_frac": round(bytes_alg / secs / 1e9 / HBM_PEAK_GBS, 5),
+            "model": "SURVEY.md 8(d): 32 B x ray segments + 12 B x pixels per frame, priced at 8 TB/s: the SoA "
+                     "ray records of a wavefront design, which this megakernel keeps in registers (not a bound)"}
+    if valu:
+        v = valu * rows_frac
+        ach = v / secs / 1e9
+        roof.update(achieved=round(ach, 2), frac=round(ach / VALU_PEAK_GINST_S, 5), valu_insts_per_launch=int(v),
+                    issue_floor_us=round(v / VALU_PEAK_GINST_S / 1e3, 3))
+    else:
+        roof["note"] = "no PMC summary for this config: the VALU fraction is unmeasured"
+    if traffic is not None:
+        traffic = int(round(traffic * rows_frac))
+        roof.update(traffic=traffic, achieved_hbm_GBs=round(traffic / secs / 1e9, 2),
+                    frac_hbm=round(traffic / secs / 1e9 / HBM_PEAK_GBS, 5))
+    return roof
 
 
 def main():
@@ -311,7 +441,6 @@ def main():
     if use_dist:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import rtx  # noqa: F401
-    from rtx.distributed import FrameExchange, FramePipeline
 
     # setup cost, outside the timed region (the reference re-parses and re-renders per
     # main.py run, provided/main.py:25-34): host parse, rtx_scene_create (records, mesh
@@ -374,109 +503,36 @@ def main():
         scaling, parallelism = "strong", "single GPU"
     else:
         # N > 1 (north star): one step = ONE frame sharded across the ranks (uint8 rows
-        # rendered by every rank) and gathered to its owner, rank k mod N; the gathers of N
-        # consecutive frames are one RCCL all_to_all overlapping the next N renders.
-        ex = FrameExchange(sc, rank, world, graph=not a.no_graph)
+        # rendered by every rank) and gathered to rank 0, awaited, frame by frame
+        dev = torch.device("cuda", local)
+        from rtx.distributed import rank_rows
+        my_rows = rank_rows(H, world, rank, True)
+        warm_out = torch.empty((max(len(my_rows), 1), W, 3), dtype=torch.uint8, device="cuda")
 
-        def run_frames(loop, n):
-            if use_dist:
-                dist.barrier()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(n):
-                loop.step()
-            loop.flush()
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            if use_dist:
-                dist.barrier()
-            return max_over_ranks(t1 - t0, use_dist)
-        # clock warm-up on this rank's own rows (no collective, so the ranks need not agree
-        # on a count), then the W warm-up steps of the frame loop
-        warm_out = torch.empty((max(ex.nrows, 1), W, 3), dtype=torch.uint8, device="cuda")
-
-        def own_rows():
-            if not ex.nrows:
-                return
-            if ex.interleave:
+        def own_rows():  # clock warm-up on this rank's own rows (no collective)
+            if len(my_rows):
                 sc.render_device(groups=(rank, world), out=warm_out, stream=stream)
-            else:
-                sc.render_device(row0=int(ex.rows[0]), nrows=len(ex.rows), out=warm_out, stream=stream)
         warm = clock_warmup(own_rows, a.clock_warmup_s, torch.cuda.synchronize)
-        for _ in range(a.warmup):
-            ex.step()
-        ex.flush()
-        torch.cuda.synchronize()
-        wall_s = run_frames(ex, a.steps)
-        # the same frames with every gather to rank 0 (FramePipeline), for comparison
-        pipe = FramePipeline(sc, rank, world)
-        for _ in range(a.warmup):
-            pipe.step()
-        pipe.flush()
-        rank0_s = run_frames(pipe, a.steps)
-        # one frame at a time (no batching across frames, no overlap): this rank's rows of
-        # the frame, uint8 (fused), then the gather to rank 0, awaited -- the latency of one
-        # sharded frame
-        from rtx.distributed import FrameGather
-        single = FrameGather(H, W, 3, world, rank, torch.uint8, torch.device("cuda", local), interleave=True, dst=0)
+        mg, _ = measure_sharded(sc, rank, world, a.steps, a.warmup, use_dist, dev, stream=stream,
+                                graph=not a.no_graph)
+        wall_s = mg.pop("frame_s")
+        # breakdown (outside the timed region): this rank's render alone, fp32 (the kernel
+        # the roofline below prices) and uint8 (the one the frame loop runs), from HIP events
+        rank_fb = torch.empty((max(len(my_rows), 1), W, 3), dtype=torch.float32, device="cuda")
 
-        def one_frame():
-            if single.nrows:
-                sc.render_device(groups=(rank, world), out=single.block, stream=stream)
-            w = single.start(async_op=True)
-            if w is not None:
-                w.wait()
-            if rank == 0:
-                single.frame()
-        for _ in range(a.warmup):
-            one_frame()
-        single_s = timed(one_frame, a.steps, use_dist)
-        # breakdown (outside the timed region): this rank's render + uint8 conversion, and
-        # one group exchange alone, each from HIP events on the launch stream
-        rank_fb = torch.empty((ex.nrows, W, 3), dtype=torch.float32, device="cuda")
-
-        def fp32_rows():  # this rank's rows into fp32: the kernel the roofline below prices
-            if ex.interleave:
-                sc.render_device(groups=(rank, world), out=rank_fb, stream=stream)
-            else:
-                sc.render_device(row0=int(ex.rows[0]), nrows=len(ex.rows), out=rank_fb, stream=stream)
+        def fp32_rows():
+            if len(my_rows):
+                sc.render_device(groups=(rank, world), out=rank_fb[:len(my_rows)], stream=stream)
         fp32_rows()  # (its first call may compile the fp32 variant of the specialized kernel)
         torch.cuda.synchronize()
         kern_ms = max_over_ranks(kernel_ms(fp32_rows, a.steps, stream), use_dist)
         kernel = sc.last_kernel
-        render_ms = max_over_ranks(kernel_ms(ex.render, a.steps, stream), use_dist)
-        kernel_rgb8 = sc.last_kernel
-        if use_dist:
-            dist.barrier()
-
-        exchange_ms = max_over_ranks(kernel_ms(ex.exchange_once, a.steps, stream), use_dist)
-        rows_frac = ex.nrows / H
-        nrows = [len(r) for r in ex.rows_all]
-        extra["multi_gpu"] = {
-            "frame_ms": round(wall_s * 1e3 / a.steps, 5),
-            "render_ms_per_rank": round(kern_ms, 5), "render_rgb8_ms_per_rank": round(render_ms, 5),
-            "kernel_rgb8": kernel_rgb8,
-            "exchange_ms_per_group": round(exchange_ms, 5), "frames_per_group": world,
-            "rows_per_rank": [min(nrows), max(nrows)],
-            "partition": ("interleaved 8-row groups r, r+N, ... (rtx_render_groups_rgb8), reordered by the owner"
-                          if ex.interleave else "np.array_split row blocks (rtx_render_rgb8), received in image order"),
-            "collective": "frame k gathered to rank k mod N; the gathers of N consecutive frames are one "
-                          "torch.distributed.all_to_all_single (RCCL), double-buffered",
-            "launch": ("one batched launch per group of N frames (rtx_render_groups_frames)" if ex.render_frames
-                       else "eager" if a.no_graph else "one HIP graph of the group's N renders per group"),
-            "gather_to_rank0": {"frame_ms": round(rank0_s * 1e3 / a.steps, 5),
-                                "Mrays_s": round(W * H * spp * a.steps / rank0_s / 1e6, 3),
-                                "note": "FramePipeline: every frame gathered to rank 0 (its ingress bounds the rate)"},
-            "single_frame": {"frame_ms": round(single_s * 1e3 / a.steps, 5),
-                             "Mrays_s": round(W * H * spp * a.steps / single_s / 1e6, 3),
-                             "note": "latency of ONE sharded frame: each rank renders its interleaved rows (uint8, "
-                                     "fused) and the frame is gathered to rank 0, awaited, frame by frame (no "
-                                     "batching across frames, no overlap)"},
-            "headline": "frame-stream throughput of one static scene state: frame k sharded over the N ranks and "
-                        "gathered to rank k mod N; a group of N frames is rendered in ONE batched launch per rank "
-                        "and exchanged by one all_to_all, overlapped with the next group (see single_frame for "
-                        "one frame's latency)",
-        }
+        render_ms = max_over_ranks(kernel_ms(own_rows, a.steps, stream), use_dist)
+        mg["render_ms_per_rank"] = round(kern_ms, 5)
+        mg["render_rgb8_ms_per_rank"] = round(render_ms, 5)
+        mg["kernel_rgb8"] = sc.last_kernel
+        rows_frac = len(my_rows) / H
+        extra["multi_gpu"] = mg
         # secondary: weak scaling (each rank renders its own whole frame per step)
         for _ in range(3):
             full_frame()
@@ -484,34 +540,13 @@ def main():
         extra["weak_scaling"] = {"Mrays_s": round(world * W * H * spp * a.steps / weak_s / 1e6, 3),
                                  "ms_per_step": round(weak_s * 1e3 / a.steps, 5),
                                  "note": "frame-parallel: each rank renders its own whole frame, no collective"}
-        scaling, parallelism = "strong", "rows x %d ranks + RCCL gather to each frame's owner" % world
+        scaling, parallelism = "strong", "rows x %d ranks + one RCCL gather to rank 0 per frame" % world
     ms_per_step = wall_s * 1e3 / a.steps
     value = W * H * spp * a.steps / wall_s / 1e6
 
     if rank == 0:
-        bytes_kernel = b_alg * rows_frac  # the dominant kernel's share of the frame
-        achieved = bytes_kernel / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic(a.pmc_json or os.path.join(REPO, "profiles", "pmc_%s.json" % a.config))
-        if traffic is not None:
-            traffic = int(round(traffic * rows_frac))
-            traffic_src = os.path.relpath(traffic_src, REPO)
-        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                "traffic_unit": "HBM bytes/launch (rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE)",
-                "traffic_source": traffic_src,
-                "model": "achieved = B_alg / kernel time, B_alg = 32 B x ray segments + 12 B x pixels "
-                         "(SURVEY.md 8d): algorithmic ray traffic, which this megakernel keeps in registers",
-                "bytes_alg_per_launch": int(bytes_kernel)}
-        if achieved > HBM_PEAK_GBS:
-            # the byte model prices an SoA wavefront design (every segment's ray record through
-            # HBM); a frame faster than that model's HBM time shows the megakernel beats it
-            roof["note"] = ("frac > 1: the frame takes less time than HBM would need to move the SoA ray "
-                            "records of the byte model; those bytes stay in registers (traffic is what moved)")
-        if traffic is not None:
-            meas = traffic / (kern_ms * 1e-3) / 1e9
-            roof["achieved_measured"] = round(meas, 2)
-            roof["frac_measured"] = round(meas / HBM_PEAK_GBS, 5)
-        valu = pmc_valu(os.path.join(REPO, traffic_src)) if traffic_src else None
+        roof = roofline(b_alg * rows_frac, kern_ms, rows_frac,
+                        a.pmc_json or os.path.join(REPO, "profiles", "pmc_%s.json" % a.config))
         out = {
             "metric": METRIC if a.config == "tsp1080" else METRIC_OTHER % CONFIGS[a.config][3],
             "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
@@ -526,16 +561,6 @@ def main():
             "segments_per_frame": segments, "cast_rays_per_frame": cast_rays, "shadow_rays_per_frame": shadow_rays,
             "roofline": roof,
         }
-        if valu:
-            v = valu * rows_frac
-            ach = v / (kern_ms * 1e-3) / 1e9
-            # the limiter actually identified: VALU issue + per-wave latency. frac prices
-            # every instruction at the 2-cycle wave64 fp32 rate (fp64, transcendental and
-            # VOP3 forms take longer, so 1.0 is not reachable)
-            out["valu"] = {"insts_per_launch": int(v), "achieved": round(ach, 1), "peak": VALU_PEAK_GINST_S,
-                           "unit": "G wave64-instructions/s", "frac": round(ach / VALU_PEAK_GINST_S, 4),
-                           "issue_floor_us": round(v / VALU_PEAK_GINST_S / 1e3, 3), "source": traffic_src}
-            roof["limiter"] = "VALU issue + per-wave latency (see valu); measured HBM traffic is frac_measured"
         out["setup_ms"] = setup
         out.update(extra)
         out.update(cpu)

@@ -1311,6 +1311,9 @@ hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& k
     // kernel name: rtx_jit_render_<mesh><sec><ext><count><jitter> (tells profiles apart)
     std::string name = "rtx_jit_render_";
     for (bool f : {mesh, sec, ext, cnt, jit}) name += f ? '1' : '0';
+    // the parity-mode jitter (replayed noise table) is a different specialization from the
+    // production Philox one: the name says which ran
+    if (jit && kp.jitter == RTX_JITTER_REPLAY) name += "_replay";
     if (spp) name += "_spp";
     if (out8) name += "_rgb8";
     // one-sample flat-scene kernels: the scene records as literals (jit_baked_records).

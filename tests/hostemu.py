@@ -112,6 +112,27 @@ def occluded_light(scene, o, light, grids):
     return occ.astype(bool), cells
 
 
+def philox(ctr, key):
+    """The device's Philox4x32-10 of one counter (4 uint32) and key (k0, k1)."""
+    c = np.ascontiguousarray(np.asarray(ctr, np.uint32))
+    f = lib().rtx_hostemu_philox
+    f.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+    f.restype = None
+    f(c.ctypes.data, int(key[0]), int(key[1]))
+    return c
+
+
+def jitter(seed, col0, ncols, height, n_dof, n_aa):
+    """The device's production jitter uniforms (jitter_block / jitter_rnd) in the replay
+    table's layout, float32 flat."""
+    out = np.zeros(ncols * height * n_dof * n_aa * 3, np.float32)
+    f = lib().rtx_hostemu_jitter
+    f.argtypes = [C.c_uint64, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]
+    f.restype = None
+    f(seed, col0, ncols, height, n_dof, n_aa, out.ctypes.data)
+    return out
+
+
 def jit_baked(scene):
     """The scene-record prelude librtx.so hands its scene-specialized kernels
     (rtx_api.hip jit_baked_records), as a string."""

@@ -325,6 +325,29 @@ extern "C" int rtx_hostemu_lgrid_stats(const rtx_scene_desc* sd, int64_t* out) {
     return RTX_OK;
 }
 
+// The device's Philox4x32-10 (rtx_trace.h philox4x32) on one counter and key: ctr is
+// overwritten with the output block.
+extern "C" void rtx_hostemu_philox(uint32_t* ctr, uint32_t k0, uint32_t k1) { philox4x32(ctr, k0, k1); }
+
+// The production jitter uniforms (rtx_kernels.h jitter_block / jitter_rnd) of the strip
+// col0 .. col0 + ncols - 1, in the replay table's layout [column][reference row][dof][aa][3].
+extern "C" void rtx_hostemu_jitter(uint64_t seed, int32_t col0, int32_t ncols, int32_t height, int32_t n_dof,
+                                   int32_t n_aa, float* out) {
+    KParams k{};
+    k.col0 = col0;
+    k.seed_lo = (uint32_t)seed;
+    k.seed_hi = (uint32_t)(seed >> 32);
+    int64_t i = 0;
+    for (int32_t cc = 0; cc < ncols; ++cc)
+        for (int32_t j = 0; j < height; ++j)
+            for (int32_t s = 0; s < n_dof * n_aa; ++s, ++i) {
+                uint32_t w[4];
+                jitter_block(k, cc, j, s >> 1, w);
+                const f3 r = jitter_rnd(w, s & 1);
+                out[3 * i] = r.x; out[3 * i + 1] = r.y; out[3 * i + 2] = r.z;
+            }
+}
+
 extern "C" const char* rtx_hostemu_last_error(void) { return g_last_error.c_str(); }
 
 extern "C" int64_t rtx_hostemu_sizeof(int which) {

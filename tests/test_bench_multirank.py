@@ -1,0 +1,100 @@
+"""bench.py's N > 1 measurement (measure_sharded: one sharded frame per step, gathered to
+rank 0 and awaited; the FrameExchange and FramePipeline streams beside it) run end to
+end on world-size-2 and -3 gloo groups, with the tests-only host build of the device
+source standing in for each rank's GPU: barriers, max-over-ranks timing and the three
+frame loops in the order the bench runs them, and the delivered frame checked against the
+oracle's PNG bytes."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, res, steps, out_q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), "python-raytracer_amd"), here):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    import hostemu
+    from common import product_scene
+    from rtx.distributed import rank_rows, to_rgb8
+    sc = product_scene("MirrorRefraction", res)
+    cache = {}
+    calls = [0]
+
+    def rows_u8(rows):
+        key = tuple(int(r) for r in rows)
+        if key not in cache:
+            cache[key] = to_rgb8(torch.from_numpy(hostemu.render_rows(sc, np.asarray(rows), threads=2)))
+        calls[0] += 1
+        return cache[key]
+
+    mine = rank_rows(res[1], world, rank, True)
+
+    def render_rows(out):  # the value loop: this rank's interleaved groups
+        out.copy_(rows_u8(mine))
+
+    def render_block(out, rows):  # FramePipeline
+        out.copy_(rows_u8(rows))
+
+    def render_block_k(out, rows, k):  # FrameExchange
+        out.copy_(rows_u8(rows))
+    mg, frame = bench.measure_sharded(sc, rank, world, steps, 2, True, torch.device("cpu"), sync=lambda: None,
+                                      render_rows=render_rows, render_block=render_block,
+                                      render_block_k=render_block_k, graph=False)
+    out_q.put((rank, mg, None if frame is None else frame.clone().numpy(), calls[0]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,res", [(2, (40, 23)), (3, (33, 26))])
+def test_bench_sharded_frame_loop(world, res):
+    from common import oracle_render
+    from oracle import oracle as O
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    steps = 4
+    procs = [ctx.Process(target=_worker, args=(r, world, port, res, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((r, (mg, f, n)) for r, mg, f, n in (q.get(timeout=240) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = O.to_png_array(oracle_render("MirrorRefraction", res))
+    mg0, frame0, _ = got[0]
+    assert np.array_equal(frame0, want)  # the value loop's last frame, on rank 0
+    for r in range(1, world):
+        assert got[r][1] is None
+        # every rank reports the same max-over-ranks times
+        assert got[r][0]["frame_s"] == mg0["frame_s"]
+        assert got[r][0]["throughput"]["frame_ms"] == mg0["throughput"]["frame_ms"]
+    assert mg0["frame_s"] > 0 and mg0["frame_ms"] == round(mg0["frame_s"] * 1e3 / steps, 5)
+    W, H = res
+    assert mg0["throughput"]["Mrays_s"] > 0 and mg0["gather_to_rank0"]["Mrays_s"] > 0
+    assert mg0["rows_per_rank"] == [min(len(r) for r in _parts(H, world)), max(len(r) for r in _parts(H, world))]
+
+
+def _parts(H, world):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "python-raytracer_amd"))
+    from rtx.scene import group_rows
+    return [group_rows(H, world, r) for r in range(world)]

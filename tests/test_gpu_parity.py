@@ -63,8 +63,48 @@ def test_jitter_replay_matches_oracle():
     assert_parity(sc.render(), ref, "DOF replay")
 
 
+def _philox_noise(sc, col0, ncols):
+    from oracle import philox as PH
+    return PH.jitter_noise(sc.seed, col0, ncols, sc.vc.height, sc.vc.dof_samples, sc.samples)
+
+
+def test_philox_config5_kernel_bit_exact():
+    """BASELINE config 5 as the bench times it: DepthOfField 3840x2160, AA 2 x DOF 32,
+    production (Philox) jitter, the whole frame in one launch of the scene-specialized
+    kernel rtx_jit_render_00001 (the replay-mode variant is named *_replay). Columns of
+    that framebuffer against the oracle fed with the restated Philox stream
+    (oracle/philox.py): bit-identical, 138,240 samples per column."""
+    edits = {"AA": {"jitter": True, "samples": 2}}
+    res = (3840, 2160)
+    sc = product_scene("DepthOfField", res, **edits)
+    assert sc.jitter_noise is None
+    fb = sc.render_device()  # [H][W][3] fp32, row 0 = top
+    torch.cuda.synchronize()
+    assert sc.last_kernel == "rtx_jit_render_00001", sc.last_kernel
+    for col in (3000, 0, 1921, 3839):
+        got = fb[:, col, :].flip(0).double().cpu().numpy()[None]  # (1, H, 3), reference row order
+        ref = oracle_render("DepthOfField", res, subimage=col, tasks=3840, noise=_philox_noise(sc, col, 1), **edits)
+        assert_parity(got, ref, "DOF 4K Philox column %d" % col)
+
+
+@pytest.mark.parametrize("res,subimage,tasks", [((64, 48), 0, 1), ((64, 48), 5, 8), ((3840, 2160), 3000, 3840)])
+def test_philox_frames_bit_exact(res, subimage, tasks):
+    """Philox-mode DepthOfField frames and strips (a 64x48 frame, a strip starting at
+    column 40, and config 5's column 3000 rendered as its own 1-column strip) against the
+    oracle with the restated stream."""
+    edits = {"AA": {"jitter": True, "samples": 2}}
+    sc = product_scene("DepthOfField", res, **edits)
+    img = sc.render(subimage, tasks)
+    assert sc.last_kernel == "rtx_jit_render_00001", sc.last_kernel
+    from rtx.scene import strip_columns
+    col0, ncols = strip_columns(res[0], subimage, tasks)
+    ref = oracle_render("DepthOfField", res, subimage=subimage, tasks=tasks, noise=_philox_noise(sc, col0, ncols), **edits)
+    assert_parity(img, ref, "DOF Philox %s strip %d/%d" % (res, subimage, tasks))
+
+
 def test_philox_jitter_is_deterministic_and_statistically_matches():
-    """Production jitter (Philox keyed by pixel and sample) vs the oracle with numpy noise."""
+    """Production jitter (Philox keyed by pixel and sample) vs the oracle with numpy's
+    stream (the reference's unseeded np.random): same distribution."""
     edits = {"AA": {"jitter": True, "samples": 1}}
     res = (128, 128)
     sc = product_scene("DepthOfField", res, **edits)

@@ -5,7 +5,7 @@
 #
 #   TAG=name STEPS="tests smoke bench configs ab pmc rocprof pipeline" bash tools/session.sh
 #
-# tests     python -m pytest tests -m gpu (TESTS="tests/x.py ..." narrows it)
+# tests     python -m pytest tests -m gpu (TESTS="tests/x.py ..." and KEXPR="a or b" narrow it)
 # smoke     __graft_entry__.smoke()
 # bench     the default bench line (N = 1, with CPU baselines unless CPU=0)
 # configs   bench.py --config C for C in CONFIGS (CPU=1 adds the CPU legs to each line)
@@ -32,8 +32,9 @@ cpu_flag() { [ "${CPU:-1}" = 1 ] && echo "--cpu-seconds ${CPU_SECONDS:-10}" || e
 for s in ${STEPS:-tests smoke bench rocprof}; do
   case $s in
     tests)
-      step pytest_gpu 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -q -p no:cacheprovider --timeout 120 \
-        --timeout-method thread
+      if [ -n "${KEXPR:-}" ]; then kx=(-k "$KEXPR"); else kx=(); fi
+      step pytest_gpu 900 python -u -m pytest ${TESTS:-tests} "${kx[@]}" -m gpu -x -q -p no:cacheprovider \
+        --timeout 120 --timeout-method thread
       rc=$?; [ $rc -eq 0 ] || [ "${KEEP_GOING:-0}" = 1 -a $rc -eq 1 ] || exit 1 ;;
     smoke)
       step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
