@@ -240,6 +240,12 @@ int rtx_fb_to_rgb8(const float* fb_dev, uint8_t* out_dev, int64_t n_values, void
  * render call on the scene or rtx_scene_destroy. */
 const char* rtx_last_kernel(const rtx_scene* scene);
 
+/* Observability (no reference counterpart): the number of scene-specialized kernel
+ * modules loaded in this process. Kernels whose source carries one scene's record values
+ * are unloaded once no scene holds them and more than $RTX_JIT_IDLE_BAKED (default 8)
+ * such idle modules exist, so the count stays bounded as scenes come and go. */
+int32_t rtx_jit_modules(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -16,8 +16,10 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <dirent.h>
 #include <fstream>
 #include <functional>
+#include <list>
 #include <map>
 #include <numeric>
 #include <mutex>
@@ -1112,9 +1114,60 @@ namespace {
 struct JitEntry {
     hipModule_t mod = nullptr;
     hipFunction_t fn = nullptr;
+    bool baked = false;  // the source carries one scene's record values (jit_baked_records)
+    int refs = 0;        // scenes whose resolved kernels hold it
 };
 std::mutex g_jit_mu;
 std::map<std::string, JitEntry> g_jit;
+// Kernels with baked records belong to one scene's values, so they are not kept for the
+// life of the process: once no scene holds one it joins an idle list, and beyond
+// kJitIdleBaked idle modules the oldest is unloaded (its scenes' buffers were freed with
+// hipFree, which waits for their kernels). The disk cache keeps at most kJitDiskBaked
+// baked code objects (rtx_b_*.co, oldest removed first).
+// ($RTX_JIT_IDLE_BAKED / $RTX_JIT_DISK_BAKED override the caps; the tests lower them.)
+size_t jit_cap(const char* env, size_t dflt) {
+    const char* e = getenv(env);
+    return (e && *e) ? (size_t)std::max(0, atoi(e)) : dflt;
+}
+constexpr size_t kJitIdleBaked = 8;
+constexpr size_t kJitDiskBaked = 64;
+std::list<std::string> g_jit_idle;  // baked keys with refs == 0, oldest first
+
+// A scene drops its hold on a resolved kernel (camera change or rtx_scene_destroy).
+void jit_release(const std::string& key) {
+    if (key.empty()) return;
+    std::lock_guard<std::mutex> lock(g_jit_mu);
+    auto it = g_jit.find(key);
+    if (it == g_jit.end() || --it->second.refs > 0 || !it->second.baked) return;
+    g_jit_idle.push_back(key);
+    const size_t cap = jit_cap("RTX_JIT_IDLE_BAKED", kJitIdleBaked);
+    while (g_jit_idle.size() > cap) {
+        auto old = g_jit.find(g_jit_idle.front());
+        g_jit_idle.pop_front();
+        if (old == g_jit.end() || old->second.refs > 0) continue;
+        (void)hipModuleUnload(old->second.mod);
+        g_jit.erase(old);
+    }
+}
+
+// Keeps the newest kJitDiskBaked baked code objects of the disk cache.
+void jit_prune_disk(const std::string& dir) {
+    DIR* d = opendir(dir.c_str());
+    if (!d) return;
+    std::vector<std::pair<time_t, std::string>> files;
+    while (dirent* e = readdir(d)) {
+        const std::string n = e->d_name;
+        if (n.rfind("rtx_b_", 0) != 0 || n.size() < 3 || n.compare(n.size() - 3, 3, ".co") != 0) continue;
+        struct stat st;
+        const std::string path = dir + "/" + n;
+        if (lstat(path.c_str(), &st) == 0 && S_ISREG(st.st_mode)) files.emplace_back(st.st_mtime, path);
+    }
+    closedir(d);
+    const size_t cap = jit_cap("RTX_JIT_DISK_BAKED", kJitDiskBaked);
+    if (files.size() <= cap) return;
+    std::sort(files.begin(), files.end());
+    for (size_t i = 0; i + cap < files.size(); ++i) (void)unlink(files[i].second.c_str());
+}
 
 // Sample-parallel mapping (render_body_spp) for the hierarchy/texture kernels when a
 // pixel has >= RTX_SPP_MIN samples (default 16): a wave then traces one pixel's nearly
@@ -1231,7 +1284,8 @@ bool jit_bake_enabled() {
 
 hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& kp, int fc_mode, bool any_speed,
                                 uint32_t ldir, int uniform_hard, bool mesh, bool sec, bool ext, bool cnt, bool jit,
-                                bool spp, bool out8, const std::string& baked, std::string* name_out) {
+                                bool spp, bool out8, const std::string& baked, std::string* name_out,
+                                std::string* key_out) {
     if (!jit_enabled()) return nullptr;
     if (v.n_plane + v.n_sphere + v.n_box + v.n_mesh > 32 || v.n_lights > 8) return nullptr;  // code size
     // CSG/texture kernels: the unrolled loops raise their (already high) register
@@ -1333,12 +1387,18 @@ hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& k
     const std::string dkey = key + "\n#device " + std::to_string(device);
     std::lock_guard<std::mutex> lock(g_jit_mu);
     auto it = g_jit.find(dkey);
-    if (it != g_jit.end()) return it->second.fn;
+    if (it != g_jit.end()) {
+        if (it->second.refs++ == 0 && it->second.baked) g_jit_idle.remove(dkey);
+        *key_out = dkey;
+        return it->second.fn;
+    }
     std::string all = key;
     for (int h = 0; h < kJitNumHeaders; ++h) all += kJitHeaderSrcs[h];
     char hash[32];
     snprintf(hash, sizeof(hash), "%016zx", std::hash<std::string>{}(all));
-    const std::string dir = jit_cache_dir(), path = dir.empty() ? "" : dir + "/rtx_" + hash + ".co";
+    const bool is_baked = !prelude.empty();
+    const std::string dir = jit_cache_dir();
+    const std::string path = dir.empty() ? "" : dir + (is_baked ? "/rtx_b_" : "/rtx_") + hash + ".co";
     std::string code;
     if (!path.empty()) {
         std::ifstream f(path, std::ios::binary);
@@ -1378,6 +1438,7 @@ hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& k
             if (f.write(code.data(), (std::streamsize)code.size())) {
                 f.close();
                 (void)rename(tmp.c_str(), path.c_str());
+                if (is_baked) jit_prune_disk(dir);
             }
         }
     }
@@ -1389,7 +1450,10 @@ hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& k
                 name.c_str(), hipGetErrorString(he));
         return nullptr;
     }
+    e.baked = is_baked;
+    e.refs = 1;
     g_jit[dkey] = e;
+    *key_out = dkey;
     return e.fn;
 }
 
@@ -1450,6 +1514,7 @@ struct rtx_scene {
         bool done = false;
         hipFunction_t fn = nullptr;
         std::string name;
+        std::string key;  // its g_jit entry (released by free_camera)
     } resolved[16];
     std::string last_kernel;  // name of the kernel the last render call launched
     std::string jit_baked;    // the scene records as constant arrays (jit_baked_records)
@@ -1482,7 +1547,10 @@ void free_camera(rtx_scene* s) {
     s->d_xs = s->d_ys = s->d_dof = s->d_aa = s->d_times = s->d_noise = nullptr;
     s->d_kp = nullptr;
     s->cam_set = false;
-    for (auto& r : s->resolved) r = rtx_scene::Resolved{};  // specialized on the camera's sample counts
+    for (auto& r : s->resolved) {  // specialized on the camera's sample counts
+        jit_release(r.key);
+        r = rtx_scene::Resolved{};
+    }
 }
 
 void free_scene(rtx_scene* s) {
@@ -1503,6 +1571,11 @@ int rtx_abi_version(void) { return RTX_ABI_VERSION; }
 const char* rtx_last_error(void) { return g_last_error.c_str(); }
 
 const char* rtx_last_kernel(const rtx_scene* s) { return s ? s->last_kernel.c_str() : ""; }
+
+int32_t rtx_jit_modules(void) {
+    std::lock_guard<std::mutex> lock(g_jit_mu);
+    return (int32_t)g_jit.size();
+}
 
 int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
     if (!out) return fail(RTX_ERR_INVALID, "rtx_scene_create: null argument");
@@ -1808,7 +1881,7 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
     if (!rs.done) {
         rs.fn = jit_render_kernel(s->device, s->view, s->kp, s->fc_mode, s->any_speed, s->light_dir_mask,
                                   s->uniform_hard, s->has_mesh, s->has_secondary, s->has_ext, cnt, jit, spp_mode,
-                                  out8, s->jit_baked, &rs.name);
+                                  out8, s->jit_baked, &rs.name, &rs.key);
         rs.done = true;
     }
     if (rs.fn && jit_enabled()) {

@@ -2055,12 +2055,37 @@ RTX_HD Surface resolve_hit(const SceneView& S, const Hit& h, const HHit& hh, f3 
 // scenes never use.
 __host__ __device__ __attribute__((noinline)) inline double pow_general(double x, double y) { return pow(x, y); }
 
-// `x ** hardness` (CPython float_pow -> pow) in fp64. Integer exponents use binary
-// exponentiation; the fp32 cast that follows makes it equal to libm pow except when the
-// exact value lies within a few fp64 ulps of an fp32 rounding boundary. The loop runs a
-// scene-uniform number of steps (bits of the largest integer hardness) with selects, so
-// lanes shading different materials do not diverge; each lane performs exactly the
-// multiplications of `while (n) { if (n & 1) r *= b; b *= b; n >>= 1; }`.
+// x ** n for an integer n >= 0 in double-double arithmetic (Dekker products through fma,
+// relative error below 2^-98 for n < 2^16), rounded once to fp64: fl64 of the exact power,
+// which is what a correctly rounded libm pow returns. The rare path of spec_pow.
+RTX_HD void dd_mul(double& ah, double& al, double bh, double bl) {
+    const double p = ah * bh;
+    double e = __builtin_fma(ah, bh, -p);  // exact: ah * bh = p + e
+    e = e + (ah * bl + al * bh);
+    const double s = p + e;
+    al = e - (s - p);
+    ah = s;
+}
+__host__ __device__ __attribute__((noinline)) inline double pow_int_dd(double x, int n) {
+    double rh = 1.0, rl = 0.0, bh = x, bl = 0.0;
+    while (n) {
+        if (n & 1) dd_mul(rh, rl, bh, bl);
+        n >>= 1;
+        if (n) dd_mul(bh, bl, bh, bl);
+    }
+    return rh + rl;
+}
+
+// `x ** hardness` (CPython float_pow -> libm pow) in fp64, cast to fp32 by the caller.
+// Integer exponents use binary exponentiation: at most 2 * pow_bits roundings, so the
+// result is within 2^-48 (relative; hardness <= 4096, so pow_bits <= 13) of the exact power. Its fp32 cast
+// therefore equals that of libm's correctly rounded pow unless the exact value lies that
+// close to an fp32 rounding boundary: r * (1 -/+ 2^-47) then round to different floats,
+// and only those lanes (about 2^-22 of the evaluations; tests/test_pow.py finds 2 of
+// 1.29e8 that the fast value would get wrong) recompute the power in double-double. The
+// loop runs a scene-uniform number of steps (bits of the largest integer hardness) with
+// selects, so lanes shading different materials do not diverge; each lane performs
+// exactly the multiplications of `while (n) { if (n & 1) r *= b; b *= b; n >>= 1; }`.
 RTX_HD double spec_pow(double x, const DMat& m, int pow_bits) {
     if (RTX_ABLATE == 5) return (double)__builtin_powf((float)x, (float)m.hardness);  // cost probe only
 #ifdef RTX_FIXED_HARD  // scene-specialized: every specular lobe has this integer hardness
@@ -2078,6 +2103,12 @@ RTX_HD double spec_pow(double x, const DMat& m, int pow_bits) {
             const double rb = r * b;
             r = ((n >> k) & 1) ? rb : r;
             b = b * b;
+        }
+        // fp32 rounding boundary within the error bound: the double-double power decides
+        const bool near = (float)(r * (1.0 - 0x1p-47)) != (float)(r * (1.0 + 0x1p-47));
+        if (RTX_ANY(near)) {
+            unspeculated();
+            if (near) r = pow_int_dd(x, n);
         }
         return r;
     }

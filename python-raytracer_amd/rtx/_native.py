@@ -88,7 +88,7 @@ _lib = None
 EXPORTS = ["rtx_abi_version", "rtx_last_error", "rtx_scene_create", "rtx_scene_destroy", "rtx_camera_set",
            "rtx_render", "rtx_render_groups", "rtx_group_rows", "rtx_intersect", "rtx_occluded", "rtx_fb_to_rgb8",
            "rtx_render_rgb8", "rtx_render_groups_rgb8", "rtx_last_kernel", "rtx_render_frames",
-           "rtx_render_groups_frames"]
+           "rtx_render_groups_frames", "rtx_jit_modules"]
 
 
 def load():
@@ -120,10 +120,12 @@ def load():
         lib.rtx_occluded.argtypes = [vp, C.c_int64, vp, vp, vp, C.c_double, vp, vp]
         lib.rtx_fb_to_rgb8.argtypes = [vp, vp, C.c_int64, vp]
         for fn in EXPORTS:  # every status-returning entry point (not the string / count ones)
-            if fn not in ("rtx_abi_version", "rtx_last_error", "rtx_last_kernel", "rtx_group_rows"):
+            if fn not in ("rtx_abi_version", "rtx_last_error", "rtx_last_kernel", "rtx_group_rows", "rtx_jit_modules"):
                 getattr(lib, fn).restype = C.c_int
         lib.rtx_last_kernel.argtypes = [vp]
         lib.rtx_last_kernel.restype = C.c_char_p
+        lib.rtx_jit_modules.argtypes = []
+        lib.rtx_jit_modules.restype = C.c_int32
         v = lib.rtx_abi_version()
         if v != ABI_VERSION:
             raise RuntimeError("librtx.so ABI %d != binding ABI %d" % (v, ABI_VERSION))

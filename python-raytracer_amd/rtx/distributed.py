@@ -327,9 +327,15 @@ class FrameExchange:
             self.render_block(self.slot(buf, j), self.rows, first + j)
 
     def _state(self):
-        """What a captured graph bakes in: the scene's device handle and camera upload."""
+        """What a captured graph bakes in: the scene's device handle and camera upload,
+        named by the scene's upload generation (rtx.Scene counts every native re-create and
+        camera upload from a process-wide counter, so a freed and re-allocated handle or
+        table never matches a recorded state)."""
         sc = self.scene
-        nat = getattr(sc, "_native", None)
+        gen = getattr(sc, "_gen", None)
+        if gen is not None:
+            return gen
+        nat = getattr(sc, "_native", None)  # scenes of other types: identities
         return (id(nat), getattr(nat, "h", None) and nat.h.value, id(getattr(sc, "_cam_info", None)))
 
     def capture(self, buf):

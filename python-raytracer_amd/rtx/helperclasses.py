@@ -5,6 +5,7 @@ written against the reference's objects keeps working. Vectors are numpy float32
 (PyGLM vec3 semantics); scalars are Python floats.
 """
 import math
+import weakref
 
 import numpy as np
 
@@ -100,14 +101,46 @@ for _m in ("__setitem__", "__delitem__", "__iadd__", "__imul__", "append", "exte
     setattr(_Times, _m, _tracked(_m))
 
 
+class _Vec(np.ndarray):
+    """A ViewportCamera basis vector: a writable fp32 array, like PyGLM's mutable vec3,
+    that counts its camera's version up when it is written in place -- item assignment
+    (``vc.position[0] = 1``, also through a view) or a ufunc writing into it
+    (``vc.position += d``, ``np.add(a, b, out=vc.position)``). Arithmetic on it returns
+    plain arrays. Writes that bypass both (``np.copyto``, ``fill``, a ``.view(np.ndarray)``)
+    are not seen: call Scene.invalidate() after them."""
+
+    def __array_finalize__(self, obj):
+        self._owner = getattr(obj, "_owner", None)
+
+    def _touch(self):
+        o = self._owner() if self._owner is not None else None
+        if o is not None:
+            o._bump()
+
+    def __setitem__(self, key, value):
+        super().__setitem__(key, value)
+        self._touch()
+
+    def __array_ufunc__(self, ufunc, method, *inputs, out=None, **kwargs):
+        plain = [x.view(np.ndarray) if isinstance(x, _Vec) else x for x in inputs]
+        if out is None:
+            return getattr(ufunc, method)(*plain, **kwargs)
+        kwargs["out"] = tuple(o.view(np.ndarray) if isinstance(o, _Vec) else o for o in out)
+        getattr(ufunc, method)(*plain, **kwargs)
+        for o in out:
+            if isinstance(o, _Vec):
+                o._touch()
+        return out[0] if len(out) == 1 else out
+
+
 class ViewportCamera:
     """helperclasses.py:69-108: viewport, camera basis, lens and motion samples.
 
     Every attribute assignment counts ``_version`` up, so a Scene re-uploads its camera
-    tables only after a change (Scene._set_camera). The basis vectors are kept as
-    read-only fp32 copies (assign a new vector to move the camera) and motion_times as a
-    list that reports in-place edits; a vector of another type (e.g. a PyGLM vec3 set
-    by hand) makes the scene compare every camera value per render instead."""
+    tables only after a change (Scene._set_camera). The basis vectors are kept as fp32
+    ``_Vec`` copies and motion_times (any sequence assigned) as a list; both report
+    in-place edits. A vector of another type (e.g. a PyGLM vec3 set by hand) makes the
+    scene compare every camera value per render instead."""
 
     _VECS = ("position", "u", "v", "w")
 
@@ -148,12 +181,15 @@ class ViewportCamera:
     def __setattr__(self, name, value):
         if name in self._VECS:
             if isinstance(value, np.ndarray):
-                value = value.copy()
-                value.setflags(write=False)
+                value = np.array(value).view(_Vec)
+                value._owner = weakref.ref(self)
             else:
                 object.__setattr__(self, "_untracked", True)
-        elif name == "motion_times" and isinstance(value, list):
-            value = _Times(value, self)
+        elif name == "motion_times" and not (isinstance(value, _Times) and value._owner is self):
+            try:
+                value = _Times(list(value), self)
+            except TypeError:  # not a sequence: compared by value per render
+                object.__setattr__(self, "_untracked", True)
         object.__setattr__(self, name, value)
         self._bump()
 

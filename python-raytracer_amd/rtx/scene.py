@@ -10,6 +10,7 @@ motion times) and moves buffers.
 """
 import ctypes as C
 import hashlib
+import itertools
 
 import numpy as np
 import torch
@@ -67,6 +68,9 @@ def fb_to_rgb8(fb, out=None, stream=None):
     return out
 
 
+_GENERATION = itertools.count(1)
+
+
 class _NativeScene:
     """Owns an rtx_scene handle (device buffers live until destroy)."""
 
@@ -101,6 +105,7 @@ class Scene:
         self.jitter_noise = None      # optional replayed np.random.rand() stream (parity mode)
         self._native = None
         self._cam_key = None
+        self._gen = next(_GENERATION)  # upload generation: new on every re-create / camera upload
 
     @classmethod
     def from_reference(cls, ref):
@@ -117,6 +122,7 @@ class Scene:
         self._native = None
         self._cam_key = None
         self._noise_src = None
+        self._gen = next(_GENERATION)
 
     @property
     def last_kernel(self):
@@ -137,6 +143,7 @@ class Scene:
         if self._native is None or self._native.device != torch.cuda.current_device():
             self._native = _NativeScene(self.scene_desc())
             self._cam_key = None
+            self._gen = next(_GENERATION)
         return self._native
 
     # ------------------------------------------------------------------ camera tables
@@ -224,6 +231,7 @@ class Scene:
         N.call("rtx_camera_set", nat.h, C.byref(d))
         self._cam_key = key
         self._cam_info = t
+        self._gen = next(_GENERATION)
         return t
 
     # ------------------------------------------------------------------ rendering

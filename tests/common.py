@@ -42,22 +42,12 @@ def compare(img, ref):
 
 
 # Parity bar (north_star: "within a stated fp32 tolerance of the reference"): the fp32
-# framebuffer must be bit-identical to the oracle's — every deterministic case asserts
-# frac_diff == 0. The one documented source of allowed mismatch is `x ** hardness`:
-# the device evaluates integer exponents by fp64 binary exponentiation (rtx_trace.h
-# spec_pow), whose fp32 cast can differ from libm pow's within a few fp64 ulps of an fp32
-# rounding boundary. Only tests whose scenes draw arbitrary hardness values pass
-# pow_ulps=True, which allows 0.1 % of pixels to differ with a mean |d| <= 1e-4.
-POW_MAX_FRAC_DIFF = 1e-3
-POW_MAX_MEAN_ABS = 1e-4
-
-
-def assert_parity(img, ref, what="", pow_ulps=False):
+# framebuffer must be bit-identical to the oracle's -- every deterministic case asserts
+# frac_diff == 0. No tolerance is left: `x ** hardness` (rtx_trace.h spec_pow) is held to
+# libm pow bit for bit by tests/test_pow.py.
+def assert_parity(img, ref, what=""):
     s = compare(img, ref)
-    if pow_ulps:
-        assert s["frac_diff"] <= POW_MAX_FRAC_DIFF and s["mean_abs"] <= POW_MAX_MEAN_ABS, "%s parity: %s" % (what, s)
-    else:
-        assert s["frac_diff"] == 0.0, "%s parity (exact): %s" % (what, s)
+    assert s["frac_diff"] == 0.0, "%s parity (exact): %s" % (what, s)
     return s
 
 

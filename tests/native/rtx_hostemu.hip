@@ -377,3 +377,16 @@ extern "C" int64_t rtx_hostemu_jit_baked(const rtx_scene_desc* sd, char* out, in
     }
     return (int64_t)s.size();
 }
+
+// `x ** hardness` as the shading code evaluates it (rtx_trace.h spec_pow, integer
+// hardness), cast to fp32 as regular_lighting does, for n inputs.
+extern "C" void rtx_hostemu_spec_pow(const float* x, int64_t n, int32_t hardness, float* out, int threads) {
+    DMat m{};
+    m.hard_is_int = 1;
+    m.hard_int = hardness;
+    m.hardness = hardness;
+    int bits = 0;
+    while (bits < 31 && (hardness >> bits)) ++bits;
+#pragma omp parallel for num_threads(threads > 0 ? threads : 1) schedule(static)
+    for (int64_t i = 0; i < n; ++i) out[i] = (float)spec_pow((double)x[i], m, bits);
+}

@@ -207,9 +207,9 @@ def test_f32_helpers_follow_glm_order():
 def test_camera_key_follows_every_camera_change():
     """Scene._camera_key (which decides when rtx_camera_set re-uploads the tables) is
     cached by the camera's version: equal while nothing changes, new after an attribute
-    assignment, an in-place edit of motion_times, or a scene sample setting; the basis
-    vectors are read-only, so they change only by assignment."""
-    import pytest
+    assignment, an in-place edit of a basis vector or of motion_times (a list or any other
+    sequence assigned to it), or a scene sample setting."""
+    import numpy as np
     import rtx
     from rtx import f32 as F
     sc = rtx.load_bundled_scene("TwoSpheresPlane", resolution=(64, 48))
@@ -237,9 +237,27 @@ def test_camera_key_follows_every_camera_change():
     sc.seed = 7
     changed()
     assert sc._camera_key(1, 2) != sc._camera_key(0, 1)
-    with pytest.raises(ValueError):
-        vc.position[0] = 1.0  # read-only: move the camera by assigning a vector
     assert vc.motion_times == [0, 0.25, 1.0]
+    # basis vectors are writable in place, like PyGLM's vec3, and every write is seen
+    vc.position[0] = 1.0
+    changed()
+    vc.u[1:] = 0.5
+    changed()
+    vc.v += F.vec3(0.0, 0.0, 1e-3)
+    changed()
+    np.multiply(vc.w, 2.0, out=vc.w)
+    changed()
+    assert float(vc.position[0]) == 1.0 and vc.position.dtype == np.float32
+    d = vc.position - vc.w  # arithmetic gives plain arrays, not tracked views of the camera
+    assert type(d) is np.ndarray
+    d[0] = 5.0
+    assert sc._camera_key(0, 1) == seen[-1]
+    # motion_times assigned as an ndarray: kept as a tracked list
+    vc.motion_times = np.array([0.0, 0.5])
+    changed()
+    vc.motion_times[1] = 0.75
+    changed()
+    assert list(vc.motion_times) == [0.0, 0.75]
     # a camera vector of another type: every render compares the values themselves
     vc.position = [0.0, 2.0, 7.5]
     k1 = sc._camera_key(0, 1)
