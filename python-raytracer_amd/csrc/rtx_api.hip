@@ -1111,6 +1111,26 @@ bool light_grids(const HostScene& H, std::vector<DLGrid>& grids, std::vector<int
 
 namespace {
 
+// Scene properties the specialized kernels pin (from the converted records).
+struct SceneTraits {
+    int fc_mode = 0;              // RTX_FACE_CULL_MODE of the top-level meshes: 0 none, 1 all, 2 mixed
+    bool any_speed = false;       // some top-level object moves (else the JIT pins a static scene)
+    uint32_t light_dir_mask = 0;  // bit i: light i is directional (JIT, <= 8 lights)
+    int32_t uniform_hard = -1;    // >= 0: every specular lobe's integer hardness (JIT)
+};
+SceneTraits scene_traits(const HostScene& H) {
+    SceneTraits t;
+    int n_fc = 0, n_m = 0;
+    for (const DObj& o : H.objs)
+        if (o.type == RTX_MESH) { ++n_m; n_fc += o.face_cull ? 1 : 0; }
+    t.fc_mode = n_fc == 0 ? 0 : n_fc == n_m ? 1 : 2;
+    for (const DObj& o : H.objs) t.any_speed = t.any_speed || o.has_speed;
+    t.uniform_hard = H.uniform_hard >= 0 ? H.uniform_hard : -1;
+    for (size_t i = 0; i < H.lights.size() && i < 32; ++i)
+        if (H.lights[i].type == LIGHT_DIRECTIONAL) t.light_dir_mask |= 1u << i;
+    return t;
+}
+
 struct JitEntry {
     hipModule_t mod = nullptr;
     hipFunction_t fn = nullptr;
@@ -1184,6 +1204,13 @@ bool use_spp_mode(int spp, bool ext) {
     const char* m = getenv("RTX_SPP_MIN");
     const int lo = (m && *m) ? atoi(m) : 16;
     return ext && spp >= lo;
+}
+
+// Persistent-wave experiment (rtx_kernels.h RTX_PERSIST): $RTX_PERSIST = resident waves
+// per SIMD the grid is sized for (0 or unset: off).
+int persist_waves() {
+    const char* e = getenv("RTX_PERSIST");
+    return (e && *e) ? std::max(0, atoi(e)) : 0;
 }
 
 bool jit_enabled() {
@@ -1282,20 +1309,29 @@ bool jit_bake_enabled() {
     return !(e && e[0] == '0');
 }
 
-hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& kp, int fc_mode, bool any_speed,
-                                uint32_t ldir, int uniform_hard, bool mesh, bool sec, bool ext, bool cnt, bool jit,
-                                bool spp, bool out8, const std::string& baked, std::string* name_out,
-                                std::string* key_out) {
-    if (!jit_enabled()) return nullptr;
-    if (v.n_plane + v.n_sphere + v.n_box + v.n_mesh > 32 || v.n_lights > 8) return nullptr;  // code size
+// What a scene-specialized kernel is built from: its name, hiprtc source and options.
+struct JitSpec {
+    std::string name, src;
+    std::vector<std::string> opts;
+    bool baked = false;  // the source carries the scene's record values
+};
+
+// The specialized kernel of a scene and camera for arch (false: the generic kernel runs).
+// Host code only, so the tests' host build can print it (tools/jit_offline.py compiles it
+// to ISA without a GPU).
+bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, const SceneTraits& tr, bool mesh,
+              bool sec, bool ext, bool cnt, bool jit, bool spp, bool out8, const std::string& baked, JitSpec& out) {
+    const int fc_mode = tr.fc_mode;
+    const bool any_speed = tr.any_speed;
+    const uint32_t ldir = tr.light_dir_mask;
+    const int uniform_hard = tr.uniform_hard;
+    if (v.n_plane + v.n_sphere + v.n_box + v.n_mesh > 32 || v.n_lights > 8) return false;  // code size
     // CSG/texture kernels: the unrolled loops raise their (already high) register
     // pressure and the specialized kernel measured slower (NovelScene1 105 -> 134 ms)
     if (ext) {
         const char* e = getenv("RTX_JIT_EXT");  // experiment: specialize them anyway
-        if (!(e && e[0] == '1')) return nullptr;
+        if (!(e && e[0] == '1')) return false;
     }
-    const std::string arch = device_arch(device);
-    if (arch.empty()) return nullptr;
     std::vector<std::string> opts = {"--offload-arch=" + arch, "-O3", "-std=c++17", "-ffp-contract=off",
                                      "-DRTX_FIXED_COUNTS",
                                      "-DRTX_FIXED_NP=" + std::to_string(v.n_plane),
@@ -1323,6 +1359,7 @@ hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& k
         if (!spp && !(e && e[0] == '0')) opts.push_back("-DRTX_FIXED_NCOLS=" + std::to_string(kp.ncols));
     }
     if (uniform_hard >= 0) opts.push_back("-DRTX_FIXED_HARD=" + std::to_string(uniform_hard));
+    if (!spp && persist_waves() > 0) opts.push_back("-DRTX_PERSIST=1");
     if (out8) opts.push_back("-DRTX_OUT8=1");  // uint8 framebuffer (rtx_render_rgb8)
     // secondary-ray frames keep their material index in a register: 3 LDS words per frame
     if (sec && v.n_mats <= 64) opts.push_back("-DRTX_FRAME_MATBITS=6");
@@ -1381,6 +1418,24 @@ hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& k
                             "__restrict__ P, const rtx::Launch L) {\n  rtx::" + (spp ? "render_body_spp<" : "render_body<") +
                             b(mesh) + ", " + b(sec) +
                             ", " + b(ext) + ", " + b(cnt) + ", " + b(jit) + ">(P, L);\n}\n";
+    out.name = name;
+    out.src = src;
+    out.opts = opts;
+    out.baked = !prelude.empty();
+    return true;
+}
+
+hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& kp, const SceneTraits& tr, bool mesh,
+                                bool sec, bool ext, bool cnt, bool jit, bool spp, bool out8, const std::string& baked,
+                                std::string* name_out, std::string* key_out) {
+    if (!jit_enabled()) return nullptr;
+    const std::string arch = device_arch(device);
+    if (arch.empty()) return nullptr;
+    JitSpec sp;
+    if (!jit_spec(arch, v, kp, tr, mesh, sec, ext, cnt, jit, spp, out8, baked, sp)) return nullptr;
+    const std::string& name = sp.name;
+    const std::string& src = sp.src;
+    const std::vector<std::string>& opts = sp.opts;
     std::string key = src;
     for (const auto& o : opts) key += "\n" + o;
     *name_out = name;
@@ -1396,7 +1451,7 @@ hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& k
     for (int h = 0; h < kJitNumHeaders; ++h) all += kJitHeaderSrcs[h];
     char hash[32];
     snprintf(hash, sizeof(hash), "%016zx", std::hash<std::string>{}(all));
-    const bool is_baked = !prelude.empty();
+    const bool is_baked = sp.baked;
     const std::string dir = jit_cache_dir();
     const std::string path = dir.empty() ? "" : dir + (is_baked ? "/rtx_b_" : "/rtx_") + hash + ".co";
     std::string code;
@@ -1464,10 +1519,7 @@ struct rtx_scene {
     int device = 0;
     SceneView view{};
     bool has_mesh = false, has_secondary = false, has_ext = false;
-    int fc_mode = 0;  // RTX_FACE_CULL_MODE of the top-level meshes: 0 none, 1 all, 2 mixed
-    bool any_speed = false;  // some top-level object moves (else the JIT pins a static scene)
-    uint32_t light_dir_mask = 0;  // bit i: light i is directional (JIT, <= 8 lights)
-    int32_t uniform_hard = -1;    // >= 0: every specular lobe's integer hardness (JIT)
+    SceneTraits traits;  // what the scene-specialized kernels pin
     int32_t hlevels = 0;
     // host copies for the per-time-range hierarchy bounds
     std::vector<DNode> h_nodes;
@@ -1606,16 +1658,7 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
     s->has_secondary = H.has_secondary;
     s->has_ext = H.has_ext;
     s->hlevels = H.hlevels;
-    {
-        int n_fc = 0, n_m = 0;
-        for (const DObj& o : H.objs)
-            if (o.type == RTX_MESH) { ++n_m; n_fc += o.face_cull ? 1 : 0; }
-        s->fc_mode = n_fc == 0 ? 0 : n_fc == n_m ? 1 : 2;
-        for (const DObj& o : H.objs) s->any_speed = s->any_speed || o.has_speed;
-        s->uniform_hard = H.uniform_hard >= 0 ? H.uniform_hard : -1;
-        for (size_t i = 0; i < H.lights.size() && i < 32; ++i)
-            if (H.lights[i].type == LIGHT_DIRECTIONAL) s->light_dir_mask |= 1u << i;
-    }
+    s->traits = scene_traits(H);
     s->jit_baked = jit_baked_records(H.objs, H.mats, H.lights);
     {  // primary-ray bins (per camera, rtx_camera_set)
         s->h_bins.objs = H.objs;
@@ -1879,13 +1922,19 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
     }
     rtx_scene::Resolved& rs = s->resolved[(out8 ? 8 : 0) | (cnt ? 4 : 0) | (jit ? 2 : 0) | (spp_mode ? 1 : 0)];
     if (!rs.done) {
-        rs.fn = jit_render_kernel(s->device, s->view, s->kp, s->fc_mode, s->any_speed, s->light_dir_mask,
-                                  s->uniform_hard, s->has_mesh, s->has_secondary, s->has_ext, cnt, jit, spp_mode,
-                                  out8, s->jit_baked, &rs.name, &rs.key);
+        rs.fn = jit_render_kernel(s->device, s->view, s->kp, s->traits, s->has_mesh, s->has_secondary, s->has_ext,
+                                  cnt, jit, spp_mode, out8, s->jit_baked, &rs.name, &rs.key);
         rs.done = true;
     }
     if (rs.fn && jit_enabled()) {
         void* args[] = {(void*)&kp, (void*)&L};
+        if (!spp_mode && persist_waves() > 0) {  // experiment: grid = resident wave slots
+            int cus = 0;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) == hipSuccess && cus > 0) {
+                const int64_t slots = (int64_t)cus * 4 * persist_waves() / (blk / 64);  // blocks
+                nblocks = std::min<int64_t>(nblocks, std::max<int64_t>(1, slots / std::max(1, nframes)));
+            }
+        }
         RTX_HIP(hipModuleLaunchKernel(rs.fn, (unsigned)nblocks, (unsigned)nframes, 1, blk, 1, 1,
                                       s->has_ext ? (unsigned)(hbytes * blk) : 0u, st, args, nullptr));
         s->last_kernel = rs.name;

@@ -312,6 +312,12 @@ __host__ __device__ inline int32_t primary_bin(const SceneView& S, int32_t row, 
 #ifndef RTX_PPL
 #define RTX_PPL 1
 #endif
+// Persistent waves (experiment, scene-specialized kernels: RTX_PERSIST=1 in the
+// environment): render_body loops over the launch's tiles with a grid of about the
+// resident wave slots (rtx_api.hip render_launch sizes it).
+#ifndef RTX_PERSIST
+#define RTX_PERSIST 0
+#endif
 
 // Output pixel (row, column within the block) of this work-item. RTX_TILE=1 maps each
 // 64-lane wave to an 8x8 pixel tile (coherent rays per wave); 0 maps waves to 64
@@ -416,8 +422,23 @@ __device__ __forceinline__ void render_body(const KParams* __restrict__ Pp, cons
     const FrameStack fs{frames + threadIdx.x, B};
     const HStack hs{hstack + threadIdx.x, B};
     bool any_active = false;
+#if RTX_PERSIST
+    // persistent waves: the grid holds about as many waves as the chip keeps resident, and
+    // each wave renders the tiles w, w + nw, w + 2 nw, ... of the launch (a static stride:
+    // the waves resident at one time cover a contiguous stretch of rows)
+    static_assert(RTX_TILE == 1 && RTX_PPL == 1, "persistent waves take whole 8x8 tiles");
+    const int tiles_x = (ncols + 7) >> 3;
+    const int n_tiles = tiles_x * ((L.nrows + 7) >> 3);
+    const int nw = (int)gridDim.x * (B >> 6);
+    for (int w = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (B >> 6) + (threadIdx.x >> 6))); w < n_tiles;
+         w += nw) {
+        const int lane = threadIdx.x & 63;
+        const int ty = w / tiles_x, tx = w - ty * tiles_x;
+        const PixelRC px{ty * 8 + (lane >> 3), tx * 8 + (lane & 7)};
+#else
     for (int sub = 0; sub < RTX_PPL; ++sub) {
         const PixelRC px = pixel_rc(ncols, sub, L.perm);
+#endif
         const bool active = px.r < L.nrows && px.c < ncols;
         any_active = any_active || active;
         // primary-ray face bin of the wave's 8x8 tile (its top-left pixel)

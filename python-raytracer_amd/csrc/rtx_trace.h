@@ -599,9 +599,18 @@ RTX_HD RayInv ray_inv(f3 o, f3 d) {
 // the compiler hoists their loop-invariant fp64 numerators (bound - origin) out of the
 // shading loops, where they hold VGPRs for the whole kernel (TorusMesh: 40 B/lane of
 // spills for its bounding volume's six numerators).
-__host__ __device__ __attribute__((noinline)) inline bool box_slabs_far(f3 o, f3 d, f3 mn, f3 mx, double& start,
-                                                                       int& label, double& end) {
-    return box_slabs(o, d, mn, mx, start, label, end);
+// (The result comes back by value, in registers: out-parameters of an out-of-line call
+// would live in scratch, and every caller would store their initial values there on
+// each visit -- 20 B/lane per box test, DepthOfField's extra HBM writes.)
+struct SlabFar {
+    double start, end;
+    int label;
+    bool valid;
+};
+__host__ __device__ __attribute__((noinline)) inline SlabFar box_slabs_far(f3 o, f3 d, f3 mn, f3 mx) {
+    SlabFar r;
+    r.valid = box_slabs(o, d, mn, mx, r.start, r.label, r.end);
+    return r;
 }
 
 // The same slabs decided in fp32, with box_slabs as the fallback. Each reference quotient
@@ -682,8 +691,10 @@ RTX_HD bool box_entry_iv(f3 o, f3 d, f3 mn, f3 mx, const SlabIv& iv, bool live, 
     const bool und = !yes && !no;
     if (RTX_ANY(und)) {
         if (und) {
-            double e = 0.0;
-            valid = box_slabs_far(o, d, mn, mx, start, label, e) && !(start > e || start < 0.0);
+            const SlabFar f = box_slabs_far(o, d, mn, mx);
+            start = f.start;
+            label = f.label;
+            valid = f.valid && !(f.start > f.end || f.start < 0.0);
         }
     }
     return valid;
@@ -714,9 +725,8 @@ RTX_HD bool box_shadow_iv(f3 o, f3 d, f3 mn, f3 mx, const SlabIv& iv, double t_m
     const bool und = !yes && !no;
     if (RTX_ANY(und)) {
         if (und) {
-            double start, end;
-            int label;
-            occ = box_slabs_far(o, d, mn, mx, start, label, end) && !(start > end) && 1e-4 < start && start < t_max;
+            const SlabFar f = box_slabs_far(o, d, mn, mx);
+            occ = f.valid && !(f.start > f.end) && 1e-4 < f.start && f.start < t_max;
         }
     }
     return occ;
@@ -735,10 +745,8 @@ RTX_HD bool mesh_bv(const O& ob, f3 o, f3 d) {
         const bool yes = iv.sure && !iv.reject && iv.s_hi < iv.e_lo && iv.s_lo > 0.0f;
         const bool no = iv.reject || (iv.sure && (iv.s_lo > iv.e_hi || iv.s_hi < 0.0f));
         if (yes || no) return yes;
-        double start, end;
-        int label;
-        if (!box_slabs_far(o, d, mn, mx, start, label, end)) return false;
-        return !(start > end || start < 0.0);
+        const SlabFar f = box_slabs_far(o, d, mn, mx);
+        return f.valid && !(f.start > f.end || f.start < 0.0);
     }
     double b, s, two_a;
     if (!sphere_roots(o, d, ld3(ob.bv_a), ob.bv_r2, b, s, two_a)) return false;

@@ -2,9 +2,9 @@
 
     python -m rtx.main --infile S.json --outfile out.png [--subimage k --tasks N]
 
-Full render: rot90 + truncating uint8 conversion + PNG (main.py:324-328; the viewer call
-`im.show()` is not reproduced). Strip render: numpy.save of the (strip_w, H, 3) float64
-strip (main.py:320-322), for rtx.glue. Extensions: --resolution W H and --spp AA [DOF]
+Full render: rot90 + truncating uint8 conversion + PNG (main.py:29-34; the viewer call
+`im.show()` at :35 is not reproduced). Strip render: numpy.save of the (strip_w, H, 3)
+float64 strip (main.py:26-28), for rtx.glue. Extensions: --resolution W H and --spp AA [DOF]
 edit the scene like the bench configs; --distributed renders row blocks on every rank
 of a torch.distributed job and gathers the frame to rank 0 (render.nu's role).
 """

@@ -390,3 +390,43 @@ extern "C" void rtx_hostemu_spec_pow(const float* x, int64_t n, int32_t hardness
 #pragma omp parallel for num_threads(threads > 0 ? threads : 1) schedule(static)
     for (int64_t i = 0; i < n; ++i) out[i] = (float)spec_pow((double)x[i], m, bits);
 }
+
+// The scene-specialized kernel librtx.so would build for this scene and camera on gfx950
+// (rtx_api.hip jit_spec), as text: "name\n" + one option per line + "\n" + the hiprtc
+// source. Returns the text's length (-1: the generic kernel runs, -2: bad input); writes
+// at most cap bytes (NUL-terminated). tools/jit_offline.py compiles it without a GPU.
+extern "C" int64_t rtx_hostemu_jit_spec(const rtx_scene_desc* sd, const rtx_camera_desc* cd, int32_t cnt, int32_t out8,
+                                        char* out, int64_t cap) {
+    HostScene H;
+    if (convert_scene(sd, H)) return -2;
+    KParams k;
+    if (convert_camera(cd, k)) return -2;
+    bind_view(H, k.S);
+    k.S.n_objs_all = (int32_t)H.objs.size();
+    k.S.n_mats = (int32_t)H.mats.size();
+    k.S.n_tris = (int32_t)H.tris.size();
+    k.S.n_leaves = (int32_t)H.leaves.size();
+    Grids lg;
+    lg.bind(H, k.S);
+    std::vector<int32_t> bstart, bfaces;
+    std::vector<float> bz;
+    std::vector<uint32_t> bmask;
+    int32_t bins_x = 0, mesh_bins = 0;
+    const char* be = getenv("RTX_BINS");
+    if (!(be && be[0] == '0') && primary_bins(H, cd, bstart, bfaces, bz, bmask, bins_x, mesh_bins)) k.S.bins_on = 1;
+    const int spp = k.n_dof * k.n_aa * k.n_times;
+    const bool spp_mode = use_spp_mode(spp, H.has_ext);
+    JitSpec sp;
+    if (!jit_spec("gfx950", k.S, k, scene_traits(H), H.has_mesh, H.has_secondary, H.has_ext, cnt != 0,
+                  k.jitter != RTX_JITTER_OFF, spp_mode, out8 != 0, jit_baked_records(H.objs, H.mats, H.lights), sp))
+        return -1;
+    std::string s = sp.name + "\n";
+    for (const auto& o : sp.opts) s += o + "\n";
+    s += "\n" + sp.src;
+    if (out && cap > 0) {
+        const size_t n = std::min((size_t)cap - 1, s.size());
+        memcpy(out, s.data(), n);
+        out[n] = '\0';
+    }
+    return (int64_t)s.size();
+}
