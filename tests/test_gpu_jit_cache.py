@@ -27,7 +27,7 @@ def test_baked_kernels_are_bounded(tmp_path, monkeypatch):
     monkeypatch.setenv("RTX_JIT_DISK_BAKED", "2")
     lib = N.load()
     base = lib.rtx_jit_modules()
-    d = bundled_scene_dict("TwoSpheresPlane", resolution=(32, 24))
+    d = bundled_scene_dict("TwoSpheresPlane", resolution=(32, 24), spp=(1, None))  # one sample: baked records
     d.pop("__base_dir__", None)
     counts = []
     for k in range(5):
