@@ -32,6 +32,7 @@
 #include "../../include/rtx.h"
 #include "rtx_kernels.h"
 #include "rtx_launch.h"
+#include "rtx_split.h"
 
 // faces per mesh BVH leaf (cluster); meshes of at most kFaceCullMaxFaces faces also
 // test each face's box before its exact test (DObj::face_cull)
@@ -733,6 +734,7 @@ int convert_scene(const rtx_scene_desc* desc, HostScene& H) {
 // the caller (device uploads, or host arrays in the emulation build).
 int convert_camera(const rtx_camera_desc* c, KParams& k) {
     if (!c) return fail(RTX_ERR_INVALID, "rtx_camera_set: null argument");
+    k = KParams{};
     if (c->width < 1 || c->height < 1 || c->ncols < 1 || c->col0 < 0 || (int64_t)c->col0 + c->ncols > c->width)
         return fail(RTX_ERR_INVALID, "rtx_camera_set: bad image/strip size");
     if (c->n_dof < 1 || c->n_aa < 1 || c->n_times < 1)
@@ -1573,6 +1575,10 @@ struct rtx_scene {
     // fp32 staging of the rgb8 entry points when no scene-specialized kernel is available
     float* d_scratch = nullptr;
     size_t scratch_floats = 0;
+    // the split hierarchy passes' shade-point records (rtx_split.h) and their counter
+    ShadePt* d_split = nullptr;
+    unsigned int* d_split_count = nullptr;
+    int64_t split_cap = 0;
 };
 
 namespace {
@@ -1608,6 +1614,8 @@ void free_camera(rtx_scene* s) {
 void free_scene(rtx_scene* s) {
     free_camera(s);
     (void)hipFree(s->d_scratch);
+    (void)hipFree(s->d_split);
+    (void)hipFree(s->d_split_count);
     for (void* p : {s->d_objs, s->d_tris, s->d_trins, s->d_fboxes, s->d_mats, s->d_lights, s->d_leaves, s->d_tri_orig, s->d_nodes, s->d_nmat,
                     s->d_texels, s->d_lut, s->d_bounds_abi, s->d_lgrid, s->d_lg_start, s->d_lg_faces, s->d_lg_d2})
         (void)hipFree(p);
@@ -1785,6 +1793,8 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     }
     k.xs = (cptr<float>)s->d_xs; k.ys = (cptr<float>)s->d_ys; k.dof_o = (cptr<float>)s->d_dof;
     k.aa_o = (cptr<float>)s->d_aa; k.times = (cptr<float>)s->d_times; k.noise = (cptr<float>)s->d_noise;
+    if (const char* e = getenv("RTX_WAVE_LOG_PTR"))  // tools/wave_timeline.py (RTX_WAVE_LOG kernels)
+        k.wave_log = reinterpret_cast<unsigned long long*>((uintptr_t)strtoull(e, nullptr, 0));
     RTX_HIP(hipMalloc((void**)&s->d_kp, sizeof(KParams)));
     RTX_HIP(hipMemcpy(s->d_kp, &k, sizeof(KParams), hipMemcpyHostToDevice));
     s->kp = k;
@@ -1889,6 +1899,63 @@ int launch_to_rgb8(const float* fb, uint8_t* out, int64_t n, hipStream_t st) {
     return RTX_OK;
 }
 
+// The hierarchy/texture scenes in three passes (rtx_split.h): RTX_SPLIT=1 (experiment).
+bool split_enabled() {
+    const char* e = getenv("RTX_SPLIT");
+    return e && e[0] == '1';
+}
+
+// Records per chunk ($RTX_SPLIT_RECORDS, default 2^26 = 4 GiB of 64-B records): a chunk
+// takes as many whole pixels as fit when every sample fills every chain level.
+int64_t split_records() {
+    const char* e = getenv("RTX_SPLIT_RECORDS");
+    const long long v = (e && *e) ? atoll(e) : (1ll << 26);
+    return std::min<long long>(std::max<long long>(v, 1024), 1ll << 30);
+}
+
+int render_split(rtx_scene* s, Launch L, const KParams* kp, size_t hbytes, hipStream_t st, int sel, int32_t nframes) {
+    constexpr int B = kBlock<true>;
+    const int spp = s->kp.n_dof * s->kp.n_aa * s->kp.n_times;
+    const int64_t npix = (int64_t)L.nrows * s->kp.ncols;
+    if (npix <= 0 || nframes <= 0) return RTX_OK;
+    const int levels = s->has_secondary ? kMaxDepth : 1;
+    const int ppb = spp_pixels_per_block(spp, B);
+    int64_t chunk = std::max<int64_t>(1, split_records() / ((int64_t)spp * levels));
+    if (chunk < npix) chunk = std::max<int64_t>(ppb, chunk / ppb * ppb);
+    chunk = std::min(chunk, npix);
+    const int64_t cap = chunk * spp * levels;
+    if (cap >= (1ll << 31)) return fail(RTX_ERR_INVALID, "rtx_render: split chunk too large");
+    if (s->split_cap < cap) {
+        (void)hipFree(s->d_split);
+        s->d_split = nullptr;
+        s->split_cap = 0;
+        RTX_HIP(hipMalloc((void**)&s->d_split, (size_t)cap * sizeof(ShadePt)));
+        if (!s->d_split_count) RTX_HIP(hipMalloc((void**)&s->d_split_count, sizeof(unsigned int)));
+        s->split_cap = cap;
+    }
+    auto launch = [&](int pass, const RenderLaunch& r, const Launch& Lc, const SplitBuf& sb) {
+        return s->has_mesh ? launch_split_m1(sel, pass, r, Lc, sb) : launch_split_m0(sel, pass, r, Lc, sb);
+    };
+    char* base = reinterpret_cast<char*>(L.fb);
+    for (int32_t f = 0; f < nframes; ++f) {
+        Launch Lc = L;
+        Lc.fb = reinterpret_cast<float*>(base + f * L.fstride);
+        Lc.fstride = 0;
+        for (int64_t p0 = 0; p0 < npix; p0 += chunk) {
+            const int64_t np = std::min(chunk, npix - p0), nq = np * spp;
+            Lc.pix0 = (int32_t)p0;
+            const SplitBuf sb{s->d_split, s->d_split_count, nq, cap};
+            RTX_HIP(hipMemsetAsync(s->d_split_count, 0, sizeof(unsigned int), st));
+            RenderLaunch r{kp, (unsigned)((nq + B - 1) / B), 1u, hbytes * B, st, true};
+            RTX_HIP(launch(0, r, Lc, sb));
+            RTX_HIP(launch(1, r, Lc, sb));
+            r.nblocks = (unsigned)((np + ppb - 1) / ppb);
+            RTX_HIP(launch(2, r, Lc, sb));
+        }
+    }
+    return RTX_OK;
+}
+
 int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, bool out8, int32_t nframes) {
     const int32_t nrows = L.nrows;
     int cur = -1;
@@ -1918,7 +1985,7 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
         uint64_t m = std::max<uint64_t>(1, (uint64_t)((double)T * 0.6180339887498949));
         while (T > 1 && std::gcd(m, T) != 1) ++m;
         L.perm = (uint32_t)(T > 1 ? m % T : 1);
-        L.pad0 = 0;
+        L.pix0 = 0;
     }
     rtx_scene::Resolved& rs = s->resolved[(out8 ? 8 : 0) | (cnt ? 4 : 0) | (jit ? 2 : 0) | (spp_mode ? 1 : 0)];
     if (!rs.done) {
@@ -1970,6 +2037,12 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
              s->has_secondary ? 1 : 0, s->has_ext ? 1 : 0, cnt ? 1 : 0, jit ? 1 : 0,
              (spp_mode && s->has_ext) ? "_spp" : "");
     s->last_kernel = gname;
+    if (s->has_ext && split_enabled() && s->view.n_lights <= 32) {
+        snprintf(gname, sizeof(gname), "k_split_%d%d%d%d", s->has_mesh ? 1 : 0, s->has_secondary ? 1 : 0, cnt ? 1 : 0,
+                 jit ? 1 : 0);
+        s->last_kernel = gname;
+        return render_split(s, L, kp, hbytes, st, sel & 11, nframes);
+    }
     if (s->has_ext) {  // precompiled in rtx_kern_ext_m{0,1}.hip
         const RenderLaunch rl{kp, (unsigned)nblocks, (unsigned)nframes, hbytes * kBlock<true>, st, spp_mode};
         RTX_HIP(s->has_mesh ? launch_render_ext_m1(sel, rl, L) : launch_render_ext_m0(sel, rl, L));

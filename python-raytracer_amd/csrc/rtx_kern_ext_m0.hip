@@ -4,6 +4,7 @@
 
 #define RTX_EXT_TU 1
 #include "rtx_kernels.h"
+#include "rtx_split.h"
 #include "rtx_launch.h"
 
 namespace rtx {
@@ -25,6 +26,27 @@ hipError_t launch_render_ext_m0(int sel, const RenderLaunch& r, const Launch& L)
     }
 #undef RTX_EXT_CASE
 #undef RTX_EXT_LAUNCH
+    return hipGetLastError();
+}
+
+hipError_t launch_split_m0(int sel, int pass, const RenderLaunch& r, const Launch& L, const SplitBuf& sb) {
+    constexpr int B = kBlock<true>;
+    const bool sec = (sel & 8) != 0, cnt = (sel & 2) != 0, jit = (sel & 1) != 0;
+    const dim3 g(r.nblocks), b(B);
+    if (pass == 0) {
+#define RTX_SPLIT_A(S, C, J) hipLaunchKernelGGL((k_split_trace<false, S, C, J>), g, b, r.lds_bytes, r.stream, r.kp, L, sb)
+        if (sec) { if (cnt) { if (jit) RTX_SPLIT_A(true, true, true); else RTX_SPLIT_A(true, true, false); }
+                   else { if (jit) RTX_SPLIT_A(true, false, true); else RTX_SPLIT_A(true, false, false); } }
+        else { if (cnt) { if (jit) RTX_SPLIT_A(false, true, true); else RTX_SPLIT_A(false, true, false); }
+               else { if (jit) RTX_SPLIT_A(false, false, true); else RTX_SPLIT_A(false, false, false); } }
+#undef RTX_SPLIT_A
+    } else if (pass == 1) {
+        if (cnt) hipLaunchKernelGGL((k_split_shadow<false, true>), g, b, r.lds_bytes, r.stream, r.kp, L, sb);
+        else hipLaunchKernelGGL((k_split_shadow<false, false>), g, b, r.lds_bytes, r.stream, r.kp, L, sb);
+    } else {
+        if (sec) hipLaunchKernelGGL((k_split_shade<false, true>), g, b, 0, r.stream, r.kp, L, sb);
+        else hipLaunchKernelGGL((k_split_shade<false, false>), g, b, 0, r.stream, r.kp, L, sb);
+    }
     return hipGetLastError();
 }
 

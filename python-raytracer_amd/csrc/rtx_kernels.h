@@ -28,6 +28,9 @@ struct KParams {
     int32_t width, height, col0, ncols;
     int32_t n_dof, n_aa, n_times, jitter;
     uint32_t seed_lo, seed_hi;
+    // tools/wave_timeline.py only (kernels built with RTX_WAVE_LOG): per wave, its start
+    // and end (s_memrealtime, 100 MHz) and hardware ids, 4 x uint64 per wave of the launch
+    unsigned long long* wave_log;
 };
 
 template <bool COUNT>
@@ -271,7 +274,8 @@ struct Launch {
     int32_t gphase, gstride;
     // rtx_render_frames: blockIdx.y renders frame y of a batch into fb + y * fstride bytes
     int64_t fstride;
-    uint32_t perm, pad0;  // RTX_TILE_ORDER 2: the wave permutation's multiplier
+    uint32_t perm;  // RTX_TILE_ORDER 2: the wave permutation's multiplier
+    int32_t pix0;   // split hierarchy passes (rtx_split.h): the chunk's first pixel of the block
 };
 
 // This block's framebuffer (frame blockIdx.y of a batched launch; the only frame otherwise).
@@ -404,9 +408,35 @@ __device__ __forceinline__ void stage_records_lds(const SceneView& S) {
 #endif
 }
 
+// Wave timeline probe (experiment): the wave's start/end clock and where it ran.
+#if defined(RTX_WAVE_LOG) && defined(__HIP_DEVICE_COMPILE__)
+struct WaveClock {
+    unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    __device__ void done(const KParams* Pp) const {
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        if ((threadIdx.x & 63) == 0 && Pp->wave_log != nullptr) {
+            const uint64_t w = ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+            const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+            const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+            unsigned long long* o = Pp->wave_log + 4 * w;
+            o[0] = t0;
+            o[1] = t1;
+            o[2] = hw;
+            o[3] = xcc;
+        }
+    }
+};
+#define RTX_WAVE_CLOCK_BEGIN const WaveClock wclk_;
+#define RTX_WAVE_CLOCK_END wclk_.done(Pp);
+#else
+#define RTX_WAVE_CLOCK_BEGIN
+#define RTX_WAVE_CLOCK_END
+#endif
+
 template <bool MESH, bool SEC, bool X, bool COUNT, bool JIT>
 __device__ __forceinline__ void render_body(const KParams* __restrict__ Pp, const Launch L) {
     constexpr int B = kBlock<X>;
+    RTX_WAVE_CLOCK_BEGIN
     if (MESH) stage_mesh_lds(Pp->S);
     stage_records_lds(Pp->S);
 #ifdef RTX_FIXED_NCOLS  // scene-specialized kernels pin the strip width (tile index math by constants)
@@ -448,6 +478,7 @@ __device__ __forceinline__ void render_body(const KParams* __restrict__ Pp, cons
             render_pixel<MESH, SEC, X, COUNT, JIT>(*Pp, frame_fb(L), image_row(L, px.r) - px.r, px.r, px.c, tl, fs, hs, bin);
     }
     flush_tally<COUNT>(tl, L.counters, any_active);
+    RTX_WAVE_CLOCK_END
 }
 
 // n / d and n % d for 0 <= n < 2^22, d >= 1 (rd = fl32(1 / d)): the fp32 quotient is

@@ -21,4 +21,9 @@ struct RenderLaunch {
 // sel: (SEC ? 8 : 0) | (COUNT ? 2 : 0) | (JITTER ? 1 : 0); returns hipGetLastError().
 hipError_t launch_render_ext_m0(int sel, const RenderLaunch& r, const Launch& L);
 hipError_t launch_render_ext_m1(int sel, const RenderLaunch& r, const Launch& L);
+
+// The split passes of rtx_split.h (pass 0 trace, 1 shadow, 2 shade) with r.nblocks blocks.
+struct SplitBuf;
+hipError_t launch_split_m0(int sel, int pass, const RenderLaunch& r, const Launch& L, const SplitBuf& sb);
+hipError_t launch_split_m1(int sel, int pass, const RenderLaunch& r, const Launch& L, const SplitBuf& sb);
 }  // namespace rtx

@@ -2124,9 +2124,11 @@ RTX_HD double spec_pow(double x, const DMat& m, int pow_bits) {
 }
 
 // _compute_regular_lighting (scene.py:140-187)
+// occ_mask >= 0 (the split hierarchy passes, rtx_split.h): bit li says whether light li's
+// shadow ray is occluded, as a separate pass found it; no shadow ray is traced here.
 template <bool MESH, bool X, bool COUNT>
 RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const DMat& m, f3 diffuse, float time,
-                           Tally& tl, const HStack& hs) {
+                           Tally& tl, const HStack& hs, int64_t occ_mask = -1) {
     f3 colour = mk(0.0f, 0.0f, 0.0f);
     tally_inc<COUNT>(tl, &Tally::shade);
     OriginTerms ot;
@@ -2153,7 +2155,11 @@ RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const 
             t_max = INFINITY;
         }
         tally_inc<COUNT>(tl, &Tally::shadow);
-        if (RTX_ABLATE != 1 && occluded<MESH, X, COUNT>(S, pos, sdir, t_max, time, tl, hs, otp, li)) continue;
+        if (occ_mask >= 0) {
+            if ((occ_mask >> li) & 1) continue;
+        } else if (RTX_ABLATE != 1 && occluded<MESH, X, COUNT>(S, pos, sdir, t_max, time, tl, hs, otp, li)) {
+            continue;
+        }
         if (RTX_ABLATE == 3) { colour = add(colour, mul(ld3(L.cp), diffuse)); continue; }
         f3 light_dir = point ? normalize(sdir) : ld3(L.ndir);
         f3 lambert = scale(diffuse, pos_part(dot(normal, light_dir)));

@@ -13,6 +13,7 @@ DEPS = [SRC, os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_api.h
         os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_kernels.h"),
         os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_fastmath.h"),
         os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_launch.h"),
+        os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_split.h"),
         os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_jit_sources.inc"),
         os.path.join(HERE, "..", "include", "rtx.h")]
 
@@ -54,6 +55,21 @@ def render(scene, subimage=0, tasks=1, threads=8):
     fb = np.zeros((H, cd.ncols, 3), np.float32)
     cnt = np.zeros(16, np.uint64)
     _chk(lib().rtx_hostemu_render(C.addressof(sd), C.addressof(cd), 0, H, fb.ctypes.data, cnt.ctypes.data, threads))
+    img = np.ascontiguousarray(np.transpose(fb[::-1], (1, 0, 2))).astype(np.float64)
+    return img, cnt
+
+
+def render_split(scene, subimage=0, tasks=1, threads=8, chunk_records=1 << 26):
+    """The hierarchy/texture scenes' three split passes (csrc/rtx_split.h) on the host,
+    chunked like render_split of librtx.so; same layout as render()."""
+    sd = scene.scene_desc()
+    cd, tables = scene.camera_desc(subimage, tasks)
+    H = scene.vc.height
+    fb = np.zeros((H, cd.ncols, 3), np.float32)
+    cnt = np.zeros(16, np.uint64)
+    f = lib().rtx_hostemu_render_split
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_int, C.c_int64]
+    _chk(f(C.addressof(sd), C.addressof(cd), 0, H, fb.ctypes.data, cnt.ctypes.data, threads, chunk_records))
     img = np.ascontiguousarray(np.transpose(fb[::-1], (1, 0, 2))).astype(np.float64)
     return img, cnt
 

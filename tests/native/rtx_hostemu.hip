@@ -9,6 +9,8 @@
 namespace rtx {
 hipError_t launch_render_ext_m0(int, const RenderLaunch&, const Launch&) { return hipErrorNotSupported; }
 hipError_t launch_render_ext_m1(int, const RenderLaunch&, const Launch&) { return hipErrorNotSupported; }
+hipError_t launch_split_m0(int, int, const RenderLaunch&, const Launch&, const SplitBuf&) { return hipErrorNotSupported; }
+hipError_t launch_split_m1(int, int, const RenderLaunch&, const Launch&, const SplitBuf&) { return hipErrorNotSupported; }
 }  // namespace rtx
 
 #include <omp.h>
@@ -429,4 +431,113 @@ extern "C" int64_t rtx_hostemu_jit_spec(const rtx_scene_desc* sd, const rtx_came
         out[n] = '\0';
     }
     return (int64_t)s.size();
+}
+
+// The split hierarchy passes (rtx_split.h trace_sample / shadow_record / shade_sample) on
+// the host, chunked like rtx_api.hip render_split (chunk_records: records per chunk), over
+// image rows [row0, row0 + nrows). Deeper records are appended by concurrent threads, so
+// their order varies from run to run; the frame must not.
+template <bool MESH, bool SEC, bool JIT>
+static void split_frame(const KParams& k, const Launch& L0, int64_t npix, int spp, int64_t chunk_records, float* fb,
+                        uint64_t* tot, int threads) {
+    const int levels = SEC ? kMaxDepth : 1;
+    int64_t chunk = std::max<int64_t>(1, chunk_records / ((int64_t)spp * levels));
+    chunk = std::min(chunk, npix);
+    const int64_t cap = chunk * spp * levels;
+    std::vector<ShadePt> rec((size_t)cap);
+    unsigned int count = 0;
+    for (int64_t p0 = 0; p0 < npix; p0 += chunk) {
+        const int64_t np = std::min(chunk, npix - p0), nq = np * spp;
+        Launch L = L0;
+        L.pix0 = (int32_t)p0;
+        count = 0;
+        const SplitBuf sb{rec.data(), &count, nq, cap};
+#pragma omp parallel num_threads(threads > 0 ? threads : 1)
+        {
+            uint64_t loc[RTX_COUNTERS] = {};
+            float hst[kMaxHLevels * 9];
+            const HStack hs{hst, 1};
+#pragma omp for schedule(dynamic, 64)
+            for (int64_t q = 0; q < nq; ++q) {
+                Tally tl = {};
+                auto alloc = [&](bool hit) -> int64_t {
+                    if (!hit) return -1;
+                    const int64_t slot = sb.nsamp + (int64_t)__atomic_fetch_add(sb.count, 1u, __ATOMIC_RELAXED);
+                    return slot < sb.cap ? slot : -1;
+                };
+                trace_sample<MESH, SEC, true, JIT>(k, L, sb, q, tl, hs, alloc);
+                for (int c = 0; c < kMaxDepth; ++c) loc[c] += tl.cast[c];
+                loc[RTX_CNT_TRI] += tl.tri;
+            }
+            const int64_t n = sb.nsamp + (int64_t)__atomic_load_n(sb.count, __ATOMIC_RELAXED);
+#pragma omp for schedule(dynamic, 64)
+            for (int64_t r = 0; r < n; ++r) {
+                if (!(rec[r].flags & kSpHit)) continue;
+                Tally tl = {};
+                rec[r].occ = shadow_record<MESH, true>(k.S, rec[r], tl, hs);
+                loc[RTX_CNT_SHADOW] += tl.shadow;
+                loc[RTX_CNT_SHADE] += tl.shade;
+                loc[RTX_CNT_TRI] += tl.tri;
+            }
+            float frames[kMaxDepth * 4];
+            const FrameStack fs{frames, 1};
+#pragma omp for schedule(dynamic, 16)
+            for (int64_t p = 0; p < np; ++p) {
+                f3 colour = mk(0.0f, 0.0f, 0.0f);
+                for (int s = 0; s < spp; ++s) colour = add(colour, shade_sample<MESH, SEC>(k.S, sb, p * spp + s, fs));
+                const int64_t o = 3 * (p0 + p);
+                fb[o] = sample_mean(k, colour.x);
+                fb[o + 1] = sample_mean(k, colour.y);
+                fb[o + 2] = sample_mean(k, colour.z);
+            }
+#pragma omp critical
+            for (int c = 0; c < RTX_COUNTERS; ++c) tot[c] += loc[c];
+        }
+    }
+}
+
+extern "C" int rtx_hostemu_render_split(const rtx_scene_desc* sd, const rtx_camera_desc* cd, int32_t row0,
+                                        int32_t nrows, float* fb, uint64_t* counters, int threads,
+                                        int64_t chunk_records) {
+    HostScene H;
+    int rc = convert_scene(sd, H);
+    if (rc) return rc;
+    KParams k;
+    if ((rc = convert_camera(cd, k))) return rc;
+    if (row0 < 0 || nrows < 0 || row0 + nrows > cd->height) return fail(RTX_ERR_INVALID, "bad rows");
+    if (!H.has_ext) return fail(RTX_ERR_INVALID, "the split passes serve hierarchy/texture scenes");
+    bind_view(H, k.S);
+    Grids lg;
+    lg.bind(H, k.S);
+    std::vector<float> times(cd->n_times);
+    for (int i = 0; i < cd->n_times; ++i) times[i] = (float)cd->times[i];
+    const auto mm = std::minmax_element(times.begin(), times.end());
+    Nodes nv;
+    nv.bind(H, k.S, *mm.first, *mm.second);
+    std::vector<float> noise;
+    const size_t nsamp = (size_t)cd->n_dof * cd->n_aa;
+    if (cd->jitter == RTX_JITTER_REPLAY) noise.assign(cd->noise, cd->noise + 3 * (size_t)cd->ncols * cd->height * nsamp);
+    k.xs = (cptr<float>)cd->xs; k.ys = (cptr<float>)cd->ys; k.dof_o = (cptr<float>)cd->dof_origins;
+    k.aa_o = (cptr<float>)cd->aa_origins; k.times = (cptr<float>)times.data(); k.noise = (cptr<float>)noise.data();
+    Launch L{};
+    L.row0 = row0;
+    L.nrows = nrows;
+    const int spp = k.n_dof * k.n_aa * k.n_times;
+    uint64_t tot[RTX_COUNTERS] = {};
+    const int64_t npix = (int64_t)nrows * k.ncols;
+    const bool jit = k.jitter != RTX_JITTER_OFF;
+    const int sel = (H.has_mesh ? 4 : 0) | (H.has_secondary ? 2 : 0) | (jit ? 1 : 0);
+    switch (sel) {
+        case 0: split_frame<false, false, false>(k, L, npix, spp, chunk_records, fb, tot, threads); break;
+        case 1: split_frame<false, false, true>(k, L, npix, spp, chunk_records, fb, tot, threads); break;
+        case 2: split_frame<false, true, false>(k, L, npix, spp, chunk_records, fb, tot, threads); break;
+        case 3: split_frame<false, true, true>(k, L, npix, spp, chunk_records, fb, tot, threads); break;
+        case 4: split_frame<true, false, false>(k, L, npix, spp, chunk_records, fb, tot, threads); break;
+        case 5: split_frame<true, false, true>(k, L, npix, spp, chunk_records, fb, tot, threads); break;
+        case 6: split_frame<true, true, false>(k, L, npix, spp, chunk_records, fb, tot, threads); break;
+        case 7: split_frame<true, true, true>(k, L, npix, spp, chunk_records, fb, tot, threads); break;
+    }
+    if (counters)
+        for (int q = 0; q < RTX_COUNTERS; ++q) counters[q] = tot[q];
+    return RTX_OK;
 }
