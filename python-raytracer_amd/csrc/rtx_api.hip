@@ -1208,6 +1208,11 @@ bool use_spp_mode(int spp, bool ext) {
     return ext && spp >= lo;
 }
 
+bool kp_byval() {
+    const char* e = getenv("RTX_KP_BYVAL");
+    return e && e[0] == '1';
+}
+
 // Persistent-wave experiment (rtx_kernels.h RTX_PERSIST): $RTX_PERSIST = resident waves
 // per SIMD the grid is sized for (0 or unset: off).
 int persist_waves() {
@@ -1415,9 +1420,14 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
     // (RTX_RELOAD_RECORDS): baked, DepthOfField 4K slows 7.0 -> 9.8 ms.
     const bool one_sample = kp.n_dof * kp.n_aa * kp.n_times == 1;
     const std::string prelude = (!ext && !spp && one_sample && jit_bake_enabled()) ? baked : std::string();
+    // kp_byval (experiment, $RTX_KP_BYVAL=1): the frame parameters travel in the kernel
+    // arguments instead of behind a pointer (one dependent scalar load fewer per wave)
+    const bool byval = kp_byval();
     const std::string src = prelude + std::string("#include \"rtx_kernels.h\"\nextern \"C\" __global__ RTX_RENDER_BOUNDS(") +
-                            b(mesh) + ", " + b(sec) + ", " + b(ext) + ") void " + name + "(const rtx::KParams* "
-                            "__restrict__ P, const rtx::Launch L) {\n  rtx::" + (spp ? "render_body_spp<" : "render_body<") +
+                            b(mesh) + ", " + b(sec) + ", " + b(ext) + ") void " + name +
+                            (byval ? "(const rtx::KParams Pv, const rtx::Launch L) {\n  const rtx::KParams* P = &Pv;\n"
+                                   : "(const rtx::KParams* __restrict__ P, const rtx::Launch L) {\n") +
+                            "  rtx::" + (spp ? "render_body_spp<" : "render_body<") +
                             b(mesh) + ", " + b(sec) +
                             ", " + b(ext) + ", " + b(cnt) + ", " + b(jit) + ">(P, L);\n}\n";
     out.name = name;
@@ -1994,7 +2004,7 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
         rs.done = true;
     }
     if (rs.fn && jit_enabled()) {
-        void* args[] = {(void*)&kp, (void*)&L};
+        void* args[] = {kp_byval() ? (void*)&s->kp : (void*)&kp, (void*)&L};
         if (!spp_mode && persist_waves() > 0) {  // experiment: grid = resident wave slots
             int cus = 0;
             if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) == hipSuccess && cus > 0) {

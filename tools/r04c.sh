@@ -16,4 +16,12 @@ for rep in 1 2; do
     done
   done
 done
+for rep in 1 2; do
+  for c in tsp1080 mr1080 tm1080; do
+    for v in 0 1; do
+      RTX_KP_BYVAL=$v timeout -k 10 120 python bench.py --config $c --steps 100 --warmup 5 --no-cpu-baseline > $O/${c}_kv$v.$rep.json 2> $O/${c}_kv$v.$rep.err || { echo "FAIL $c kv$v"; tail -5 $O/${c}_kv$v.$rep.err; exit 1; }
+      python -c "import json;d=json.load(open('$O/${c}_kv$v.$rep.json'));print('$c byval=$v', d['frame_ms'], d['kernel'])"
+    done
+  done
+done
 bash tools/r04b.sh
