@@ -181,9 +181,10 @@ def cpu_baseline_native(cfg, budget_s, threads=None):
                       "threads (oracle/rtx_oracle.c, gcc -O2)" % (sample, frames, dt, P, P)}
 
 
-# Python-loop baseline: rows j = 0, R, 2R, ... (reference row index) of the full-width
-# frame; every row for the 1080p configs whose whole frame fits the budget.
-PY_ROW_STRIDE = {"tsp1080": 1, "mr1080": 1, "tm1080": 16, "dof4k": 270}
+# Python-loop baseline: rows j = j0, j0 + R, j0 + 2R, ... (reference row index) of the
+# full-width frame, (R, j0) per config; every row for the 1080p configs whose whole frame
+# fits the budget. NovelScene1 (CSG + textures, ~270 samples/s per process): its middle row.
+PY_ROW_STRIDE = {"tsp1080": (1, 0), "mr1080": (1, 0), "tm1080": (16, 0), "dof4k": (270, 0), "ns1": (1024, 512)}
 _PY = {}
 
 
@@ -220,8 +221,8 @@ def cpu_baseline(cfg, processes=None):
     _, res, _, _ = CONFIGS[cfg]
     W, H = res
     P = processes or cpu_threads()
-    stride = PY_ROW_STRIDE[cfg]
-    rows = list(range(0, H, stride))
+    stride, j0 = PY_ROW_STRIDE[cfg]
+    rows = list(range(j0, H, stride))
     with mp.get_context("fork").Pool(P, initializer=_py_init, initargs=(cfg,)) as pool:
         pool.map(_py_init, [cfg] * P)  # every worker built its scene before the clock starts
         t0 = time.perf_counter()
@@ -235,7 +236,8 @@ def cpu_baseline(cfg, processes=None):
     except (OSError, StopIteration):
         pass
     sample = "full %dx%d frame" % (W, H) if stride == 1 else \
-        "rows 0, %d, 2x%d, ... (%d of %d) of the %dx%d frame" % (stride, stride, len(rows), H, W, H)
+        "rows %s (%d of %d) of the %dx%d frame" % (", ".join(str(r) for r in rows[:3]) + (", ..." if len(rows) > 3 else ""),
+                                                   len(rows), H, W, H)
     return {"value": nsamp / dt / 1e6, "unit": "Mrays/s", "cores": P, "kind": "port",
             "sample": "%s, %d samples in %.1f s; %d processes, one np.array_split column strip each (as render.nu); "
                       "oracle/pyloop.py: the reference's per-sample Python loop, bit-identical to the C oracle; "
@@ -434,7 +436,7 @@ def main():
         # host baselines first, before this process touches the GPU (the Python loop forks)
         cpu["cpu_baseline"] = cpu_baseline(a.config)
         cpu["cpu_baseline_native"] = cpu_baseline_native(a.config, a.cpu_seconds)
-        if cpu["cpu_baseline"] is None:  # hierarchy/texture/large-mesh configs: C restatement only
+        if cpu["cpu_baseline"] is None:  # configs without a Python-loop sample: C restatement only
             cpu["cpu_baseline"] = cpu.pop("cpu_baseline_native")
     torch.cuda.set_device(local)
     use_dist = world > 1 or a.force_dist or a.pipeline

@@ -339,6 +339,7 @@ class OracleScene:
         self._keep.append(td)
         s.tex_data = td.ctypes.data_as(C.POINTER(C.c_ubyte))
         self.records = records
+        self.base_dir = base_dir
         self.s = s
         self.width, self.height = s.width, s.height
         self.n_samples = s.samples * s.dof_samples * (s.motion_samples + s.motion_final)

@@ -8,12 +8,15 @@ PyGLM's fp32 vector arithmetic done on numpy float32 scalars and Python's fp64 s
 as Python floats. tests/test_pyloop.py proves it bit-identical to the C oracle
 (oracle/rtx_oracle.c, itself pinned to the published renders).
 
-Scope: the flat scenes of the benchmark configs (spheres, planes with checkers, boxes,
-triangle meshes with their bounding volume, point / directional lights, mirror and
-refractive materials, motion blur, DOF / AA, replayed jitter). Hierarchies and textures
-raise NotImplementedError.
+Scope: every scene the oracle renders: spheres, planes with checkers, boxes, triangle
+meshes with their bounding volume, point / directional lights, mirror and refractive
+materials, motion blur, DOF / AA, replayed jitter, and (round 4) CSG hierarchies
+(provided/geometry/hierarchy.py, with GLM's float mat4 restated below) and plane / box
+textures (simple_geometry.py:150-173, :312-355).
 """
+import ctypes
 import math
+import os
 
 import numpy as np
 
@@ -85,6 +88,93 @@ def refract(i, n, eta):
     return sub(scale(i, eta), scale(n, eta * d + np.sqrt(k)))
 
 
+# ---------------------------------------------------------------- GLM mat4 (float)
+# m[column][row] of numpy float32 scalars, every operation in GLM 0.9.9's generic order
+# (PyGLM wraps it); cos / sin of the float angle are libm's cosf / sinf, as GLM calls them.
+_LIBM = ctypes.CDLL("libm.so.6")
+_LIBM.cosf.restype = _LIBM.sinf.restype = ctypes.c_float
+_LIBM.cosf.argtypes = _LIBM.sinf.argtypes = [ctypes.c_float]
+
+
+def m_identity():
+    return [[f32(1.0) if c == k else f32(0.0) for k in range(4)] for c in range(4)]
+
+
+def m_translate(m, v):
+    """glm.translate: column 3 = m0 v.x + m1 v.y + m2 v.z + m3."""
+    r = [list(col) for col in m]
+    r[3] = [((m[0][k] * v[0] + m[1][k] * v[1]) + m[2][k] * v[2]) + m[3][k] for k in range(4)]
+    return r
+
+
+def m_rotate(m, angle, v):
+    """glm.rotate(m, angle, axis)."""
+    c, s = f32(_LIBM.cosf(angle)), f32(_LIBM.sinf(angle))
+    a = normalize(v)
+    t = scale(a, f32(1.0) - c)
+    R = [[c + t[0] * a[0], t[0] * a[1] + s * a[2], t[0] * a[2] - s * a[1]],
+         [t[1] * a[0] - s * a[2], c + t[1] * a[1], t[1] * a[2] + s * a[0]],
+         [t[2] * a[0] + s * a[1], t[2] * a[1] - s * a[0], c + t[2] * a[2]]]
+    r = [[(m[0][k] * R[col][0] + m[1][k] * R[col][1]) + m[2][k] * R[col][2] for k in range(4)] for col in range(3)]
+    return r + [list(m[3])]
+
+
+def m_scale(m, v):
+    """glm.scale: columns 0-2 times v's components."""
+    return [[m[col][k] * v[col] for k in range(4)] for col in range(3)] + [list(m[3])]
+
+
+def m_inverse(m):
+    """glm.inverse (compute_inverse<4, 4>: cofactors, then one reciprocal of the determinant)."""
+    c00 = m[2][2] * m[3][3] - m[3][2] * m[2][3]
+    c02 = m[1][2] * m[3][3] - m[3][2] * m[1][3]
+    c03 = m[1][2] * m[2][3] - m[2][2] * m[1][3]
+    c04 = m[2][1] * m[3][3] - m[3][1] * m[2][3]
+    c06 = m[1][1] * m[3][3] - m[3][1] * m[1][3]
+    c07 = m[1][1] * m[2][3] - m[2][1] * m[1][3]
+    c08 = m[2][1] * m[3][2] - m[3][1] * m[2][2]
+    c10 = m[1][1] * m[3][2] - m[3][1] * m[1][2]
+    c11 = m[1][1] * m[2][2] - m[2][1] * m[1][2]
+    c12 = m[2][0] * m[3][3] - m[3][0] * m[2][3]
+    c14 = m[1][0] * m[3][3] - m[3][0] * m[1][3]
+    c15 = m[1][0] * m[2][3] - m[2][0] * m[1][3]
+    c16 = m[2][0] * m[3][2] - m[3][0] * m[2][2]
+    c18 = m[1][0] * m[3][2] - m[3][0] * m[1][2]
+    c19 = m[1][0] * m[2][2] - m[2][0] * m[1][2]
+    c20 = m[2][0] * m[3][1] - m[3][0] * m[2][1]
+    c22 = m[1][0] * m[3][1] - m[3][0] * m[1][1]
+    c23 = m[1][0] * m[2][1] - m[2][0] * m[1][1]
+    f0, f1, f2 = (c00, c00, c02, c03), (c04, c04, c06, c07), (c08, c08, c10, c11)
+    f3_, f4, f5 = (c12, c12, c14, c15), (c16, c16, c18, c19), (c20, c20, c22, c23)
+    v0 = (m[1][0], m[0][0], m[0][0], m[0][0])
+    v1 = (m[1][1], m[0][1], m[0][1], m[0][1])
+    v2 = (m[1][2], m[0][2], m[0][2], m[0][2])
+    v3 = (m[1][3], m[0][3], m[0][3], m[0][3])
+    sa, sb = (f32(1), f32(-1), f32(1), f32(-1)), (f32(-1), f32(1), f32(-1), f32(1))
+    inv = [[((v1[k] * f0[k] - v2[k] * f1[k]) + v3[k] * f2[k]) * sa[k] for k in range(4)],
+           [((v0[k] * f0[k] - v2[k] * f3_[k]) + v3[k] * f4[k]) * sb[k] for k in range(4)],
+           [((v0[k] * f1[k] - v1[k] * f3_[k]) + v3[k] * f5[k]) * sa[k] for k in range(4)],
+           [((v0[k] * f2[k] - v1[k] * f4[k]) + v2[k] * f5[k]) * sb[k] for k in range(4)]]
+    d0 = [m[0][k] * inv[k][0] for k in range(4)]
+    one_over = f32(1.0) / ((d0[0] + d0[1]) + (d0[2] + d0[3]))
+    return [[inv[c][k] * one_over for k in range(4)] for c in range(4)]
+
+
+def m_transpose(m):
+    return [[m[k][c] for k in range(4)] for c in range(4)]
+
+
+def m_vec4(m, v):
+    """mat4 * vec4: (m0 x + m1 y) + (m2 z + m3 w)."""
+    return [(m[0][k] * v[0] + m[1][k] * v[1]) + (m[2][k] * v[2] + m[3][k] * v[3]) for k in range(4)]
+
+
+def m_xform(m, p, w):
+    """glm.vec3(m * glm.vec4(p, w))."""
+    o = m_vec4(m, (p[0], p[1], p[2], f32(w)))
+    return (o[0], o[1], o[2])
+
+
 # ---------------------------------------------------------------- geometry (provided/geometry)
 class Hit:
     """geometry/__init__.py:15-35 Intersection(time, normal, position, mat)."""
@@ -131,12 +221,20 @@ class Sphere:
             return False
         return any(SPHERE_SHADOW_EPSILON < t < t_max for t in roots)
 
+    def is_inside(self, p, time):  # simple_geometry.py:74-80
+        c = self.center if self.speed is None else add(self.center, scale(self.speed, time))
+        return float(length(sub(p, c))) < self.radius
+
+    def get_material(self, p, time):  # Geometry.get_material
+        return self.mats[0]
+
 
 class Plane:
-    """simple_geometry.py:86-176 (no textures)."""
+    """simple_geometry.py:86-176."""
 
-    def __init__(self, point, normal, mats, speed):
+    def __init__(self, point, normal, mats, speed, texture=None, texture_scale=1.0):
         self.point, self.normal, self.mats, self.speed = point, normal, mats, speed
+        self.texture, self.texture_scale = texture, texture_scale
         n = normal
         if n in (V(0, 1, 0), V(0, -1, 0), V(0, 0, 1)):
             self.width_axis = V(1, 0, 0)
@@ -161,6 +259,26 @@ class Plane:
         x = float(dot(sub(p, pos), self.width_axis))
         z = float(dot(sub(p, pos), self.height_axis))
         return self.mats[(math.floor(float(pos[0]) - x) + math.floor(float(pos[2]) - z)) % 2]
+
+    def get_material(self, p, time):
+        return self.material(p, time)
+
+    def is_inside(self, p, time):  # Geometry.is_inside
+        return False
+
+    def get_diffuse(self, p, time):
+        """simple_geometry.py:150-173: the texel at the point projected on the plane (the
+        projection uses the unmoved point, the texel offsets the moved one)."""
+        if self.texture is None:
+            return self.material(p, time).diffuse
+        pos = self._pos(time)
+        q = sub(p, scale(self.normal, dot(sub(p, self.point), self.normal)))
+        tex = self.texture
+        h, w = tex.shape[0], tex.shape[1]
+        i = int((float(dot(sub(q, pos), self.width_axis)) * 1000.0 / self.texture_scale) % w)
+        j = int((float(dot(sub(q, pos), self.height_axis)) * 1000.0 / self.texture_scale) % h)
+        px = tex[j, i]
+        return V(int(px[0]) / 255, int(px[1]) / 255, int(px[2]) / 255)
 
     def intersect(self, o, d, time):
         pos = self._pos(time)
@@ -201,10 +319,48 @@ _AXES = (V(1, 0, 0), V(0, 1, 0), V(0, 0, 1))
 
 
 class AABB:
-    """simple_geometry.py:179-307 (no textures)."""
+    """simple_geometry.py:179-355."""
 
-    def __init__(self, minpos, maxpos, mats, speed):
+    def __init__(self, minpos, maxpos, mats, speed, texture=None):
         self.minpos, self.maxpos, self.mats, self.speed = minpos, maxpos, mats, speed
+        self.texture = texture
+
+    def is_inside(self, p, time):  # simple_geometry.py:296-307
+        mn, mx = self._box(time)
+        return all(float(mn[k]) < float(p[k]) < float(mx[k]) for k in range(3))
+
+    def get_material(self, p, time):
+        return self.mats[0]
+
+    def get_diffuse(self, p, time):
+        """simple_geometry.py:312-355: the face the point lies on (within 1e-4) picks the
+        texel; getpixel truncates the clamped float coordinates."""
+        if self.texture is None:
+            return self.mats[0].diffuse
+        mn, mx = self._box(time)
+        x = (float(p[0]) - float(mn[0])) / (float(mx[0]) - float(mn[0]))
+        y = (float(p[1]) - float(mn[1])) / (float(mx[1]) - float(mn[1]))
+        z = (float(p[2]) - float(mn[2])) / (float(mx[2]) - float(mn[2]))
+        tex = self.texture
+        h, w = tex.shape[0], tex.shape[1]
+        if abs(p[0] - mn[0]) < EPSILON:
+            i, j = z * w, (1 - y) * h
+        elif abs(p[0] - mx[0]) < EPSILON:
+            i, j = (1 - z) * w, (1 - y) * h
+        elif abs(p[1] - mn[1]) < EPSILON:
+            i, j = x * w, (1 - z) * h
+        elif abs(p[1] - mx[1]) < EPSILON:
+            i, j = x * w, z * h
+        elif abs(p[2] - mn[2]) < EPSILON:
+            i, j = (1 - x) * w, (1 - y) * h
+        elif abs(p[2] - mx[2]) < EPSILON:
+            i, j = x * w, (1 - y) * h
+        else:
+            i, j = 0, 0
+        i = min(max(0, i), w - 1)
+        j = min(max(0, j), h - 1)
+        px = tex[int(j), int(i)]
+        return V(int(px[0]) / 255, int(px[1]) / 255, int(px[2]) / 255)
 
     def _box(self, time):
         if self.speed is None:
@@ -316,6 +472,96 @@ class Mesh:
         return False
 
 
+def _no_inside(self, p, time):  # Geometry.is_inside (meshes, hierarchy.py reads it)
+    return False
+
+
+def _first_material(self, p, time):  # Geometry.get_material
+    return self.mats[0]
+
+
+Mesh.is_inside = _no_inside
+Mesh.get_material = _first_material
+
+
+class Hierarchy:
+    """hierarchy.py:11-138: children in the node's frame (Minv applied to rays and points
+    on the way down, M and transpose(Minv) to hit positions and normals on the way up)."""
+
+    def __init__(self, kind, trs, mats):
+        self.kind, self.mats, self.children = kind, mats, []
+        t, r, sc = V(*trs[0:3]), V(*trs[3:6]), V(*trs[6:9])
+        k = math.pi / 180.0  # glm.radians of a Python float: fp64, then the float angle
+        m = m_translate(m_identity(), t)
+        m = m_rotate(m, f32(float(r[0]) * k), V(1, 0, 0))
+        m = m_rotate(m, f32(float(r[1]) * k), V(0, 1, 0))
+        m = m_rotate(m, f32(float(r[2]) * k), V(0, 0, 1))
+        self.M = m_scale(m, sc)
+        self.Minv = m_inverse(self.M)
+        self.MinvT = m_transpose(self.Minv)
+
+    def intersect(self, o, d, time):
+        mo, md = m_xform(self.Minv, o, 1.0), m_xform(self.Minv, d, 0.0)
+        out = []
+        if self.kind == "union":
+            for c in self.children:
+                out += c.intersect(mo, md, time)
+        elif self.kind == "intersection":
+            for c in self.children:
+                for h in c.intersect(mo, md, time):
+                    if all(o2 is c or o2.is_inside(h.position, time) for o2 in self.children):
+                        out.append(h)
+        elif self.kind == "difference":
+            a, b = self.children[0], self.children[1]
+            ha, hb = a.intersect(mo, md, time), b.intersect(mo, md, time)
+            for h in ha:
+                if not b.is_inside(h.position, time):
+                    out.append(h)
+            for h in hb:
+                if a.is_inside(h.position, time):
+                    h.mat = a.get_material(h.position, time)
+                    h.normal = neg(h.normal)
+                    out.append(h)
+        for h in out:
+            if h.mat is None:
+                h.mat = self.mats[0]  # IndexError without materials, as the reference
+            h.position = m_xform(self.M, h.position, 1.0)
+            v = m_vec4(self.MinvT, (h.normal[0], h.normal[1], h.normal[2], f32(0.0)))
+            inv = f32(1.0) / np.sqrt((v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]))
+            h.normal = (v[0] * inv, v[1] * inv, v[2] * inv)  # the vec4's w stays in the length
+        return out
+
+    def shadow_intersect(self, o, d, t_max, time):
+        mo, md = m_xform(self.Minv, o, 1.0), m_xform(self.Minv, d, 0.0)
+        if self.kind == "union":
+            return any(c.shadow_intersect(mo, md, t_max, time) for c in self.children)
+        if self.kind == "intersection":
+            return all(c.shadow_intersect(mo, md, t_max, time) for c in self.children)
+        if self.kind == "difference":
+            a, b = self.children[0], self.children[1]
+            if any(h.time > SHADOW_EPSILON and not b.is_inside(h.position, time) for h in a.intersect(mo, md, time)):
+                return True
+            return any(h.time > SHADOW_EPSILON and a.is_inside(h.position, time) for h in b.intersect(mo, md, time))
+        return False
+
+    def is_inside(self, p, time):
+        q = m_xform(self.Minv, p, 1.0)
+        if self.kind == "union":
+            return any(c.is_inside(q, time) for c in self.children)
+        if self.kind == "intersection":
+            return all(c.is_inside(q, time) for c in self.children)
+        if self.kind == "difference":
+            return self.children[0].is_inside(q, time) and not self.children[1].is_inside(q, time)
+        return False
+
+    def get_material(self, p, time):
+        q = m_xform(self.Minv, p, 1.0)
+        for c in self.children:
+            if c.is_inside(q, time):
+                return c.get_material(q, time)
+        return None
+
+
 def barycentric(p, a, b, c):
     """igl.barycentric_coordinates_tri on float32 rows (mesh.py:104-111), as the oracle
     restates it."""
@@ -363,29 +609,44 @@ class PyLoopScene:
             m.diffuse, m.specular, m.hardness = v(s.mat_diffuse, i), v(s.mat_specular, i), s.mat_hardness[i]
             m.kind, m.tint, m.refr_index = s.mat_type[i], s.mat_tint[i], s.mat_refr[i]
             self.mats.append(m)
-        self.objects = []
+        from . import oracle as _O
+        textures = {}
+        built = []
         for i, r in enumerate(osc.records):
-            if r["kind"] == "node" or s.obj_tex[i] >= 0:
-                raise NotImplementedError("pyloop: hierarchies and textures are not restated")
-            mats = [self.mats[s.obj_mat[4 * i + k]] for k in range(s.obj_nmat[i])]
+            mats = [self.mats[k] for k in r["mats"]]
             speed = v(s.obj_speed, i) if s.obj_has_speed[i] else None
             kind = r["kind"]
-            if kind == "sphere":
-                self.objects.append(Sphere(v(s.obj_a, i), s.obj_scalar[i], mats, speed))
+            tex = None
+            if s.obj_tex[i] >= 0:  # the oracle's scene-order texture list (Image.open + getpixel)
+                path = r["json"]["texture"]
+                if osc.base_dir is not None and not os.path.exists(path):
+                    path = os.path.join(osc.base_dir, path)
+                if path not in textures:
+                    textures[path] = _O._load_texture(path)
+                tex = textures[path]
+            if kind == "node":
+                g = Hierarchy(r["htype"] if r["htype"] in ("union", "intersection", "difference") else None,
+                              [s.node_trs[9 * i + k] for k in range(9)], mats)
+            elif kind == "sphere":
+                g = Sphere(v(s.obj_a, i), s.obj_scalar[i], mats, speed)
             elif kind == "plane":
-                self.objects.append(Plane(v(s.obj_a, i), v(s.obj_b, i), mats, speed))
+                g = Plane(v(s.obj_a, i), v(s.obj_b, i), mats, speed, tex, s.obj_tex_scale[i])
             elif kind == "box":
                 if s.obj_box_mode[i] == 0:
                     half = tuple(x / f32(2) for x in v(s.obj_b, i))  # dimension / 2
                     c = v(s.obj_a, i)
-                    self.objects.append(AABB(sub(c, half), add(c, half), mats, speed))
+                    g = AABB(sub(c, half), add(c, half), mats, speed, tex)
                 else:
-                    self.objects.append(AABB(v(s.obj_c, i), v(s.obj_b, i), mats, speed))
+                    g = AABB(v(s.obj_c, i), v(s.obj_b, i), mats, speed, tex)
             else:
                 vo, nv, fo, nf = s.mesh_vert_off[i], s.mesh_nverts[i], s.mesh_face_off[i], s.mesh_nfaces[i]
                 verts = [(s.verts[3 * k], s.verts[3 * k + 1], s.verts[3 * k + 2]) for k in range(vo, vo + nv)]
                 faces = [(s.faces[3 * k], s.faces[3 * k + 1], s.faces[3 * k + 2]) for k in range(fo, fo + nf)]
-                self.objects.append(Mesh(verts, faces, v(s.obj_a, i), s.obj_scalar[i], bool(s.obj_flat[i]), mats))
+                g = Mesh(verts, faces, v(s.obj_a, i), s.obj_scalar[i], bool(s.obj_flat[i]), mats)
+            built.append(g)
+            if r["parent"] >= 0:
+                built[r["parent"]].children.append(g)
+        self.objects = [g for g, r in zip(built, osc.records) if r["parent"] < 0]
         self.current_time = 0.0
         self.rays = 0
 
@@ -437,7 +698,9 @@ class PyLoopScene:
     def lighting(self, d, hit):
         colour = ZERO
         m = hit.mat
-        diffuse = m.diffuse
+        # scene.py:143-146: Plane / AABB hits (hierarchy leaves too) shade with get_diffuse
+        diffuse = hit.geom.get_diffuse(hit.position, self.current_time) if isinstance(hit.geom, (Plane, AABB)) \
+            else m.diffuse
         p, n = hit.position, hit.normal
         for kind, lcol, lvec, power in self.lights:
             if kind == 0:

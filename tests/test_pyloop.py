@@ -50,10 +50,21 @@ def test_pyloop_jitter_replay_and_row_subset():
     assert np.array_equal(part[:, [0, 5, 11]], full[:, [0, 5, 11]])
 
 
-def test_pyloop_refuses_hierarchies():
-    d, base = O.load_bundle("NovelScene1", resolution=[8, 4])
-    with pytest.raises(NotImplementedError):
-        P.PyLoopScene(O.OracleScene(d, base))
+@pytest.mark.parametrize("name,res", [("NovelScene1", (24, 12)), ("NovelScene2", (4, 2))])
+def test_pyloop_hierarchies_and_textures_equal_oracle(name, res):
+    """CSG hierarchies (GLM mat4 restated in Python floats) and plane / box textures."""
+    d, base = O.load_bundle(name, resolution=list(res), AA={"jitter": False, "samples": 1})
+    osc = O.OracleScene(d, base)
+    assert np.array_equal(P.PyLoopScene(osc).render(), osc.render())
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_pyloop_random_hierarchy_scenes_equal_oracle(seed):
+    import os
+    from scenegen import random_hier_scene
+    d = random_hier_scene(seed, res=(20, 15), mesh=(seed % 4 == 0))
+    osc = O.OracleScene(d, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets"))
+    assert np.array_equal(P.PyLoopScene(osc).render(), osc.render())
 
 
 def _config1_strip(k):

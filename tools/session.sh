@@ -13,6 +13,7 @@
 # pmc       rocprofv3 counter passes (FETCH_SIZE, WRITE_SIZE, instruction mix) per CONFIGS
 #           -> $OUT/pmc_<config>.json
 # rocprof   rocprofv3 --kernel-trace --stats of the default bench
+# rocprof_configs  the same for each of CONFIGS -> $OUT/<config>_kernel_stats.csv
 # pipeline  the multi-GPU frame loop over RCCL with one rank (PIPE_CONFIGS)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -59,6 +60,14 @@ for s in ${STEPS:-tests smoke bench rocprof}; do
     rocprof)
       step rocprof 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py \
         --steps 100 --warmup 10 --no-cpu-baseline || exit 1 ;;
+    rocprof_configs)  # rocprofv3 kernel statistics of each config's bench run
+      for c in $CFGS; do
+        st=100; [ $c = dof4k ] && st=10; [ $c = ns1 ] && st=10; [ $c = ns2 ] && st=3
+        step rocprof_$c 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$c" -o run --output-format csv -- python3 bench.py \
+          --config $c --steps $st --warmup 3 --no-cpu-baseline || exit 1
+        cp "$OUT/prof_$c/run_kernel_stats.csv" "$OUT/${c}_kernel_stats.csv" 2>/dev/null || \
+          find "$OUT/prof_$c" -name '*kernel_stats.csv' -exec cp {} "$OUT/${c}_kernel_stats.csv" \;
+      done ;;
     pipeline)
       for c in ${PIPE_CONFIGS:-tsp1080 dof4k}; do
         st=200; [ $c = dof4k ] && st=20
