@@ -1208,11 +1208,6 @@ bool use_spp_mode(int spp, bool ext) {
     return ext && spp >= lo;
 }
 
-bool kp_byval() {
-    const char* e = getenv("RTX_KP_BYVAL");
-    return e && e[0] == '1';
-}
-
 // Persistent-wave experiment (rtx_kernels.h RTX_PERSIST): $RTX_PERSIST = resident waves
 // per SIMD the grid is sized for (0 or unset: off).
 int persist_waves() {
@@ -1420,14 +1415,12 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
     // (RTX_RELOAD_RECORDS): baked, DepthOfField 4K slows 7.0 -> 9.8 ms.
     const bool one_sample = kp.n_dof * kp.n_aa * kp.n_times == 1;
     const std::string prelude = (!ext && !spp && one_sample && jit_bake_enabled()) ? baked : std::string();
-    // kp_byval (experiment, $RTX_KP_BYVAL=1): the frame parameters travel in the kernel
-    // arguments instead of behind a pointer (one dependent scalar load fewer per wave)
-    const bool byval = kp_byval();
+    // (The frame parameters stay behind a pointer: passed by value in the kernel arguments,
+    // one dependent scalar load fewer per wave, they measured equal on TSP/MR/TM,
+    // profiles/r04/kp_byval/.)
     const std::string src = prelude + std::string("#include \"rtx_kernels.h\"\nextern \"C\" __global__ RTX_RENDER_BOUNDS(") +
-                            b(mesh) + ", " + b(sec) + ", " + b(ext) + ") void " + name +
-                            (byval ? "(const rtx::KParams Pv, const rtx::Launch L) {\n  const rtx::KParams* P = &Pv;\n"
-                                   : "(const rtx::KParams* __restrict__ P, const rtx::Launch L) {\n") +
-                            "  rtx::" + (spp ? "render_body_spp<" : "render_body<") +
+                            b(mesh) + ", " + b(sec) + ", " + b(ext) + ") void " + name + "(const rtx::KParams* "
+                            "__restrict__ P, const rtx::Launch L) {\n  rtx::" + (spp ? "render_body_spp<" : "render_body<") +
                             b(mesh) + ", " + b(sec) +
                             ", " + b(ext) + ", " + b(cnt) + ", " + b(jit) + ">(P, L);\n}\n";
     out.name = name;
@@ -1909,10 +1902,12 @@ int launch_to_rgb8(const float* fb, uint8_t* out, int64_t n, hipStream_t st) {
     return RTX_OK;
 }
 
-// The hierarchy/texture scenes in three passes (rtx_split.h): RTX_SPLIT=1 (experiment).
+// The hierarchy/texture scenes in three passes (rtx_split.h), the default: NovelScene1
+// 2048x1024 AA32 25.8 -> 22.3 ms, NovelScene2 133.9 -> 98.1 ms (twice on one box,
+// profiles/r04/split/). RTX_SPLIT=0 launches the one-kernel form (render_body_spp).
 bool split_enabled() {
     const char* e = getenv("RTX_SPLIT");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
 }
 
 // Records per chunk ($RTX_SPLIT_RECORDS, default 2^26 = 4 GiB of 64-B records): a chunk
@@ -2004,7 +1999,7 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
         rs.done = true;
     }
     if (rs.fn && jit_enabled()) {
-        void* args[] = {kp_byval() ? (void*)&s->kp : (void*)&kp, (void*)&L};
+        void* args[] = {(void*)&kp, (void*)&L};
         if (!spp_mode && persist_waves() > 0) {  // experiment: grid = resident wave slots
             int cus = 0;
             if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) == hipSuccess && cus > 0) {

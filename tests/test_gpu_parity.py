@@ -342,6 +342,7 @@ def test_scene_specialized_kernel_equals_generic(name, res, edits, monkeypatch):
     really ran the kernel it is meant to (hierarchy/texture scenes specialize only under
     RTX_JIT_EXT=1, which this test sets)."""
     monkeypatch.setenv("RTX_JIT_EXT", "1")
+    monkeypatch.setenv("RTX_SPLIT", "0")  # the generic side: the one-kernel form
     sc = product_scene(name, res, **edits)
     cnt_a = torch.zeros(16, dtype=torch.int64, device="cuda")
     a = sc.render_device(counters=cnt_a).clone()
@@ -355,9 +356,9 @@ def test_scene_specialized_kernel_equals_generic(name, res, edits, monkeypatch):
 
 def test_default_flat_scenes_run_the_specialized_kernel():
     """The production path for flat scenes is the scene-specialized kernel (bench.py reports
-    its name); hierarchy/texture scenes run the precompiled generic kernel."""
+    its name); hierarchy/texture scenes run the split passes (csrc/rtx_split.h)."""
     for name, prefix in (("TwoSpheresPlane", "rtx_jit_render_00000"), ("TorusMesh", "rtx_jit_render_10000"),
-                         ("MirrorRefraction", "rtx_jit_render_01000"), ("NovelScene1", "k_render_ext_")):
+                         ("MirrorRefraction", "rtx_jit_render_01000"), ("NovelScene1", "k_split_")):
         sc = product_scene(name, (64, 32))
         sc.render_device()
         assert sc.last_kernel.startswith(prefix), (name, sc.last_kernel)
@@ -399,6 +400,7 @@ def test_sample_parallel_mapping_matches_oracle(name, res, edits, monkeypatch):
     NovelScene2's 240) vs the oracle: exact, i.e. the owner lanes' in-order LDS sums equal
     the reference's per-pixel accumulation."""
     monkeypatch.setenv("RTX_SPP", "1")
+    monkeypatch.setenv("RTX_SPLIT", "0")  # hierarchy scenes: the one-kernel form's mapping
     sc = product_scene(name, res, **edits)
     W, H = res
     fb = torch.full((H, W, 3), float("nan"), dtype=torch.float32, device="cuda")  # every pixel must be written
@@ -420,6 +422,7 @@ def test_sample_parallel_mapping_matches_oracle(name, res, edits, monkeypatch):
 def test_sample_parallel_equals_pixel_mapping(name, res, edits, rows, monkeypatch):
     """Both mappings on the production (Philox) jitter: identical framebuffers (bitwise)
     and ray counters, on row blocks that start mid-frame."""
+    monkeypatch.setenv("RTX_SPLIT", "0")  # hierarchy scenes: the one-kernel form's two mappings
     sc = product_scene(name, res, **edits)
     out = {}
     for mode in ("0", "1"):
