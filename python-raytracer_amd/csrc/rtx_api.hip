@@ -1362,6 +1362,7 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
     }
     if (uniform_hard >= 0) opts.push_back("-DRTX_FIXED_HARD=" + std::to_string(uniform_hard));
     if (!spp && persist_waves() > 0) opts.push_back("-DRTX_PERSIST=1");
+    if (!spp && kp.tile_perm != nullptr) opts.push_back("-DRTX_TILE_PERM=1");
     if (out8) opts.push_back("-DRTX_OUT8=1");  // uint8 framebuffer (rtx_render_rgb8)
     // secondary-ray frames keep their material index in a register: 3 LDS words per frame
     if (sec && v.n_mats <= 64) opts.push_back("-DRTX_FRAME_MATBITS=6");
@@ -1579,6 +1580,7 @@ struct rtx_scene {
     float* d_scratch = nullptr;
     size_t scratch_floats = 0;
     // the split hierarchy passes' shade-point records (rtx_split.h) and their counter
+    void* d_tile_perm = nullptr;  // RTX_TILE_PERM_FILE (experiment)
     ShadePt* d_split = nullptr;
     unsigned int* d_split_count = nullptr;
     int64_t split_cap = 0;
@@ -1605,6 +1607,8 @@ void free_camera(rtx_scene* s) {
     (void)hipFree(s->d_bounds_cam);
     s->d_bounds_cam = nullptr;
     (void)hipFree(s->d_kp);
+    (void)hipFree(s->d_tile_perm);
+    s->d_tile_perm = nullptr;
     s->d_xs = s->d_ys = s->d_dof = s->d_aa = s->d_times = s->d_noise = nullptr;
     s->d_kp = nullptr;
     s->cam_set = false;
@@ -1798,6 +1802,25 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     k.aa_o = (cptr<float>)s->d_aa; k.times = (cptr<float>)s->d_times; k.noise = (cptr<float>)s->d_noise;
     if (const char* e = getenv("RTX_WAVE_LOG_PTR"))  // tools/wave_timeline.py (RTX_WAVE_LOG kernels)
         k.wave_log = reinterpret_cast<unsigned long long*>((uintptr_t)strtoull(e, nullptr, 0));
+    if (const char* e = getenv("RTX_TILE_PERM_FILE")) {  // experiment: a tile dispatch order (int32 per tile)
+        const int64_t nt = (int64_t)((c->ncols + 7) / 8) * ((c->height + 7) / 8);
+        std::ifstream f(e, std::ios::binary);
+        std::vector<int32_t> perm((size_t)nt);
+        if (f && f.read(reinterpret_cast<char*>(perm.data()), nt * 4) && f.peek() == EOF) {
+            std::vector<char> seen((size_t)nt, 0);
+            bool ok = true;
+            for (int32_t t : perm) ok = ok && t >= 0 && t < nt && !seen[(size_t)t]++;
+            // padded to the whole-frame launch's waves (blocks of kBlock<false> / 64 waves;
+            // the padding waves keep their own, inactive, tiles)
+            const int64_t wpb = kBlock<false> / 64, nw = (nt + wpb - 1) / wpb * wpb;
+            for (int64_t w = nt; w < nw; ++w) perm.push_back((int32_t)w);
+            if (ok && (rc = upload(&s->d_tile_perm, perm)) == RTX_OK) {
+                k.tile_perm = (cptr<int32_t>)s->d_tile_perm;
+                k.tile_perm_n = (int32_t)nw;
+            }
+            if (rc) return rc;
+        }
+    }
     RTX_HIP(hipMalloc((void**)&s->d_kp, sizeof(KParams)));
     RTX_HIP(hipMemcpy(s->d_kp, &k, sizeof(KParams), hipMemcpyHostToDevice));
     s->kp = k;
@@ -1991,6 +2014,9 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
         while (T > 1 && std::gcd(m, T) != 1) ++m;
         L.perm = (uint32_t)(T > 1 ? m % T : 1);
         L.pix0 = 0;
+        L.tperm = (s->kp.tile_perm != nullptr && L.row0 == 0 && L.nrows == s->kp.height && L.gstride == 0 &&
+                   (int64_t)nblocks * (blk / 64) == s->kp.tile_perm_n) ? 1 : 0;
+        L.pad1 = 0;
     }
     rtx_scene::Resolved& rs = s->resolved[(out8 ? 8 : 0) | (cnt ? 4 : 0) | (jit ? 2 : 0) | (spp_mode ? 1 : 0)];
     if (!rs.done) {

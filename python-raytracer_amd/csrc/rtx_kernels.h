@@ -31,6 +31,10 @@ struct KParams {
     // tools/wave_timeline.py only (kernels built with RTX_WAVE_LOG): per wave, its start
     // and end (s_memrealtime, 100 MHz) and hardware ids, 4 x uint64 per wave of the launch
     unsigned long long* wave_log;
+    // dispatch order of a whole frame's 8x8 tiles (RTX_TILE_PERM kernels): wave w renders
+    // tile tile_perm[w]; n entries
+    cptr<int32_t> tile_perm;
+    int32_t tile_perm_n, pad3;
 };
 
 template <bool COUNT>
@@ -276,6 +280,8 @@ struct Launch {
     int64_t fstride;
     uint32_t perm;  // RTX_TILE_ORDER 2: the wave permutation's multiplier
     int32_t pix0;   // split hierarchy passes (rtx_split.h): the chunk's first pixel of the block
+    int32_t tperm;  // RTX_TILE_PERM kernels: 1 = this launch is a whole frame, dispatch by P.tile_perm
+    int32_t pad1;
 };
 
 // This block's framebuffer (frame blockIdx.y of a batched launch; the only frame otherwise).
@@ -337,11 +343,18 @@ struct PixelRC {
 #ifndef RTX_TILE_ORDER
 #define RTX_TILE_ORDER 0
 #endif
-__device__ __forceinline__ PixelRC pixel_rc(int32_t ncols, int sub, uint32_t perm = 1) {
+// Tile dispatch order from a table (experiment, scene-specialized kernels of cameras with
+// a tile_perm: RTX_TILE_PERM_FILE): whole-frame launches render tile tile_perm[wave].
+#ifndef RTX_TILE_PERM
+#define RTX_TILE_PERM 0
+#endif
+__device__ __forceinline__ PixelRC pixel_rc(int32_t ncols, int sub, uint32_t perm = 1,
+                                            const int32_t RTX_CONST* tperm = nullptr) {
     const int lane = threadIdx.x & 63;
     int wave = __builtin_amdgcn_readfirstlane(
         (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RTX_PPL + sub));
     const uint32_t T = gridDim.x * (blockDim.x >> 6) * RTX_PPL;
+    if (RTX_TILE_PERM && tperm != nullptr) wave = tperm[wave];
     if (RTX_TILE_ORDER == 1) wave = (int)T - 1 - wave;
     if (RTX_TILE_ORDER == 2) wave = (int)(((uint64_t)(uint32_t)wave * perm) % T);
     if (RTX_TILE == 0) {
@@ -467,7 +480,11 @@ __device__ __forceinline__ void render_body(const KParams* __restrict__ Pp, cons
         const PixelRC px{ty * 8 + (lane >> 3), tx * 8 + (lane & 7)};
 #else
     for (int sub = 0; sub < RTX_PPL; ++sub) {
+#if RTX_TILE_PERM
+        const PixelRC px = pixel_rc(ncols, sub, L.perm, L.tperm ? Pp->tile_perm : nullptr);
+#else
         const PixelRC px = pixel_rc(ncols, sub, L.perm);
+#endif
 #endif
         const bool active = px.r < L.nrows && px.c < ncols;
         any_active = any_active || active;

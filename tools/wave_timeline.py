@@ -20,6 +20,7 @@ p = argparse.ArgumentParser()
 p.add_argument("--config", default="tsp1080")
 p.add_argument("--frames", type=int, default=2000)
 p.add_argument("--json", default=None)
+p.add_argument("--npz", default=None, help="per-wave start/end (us) and hardware ids, for schedule simulations")
 a = p.parse_args()
 os.environ["RTX_JIT_FLAGS"] = (os.environ.get("RTX_JIT_FLAGS", "") + " -DRTX_WAVE_LOG=1").strip()
 torch.cuda.set_device(0)
@@ -76,6 +77,10 @@ out = {
     "start_profile_us": [round(float(np.percentile(s, q)), 3) for q in (1, 10, 25, 50, 75, 90, 99, 100)],
 }
 print(json.dumps(out))
+if a.npz:
+    np.savez_compressed(a.npz, start_us=s.astype(np.float32), end_us=e.astype(np.float32), xcc=xc.astype(np.int8),
+                        se=se.astype(np.int8), cu=cu.astype(np.int8), simd=simd.astype(np.int8),
+                        tiles_x=np.int32((W + 7) // 8))
 if a.json:
     with open(a.json, "w") as f:
         json.dump(out, f, indent=1)
