@@ -1215,6 +1215,12 @@ int persist_waves() {
     return (e && *e) ? std::max(0, atoi(e)) : 0;
 }
 
+// The measured tile schedule (tile_schedule); $RTX_TILE_SCHED=0: off.
+bool tile_sched_enabled() {
+    const char* e = getenv("RTX_TILE_SCHED");
+    return !(e && e[0] == '0');
+}
+
 bool jit_enabled() {
     const char* e = getenv("RTX_JIT");
     return !(e && e[0] == '0');
@@ -1362,7 +1368,7 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
     }
     if (uniform_hard >= 0) opts.push_back("-DRTX_FIXED_HARD=" + std::to_string(uniform_hard));
     if (!spp && persist_waves() > 0) opts.push_back("-DRTX_PERSIST=1");
-    if (!spp && kp.tile_perm != nullptr) opts.push_back("-DRTX_TILE_PERM=1");
+    if (!spp && !ext && kp.tile_time != nullptr) opts.push_back("-DRTX_TILE_SCHED=1");
     if (out8) opts.push_back("-DRTX_OUT8=1");  // uint8 framebuffer (rtx_render_rgb8)
     // secondary-ray frames keep their material index in a register: 3 LDS words per frame
     if (sec && v.n_mats <= 64) opts.push_back("-DRTX_FRAME_MATBITS=6");
@@ -1580,7 +1586,12 @@ struct rtx_scene {
     float* d_scratch = nullptr;
     size_t scratch_floats = 0;
     // the split hierarchy passes' shade-point records (rtx_split.h) and their counter
-    void* d_tile_perm = nullptr;  // RTX_TILE_PERM_FILE (experiment)
+    // the measured tile schedule (tile_schedule): dispatch order and wave durations of a
+    // whole frame's tiles; state 0 none, 1 measure the next whole frame, 2 sort, 3 ordered,
+    // 4 measured and left in row-major order
+    void* d_tile_perm = nullptr;
+    void* d_tile_time = nullptr;
+    int tile_sched = 0;
     ShadePt* d_split = nullptr;
     unsigned int* d_split_count = nullptr;
     int64_t split_cap = 0;
@@ -1608,7 +1619,10 @@ void free_camera(rtx_scene* s) {
     s->d_bounds_cam = nullptr;
     (void)hipFree(s->d_kp);
     (void)hipFree(s->d_tile_perm);
+    (void)hipFree(s->d_tile_time);
     s->d_tile_perm = nullptr;
+    s->d_tile_time = nullptr;
+    s->tile_sched = 0;
     s->d_xs = s->d_ys = s->d_dof = s->d_aa = s->d_times = s->d_noise = nullptr;
     s->d_kp = nullptr;
     s->cam_set = false;
@@ -1802,24 +1816,20 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     k.aa_o = (cptr<float>)s->d_aa; k.times = (cptr<float>)s->d_times; k.noise = (cptr<float>)s->d_noise;
     if (const char* e = getenv("RTX_WAVE_LOG_PTR"))  // tools/wave_timeline.py (RTX_WAVE_LOG kernels)
         k.wave_log = reinterpret_cast<unsigned long long*>((uintptr_t)strtoull(e, nullptr, 0));
-    if (const char* e = getenv("RTX_TILE_PERM_FILE")) {  // experiment: a tile dispatch order (int32 per tile)
+    if (tile_sched_enabled() && !s->has_ext && (s->has_secondary || s->has_mesh)) {
+        // the measured tile schedule (tile_schedule): identity order until measured
+        const int64_t wpb = kBlock<false> / 64;
         const int64_t nt = (int64_t)((c->ncols + 7) / 8) * ((c->height + 7) / 8);
-        std::ifstream f(e, std::ios::binary);
-        std::vector<int32_t> perm((size_t)nt);
-        if (f && f.read(reinterpret_cast<char*>(perm.data()), nt * 4) && f.peek() == EOF) {
-            std::vector<char> seen((size_t)nt, 0);
-            bool ok = true;
-            for (int32_t t : perm) ok = ok && t >= 0 && t < nt && !seen[(size_t)t]++;
-            // padded to the whole-frame launch's waves (blocks of kBlock<false> / 64 waves;
-            // the padding waves keep their own, inactive, tiles)
-            const int64_t wpb = kBlock<false> / 64, nw = (nt + wpb - 1) / wpb * wpb;
-            for (int64_t w = nt; w < nw; ++w) perm.push_back((int32_t)w);
-            if (ok && (rc = upload(&s->d_tile_perm, perm)) == RTX_OK) {
-                k.tile_perm = (cptr<int32_t>)s->d_tile_perm;
-                k.tile_perm_n = (int32_t)nw;
-            }
-            if (rc) return rc;
-        }
+        const int64_t nw = (nt + wpb - 1) / wpb * wpb;
+        std::vector<int32_t> ident((size_t)nw);
+        std::iota(ident.begin(), ident.end(), 0);
+        if ((rc = upload(&s->d_tile_perm, ident)) ||
+            (rc = upload(&s->d_tile_time, std::vector<uint32_t>((size_t)nw, 0u))))
+            return rc;
+        k.tile_perm = (cptr<int32_t>)s->d_tile_perm;
+        k.tile_time = reinterpret_cast<unsigned int*>(s->d_tile_time);
+        k.tile_n = (int32_t)nt;
+        s->tile_sched = 1;
     }
     RTX_HIP(hipMalloc((void**)&s->d_kp, sizeof(KParams)));
     RTX_HIP(hipMemcpy(s->d_kp, &k, sizeof(KParams), hipMemcpyHostToDevice));
@@ -1933,6 +1943,41 @@ bool split_enabled() {
     return !(e && e[0] == '0');
 }
 
+// The measured tile schedule ($RTX_TILE_SCHED=0: off). A frame's 8x8 tiles cost very
+// different amounts where some pixels follow long reflect/refract chains or cross a mesh
+// (MirrorRefraction 1080p: waves of 2 to 32 us; TorusMesh: 4 to 28 us), and a long wave
+// dispatched late sets the frame's end (profiles/r04/wave_timeline/). The first whole
+// frame after a camera upload records each wave's duration; before the next whole frame
+// the host sorts the tiles longest first (one stream synchronization per camera) and,
+// where the durations are heavy-tailed (max > 3 x mean), later frames dispatch in that
+// order (MirrorRefraction 41.4 -> 38.6 us, TorusMesh 52.8 -> 49.7 us with orders measured
+// on the same box, profiles/r04/tile_order/; TwoSpheresPlane and DepthOfField gain
+// nothing). The order changes when tiles run, not what they compute.
+int tile_schedule(rtx_scene* s, hipStream_t st) {
+    if (s->tile_sched != 2) return RTX_OK;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return RTX_OK;
+    const int32_t n = s->kp.tile_n;
+    std::vector<uint32_t> t((size_t)n);
+    RTX_HIP(hipMemcpyAsync(t.data(), s->d_tile_time, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, st));
+    RTX_HIP(hipStreamSynchronize(st));
+    double sum = 0.0;
+    uint32_t mx = 0;
+    for (uint32_t v : t) { sum += v; mx = std::max(mx, v); }
+    const double mean = n > 0 ? sum / n : 0.0;
+    if (!(mean > 0.0) || (double)mx <= 3.0 * mean) {
+        s->tile_sched = 4;
+        return RTX_OK;
+    }
+    std::vector<int32_t> perm((size_t)n);
+    std::iota(perm.begin(), perm.end(), 0);
+    std::stable_sort(perm.begin(), perm.end(), [&](int32_t a, int32_t b) { return t[a] > t[b]; });
+    RTX_HIP(hipMemcpyAsync(s->d_tile_perm, perm.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
+    RTX_HIP(hipStreamSynchronize(st));  // (perm is a local: wait for the copy)
+    s->tile_sched = 3;
+    return RTX_OK;
+}
+
 // Records per chunk ($RTX_SPLIT_RECORDS, default 2^26 = 4 GiB of 64-B records): a chunk
 // takes as many whole pixels as fit when every sample fills every chain level.
 int64_t split_records() {
@@ -2014,9 +2059,8 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
         while (T > 1 && std::gcd(m, T) != 1) ++m;
         L.perm = (uint32_t)(T > 1 ? m % T : 1);
         L.pix0 = 0;
-        L.tperm = (s->kp.tile_perm != nullptr && L.row0 == 0 && L.nrows == s->kp.height && L.gstride == 0 &&
-                   (int64_t)nblocks * (blk / 64) == s->kp.tile_perm_n) ? 1 : 0;
-        L.pad1 = 0;
+        L.tperm = 0;
+        L.tlog = 0;
     }
     rtx_scene::Resolved& rs = s->resolved[(out8 ? 8 : 0) | (cnt ? 4 : 0) | (jit ? 2 : 0) | (spp_mode ? 1 : 0)];
     if (!rs.done) {
@@ -2026,6 +2070,14 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
     }
     if (rs.fn && jit_enabled()) {
         void* args[] = {(void*)&kp, (void*)&L};
+        // whole-frame launches follow the measured tile schedule
+        const bool whole = s->tile_sched != 0 && !spp_mode && L.row0 == 0 && L.nrows == s->kp.height &&
+                           L.gstride == 0;
+        if (whole) {
+            if (int rc = tile_schedule(s, st)) return rc;
+            L.tlog = s->tile_sched == 1;
+            L.tperm = s->tile_sched == 3;
+        }
         if (!spp_mode && persist_waves() > 0) {  // experiment: grid = resident wave slots
             int cus = 0;
             if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) == hipSuccess && cus > 0) {
@@ -2035,7 +2087,8 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
         }
         RTX_HIP(hipModuleLaunchKernel(rs.fn, (unsigned)nblocks, (unsigned)nframes, 1, blk, 1, 1,
                                       s->has_ext ? (unsigned)(hbytes * blk) : 0u, st, args, nullptr));
-        s->last_kernel = rs.name;
+        if (L.tlog) s->tile_sched = 2;  // measured: sorted before the next whole frame
+        s->last_kernel = L.tperm ? rs.name + "+tiles" : rs.name;
         return RTX_OK;
     }
     if (out8 && nframes > 1) {  // generic kernels: the uint8 fallback below, one frame at a time

@@ -31,10 +31,12 @@ struct KParams {
     // tools/wave_timeline.py only (kernels built with RTX_WAVE_LOG): per wave, its start
     // and end (s_memrealtime, 100 MHz) and hardware ids, 4 x uint64 per wave of the launch
     unsigned long long* wave_log;
-    // dispatch order of a whole frame's 8x8 tiles (RTX_TILE_PERM kernels): wave w renders
-    // tile tile_perm[w]; n entries
+    // measured tile schedule (RTX_TILE_SCHED kernels, rtx_api.hip tile_schedule): the
+    // dispatch order of a whole frame's 8x8 tiles (wave w renders tile tile_perm[w]) and,
+    // while it is measured, each tile's wave duration (s_memrealtime ticks); tile_n entries
     cptr<int32_t> tile_perm;
-    int32_t tile_perm_n, pad3;
+    unsigned int* tile_time;
+    int32_t tile_n, pad3;
 };
 
 template <bool COUNT>
@@ -280,8 +282,8 @@ struct Launch {
     int64_t fstride;
     uint32_t perm;  // RTX_TILE_ORDER 2: the wave permutation's multiplier
     int32_t pix0;   // split hierarchy passes (rtx_split.h): the chunk's first pixel of the block
-    int32_t tperm;  // RTX_TILE_PERM kernels: 1 = this launch is a whole frame, dispatch by P.tile_perm
-    int32_t pad1;
+    int32_t tperm;  // RTX_TILE_SCHED kernels: 1 = dispatch a whole frame's tiles by P.tile_perm
+    int32_t tlog;   // RTX_TILE_SCHED kernels: 1 = record each wave's duration in P.tile_time
 };
 
 // This block's framebuffer (frame blockIdx.y of a batched launch; the only frame otherwise).
@@ -343,18 +345,20 @@ struct PixelRC {
 #ifndef RTX_TILE_ORDER
 #define RTX_TILE_ORDER 0
 #endif
-// Tile dispatch order from a table (experiment, scene-specialized kernels of cameras with
-// a tile_perm: RTX_TILE_PERM_FILE): whole-frame launches render tile tile_perm[wave].
-#ifndef RTX_TILE_PERM
-#define RTX_TILE_PERM 0
+// Measured tile schedule (scene-specialized kernels of scenes with secondary rays or
+// meshes, rtx_api.hip tile_schedule): whole-frame launches can dispatch the tiles in a
+// table's order (longest measured first) and record each wave's duration.
+#ifndef RTX_TILE_SCHED
+#define RTX_TILE_SCHED 0
 #endif
 __device__ __forceinline__ PixelRC pixel_rc(int32_t ncols, int sub, uint32_t perm = 1,
-                                            const int32_t RTX_CONST* tperm = nullptr) {
+                                            const int32_t RTX_CONST* tperm = nullptr, int* tile = nullptr) {
     const int lane = threadIdx.x & 63;
     int wave = __builtin_amdgcn_readfirstlane(
         (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RTX_PPL + sub));
     const uint32_t T = gridDim.x * (blockDim.x >> 6) * RTX_PPL;
-    if (RTX_TILE_PERM && tperm != nullptr) wave = tperm[wave];
+    if (RTX_TILE_SCHED && tperm != nullptr) wave = tperm[wave];
+    if (tile) *tile = wave;
     if (RTX_TILE_ORDER == 1) wave = (int)T - 1 - wave;
     if (RTX_TILE_ORDER == 2) wave = (int)(((uint64_t)(uint32_t)wave * perm) % T);
     if (RTX_TILE == 0) {
@@ -479,9 +483,14 @@ __device__ __forceinline__ void render_body(const KParams* __restrict__ Pp, cons
         const int ty = w / tiles_x, tx = w - ty * tiles_x;
         const PixelRC px{ty * 8 + (lane >> 3), tx * 8 + (lane & 7)};
 #else
+#if RTX_TILE_SCHED && defined(__HIP_DEVICE_COMPILE__)
+    static_assert(RTX_TILE == 1 && RTX_PPL == 1, "the tile schedule orders whole 8x8 tiles");
+    const unsigned long long tclk0 = L.tlog ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    int tile = 0;
+#endif
     for (int sub = 0; sub < RTX_PPL; ++sub) {
-#if RTX_TILE_PERM
-        const PixelRC px = pixel_rc(ncols, sub, L.perm, L.tperm ? Pp->tile_perm : nullptr);
+#if RTX_TILE_SCHED && defined(__HIP_DEVICE_COMPILE__)
+        const PixelRC px = pixel_rc(ncols, sub, L.perm, L.tperm ? Pp->tile_perm : nullptr, &tile);
 #else
         const PixelRC px = pixel_rc(ncols, sub, L.perm);
 #endif
@@ -495,6 +504,10 @@ __device__ __forceinline__ void render_body(const KParams* __restrict__ Pp, cons
             render_pixel<MESH, SEC, X, COUNT, JIT>(*Pp, frame_fb(L), image_row(L, px.r) - px.r, px.r, px.c, tl, fs, hs, bin);
     }
     flush_tally<COUNT>(tl, L.counters, any_active);
+#if RTX_TILE_SCHED && defined(__HIP_DEVICE_COMPILE__) && !RTX_PERSIST
+    if (L.tlog && (threadIdx.x & 63) == 0 && tile < Pp->tile_n)
+        Pp->tile_time[tile] = (unsigned int)(__builtin_amdgcn_s_memrealtime() - tclk0);
+#endif
     RTX_WAVE_CLOCK_END
 }
 

@@ -541,3 +541,23 @@ extern "C" int rtx_hostemu_render_split(const rtx_scene_desc* sd, const rtx_came
         for (int q = 0; q < RTX_COUNTERS; ++q) counters[q] = tot[q];
     return RTX_OK;
 }
+
+// The primary-ray bins rtx_camera_set builds for a camera (rtx_api.hip primary_bins): per
+// 8x8 tile its sphere/box mask and its number of candidate mesh faces. Returns the number
+// of bins (0: the camera has none).
+extern "C" int64_t rtx_hostemu_bins(const rtx_scene_desc* sd, const rtx_camera_desc* cd, uint32_t* mask,
+                                    int32_t* nfaces, int64_t cap) {
+    HostScene H;
+    if (convert_scene(sd, H)) return -1;
+    std::vector<int32_t> bstart, bfaces;
+    std::vector<float> bz;
+    std::vector<uint32_t> bmask;
+    int32_t bins_x = 0, mesh_bins = 0;
+    if (!primary_bins(H, cd, bstart, bfaces, bz, bmask, bins_x, mesh_bins)) return 0;
+    const int64_t n = (int64_t)bmask.size();
+    for (int64_t b = 0; b < n && b < cap; ++b) {
+        mask[b] = bmask[b];
+        nfaces[b] = mesh_bins && b + 1 < (int64_t)bstart.size() ? bstart[b + 1] - bstart[b] : 0;
+    }
+    return n;
+}
