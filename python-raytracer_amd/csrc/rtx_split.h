@@ -244,6 +244,7 @@ __device__ __forceinline__ void split_shadow(const KParams* __restrict__ Pp, con
     extern __shared__ float hstack[];
     const HStack hs{hstack + threadIdx.x, B};
     Tally tl = {};
+    const SceneView S = Pp->S;
     const int64_t n = sb.nsamp + (int64_t)*sb.count;
     bool any = false;
     for (int64_t r = (int64_t)blockIdx.x * B + threadIdx.x; r - (int64_t)threadIdx.x < n;
@@ -251,7 +252,7 @@ __device__ __forceinline__ void split_shadow(const KParams* __restrict__ Pp, con
         const bool hit = r < n && (sb.rec[r].flags & kSpHit);
         if (!RTX_ANY(hit)) continue;
         any = true;
-        if (hit) sb.rec[r].occ = shadow_record<MESH, COUNT>(Pp->S, sb.rec[r], tl, hs);
+        if (hit) sb.rec[r].occ = shadow_record<MESH, COUNT>(S, sb.rec[r], tl, hs);
     }
     flush_tally<COUNT>(tl, L.counters, any);
 }

@@ -997,7 +997,9 @@ RTX_HD f3 box_normal(int label, f3 d) {
 // Spheres, planes and boxes emit through ONE call site (a loop over their <= 2 hits), so
 // the walk-up the caller's emit inlines is compiled once per leaf_hits, not once per hit
 // kind.
-template <bool MESH, class O, class Emit>
+// SURF = false (shadow enumerations, diff_shadow): the hit's normal and material are not
+// needed, so they are not computed (emit receives zeros and -1).
+template <bool MESH, class O, class Emit, bool SURF = true>
 RTX_HD void leaf_hits(const SceneView& S, const O& ob, f3 o, f3 d, float time, Emit&& emit) {
     double th[2];
     int nh = 0;
@@ -1038,7 +1040,8 @@ RTX_HD void leaf_hits(const SceneView& S, const O& ob, f3 o, f3 d, float time, E
             const f3 p = get_point(o, d, t);
             if (dot(cross(ld3(T.e01), sub(p, v0)), n) >= 0.0f && dot(cross(ld3(T.e12), sub(p, ld3(T.v1))), n) >= 0.0f &&
                 dot(cross(ld3(T.e20), sub(p, ld3(T.v2))), n) >= 0.0f)
-                emit(t, p, ob.flat ? n : smooth_normal(T, (DTriN)S.trins[ob.tri_begin + f], p), ob.mat0);
+                emit(t, p, !SURF ? n : ob.flat ? n : smooth_normal(T, (DTriN)S.trins[ob.tri_begin + f], p),
+                     SURF ? ob.mat0 : -1);
         }
         return;
     }
@@ -1047,8 +1050,8 @@ RTX_HD void leaf_hits(const SceneView& S, const O& ob, f3 o, f3 d, float time, E
         const double t = k ? th[1] : th[0];
         const f3 p = get_point(o, d, t);
         f3 nrm = nb;
-        if (ob.type == OBJ_SPHERE) nrm = normalize(sub(p, c));
-        emit(t, p, nrm, ob.type == OBJ_PLANE ? plane_material(ob, p, time) : ob.mat0);
+        if (SURF && ob.type == OBJ_SPHERE) nrm = normalize(sub(p, c));
+        emit(t, p, nrm, !SURF ? -1 : ob.type == OBJ_PLANE ? plane_material(ob, p, time) : ob.mat0);
     }
 }
 
@@ -1269,9 +1272,11 @@ RTX_HX int32_t get_material(const SceneView& S, const HStack& hs, int x, f3 p, f
 // hits outside child 1 and child-1 hits inside child 0 (material of child 0, normal
 // negated), then None materials fall back to the node's and position/normal move to the
 // parent frame (hierarchy.py:49-76). Returns false if a filter drops the hit.
+template <bool SURF = true>
 RTX_HX bool walk_up(const SceneView& S, const HStack& hs, int cur, int stop, float time, f3& pos, f3& n,
                     int32_t& mat) {
     while (cur != stop) {
+        cur = wave_uniform(cur);  // (a leaf's ancestors: the same in every lane)
         cref<DNodeHot> c = S.nodes[cur];
         const int a = c.parent;
         cref<DNodeHot> A = S.nodes[a];
@@ -1283,17 +1288,17 @@ RTX_HX bool walk_up(const SceneView& S, const HStack& hs, int cur, int stop, flo
             const bool keep = inter || c.cidx != 0;  // the is_inside answer that keeps the hit
             for (int j = inter ? c0 : (c.cidx == 0 ? c1 : c0); j < A.end; j = S.nodes[j].end) {
                 if (j == cur) continue;
-                if (is_inside(S, hs, j, pos, time) != keep) return false;
+                if (is_inside(S, hs, wave_uniform(j), pos, time) != keep) return false;
                 if (!inter) break;
             }
-            if (!inter && c.cidx != 0) {
+            if (SURF && !inter && c.cidx != 0) {
                 mat = get_material(S, hs, c0, pos, time);
                 n = neg(n);
             }
         }
-        if (mat < 0) mat = A.mat0 < 0 ? 0 : A.mat0;  // the reference raises IndexError for A.mat0 < 0
+        if (SURF && mat < 0) mat = A.mat0 < 0 ? 0 : A.mat0;  // the reference raises IndexError for A.mat0 < 0
         pos = xform(S.nmat[a].M, pos, 1.0f);
-        n = normal_xform(S.nmat[a].Minv, n);
+        if (SURF) n = normal_xform(S.nmat[a].Minv, n);
         cur = a;
     }
     return true;
@@ -1302,7 +1307,7 @@ RTX_HX bool walk_up(const SceneView& S, const HStack& hs, int cur, int stop, flo
 // Enumerates s.intersect(R[depth(s)]) in the reference's list order: want(t64) is asked
 // before a hit's filters run (t does not change on the way up), take(t64, position,
 // normal, material, leaf DObj) receives every surviving hit in the frame of s's parent.
-template <bool MESH, class Want, class Take, class Cap>
+template <bool MESH, class Want, class Take, class Cap, bool SURF = true>
 RTX_HD void hier_enum(const SceneView& S, const HStack& hs, int s, float time, Want& want, Take& take, Cap& cap) {
     // subtrees whose hit region the ray cannot meet before cap() are skipped (wave-uniform)
     auto culled = [&](int c, int32_t depth) {
@@ -1310,11 +1315,13 @@ RTX_HD void hier_enum(const SceneView& S, const HStack& hs, int s, float time, W
         hs.get_ray(depth, ro, rd);
         return !RTX_ANY(ray_meets(S.hbox[c].lo, S.hbox[c].hi, ro, rd, cap()));
     };
+    s = wave_uniform(s);
     cref<DNodeHot> root = S.nodes[s];
     if (culled(s, root.depth)) return;
     if (root.kind == HN_OTHER) return;  // unknown hierarchy_type: no hits
     // preorder from s itself (a leaf root is visited once), one leaf visit site
     for (int i = s; i < root.end;) {
+        i = wave_uniform(i);
         cref<DNodeHot> c = S.nodes[i];
         if (i != s) {
             if (c.pkind == HN_DIFF && c.cidx >= 2) { i = c.end; continue; }  // difference reads children 0, 1
@@ -1325,10 +1332,11 @@ RTX_HD void hier_enum(const SceneView& S, const HStack& hs, int s, float time, W
         hs.get_ray(c.depth, ro, rd);
         if (c.kind == HN_LEAF) {
             const int32_t obj = c.obj, li = i;
-            leaf_hits<MESH>(S, S.objs[obj], ro, rd, time, [&](double t, f3 pos, f3 n, int32_t mat) {
+            auto emit = [&](double t, f3 pos, f3 n, int32_t mat) {
                 if (!want(t)) return;
-                if (walk_up(S, hs, li, s, time, pos, n, mat)) take(t, pos, n, mat, obj);
-            });
+                if (walk_up<SURF>(S, hs, li, s, time, pos, n, mat)) take(t, pos, n, mat, obj);
+            };
+            leaf_hits<MESH, cref<DObj>, decltype(emit)&, SURF>(S, S.objs[obj], ro, rd, time, emit);
         } else {
             hs.put_ray(c.depth + 1, xform(S.nmat[i].Minv, ro, 1.0f), xform(S.nmat[i].Minv, rd, 0.0f));
         }
@@ -1340,6 +1348,7 @@ RTX_HD void hier_enum(const SceneView& S, const HStack& hs, int s, float time, W
 // the shadow epsilon that the other child does not veto; no t_max test.
 template <bool MESH>
 RTX_HD bool diff_shadow(const SceneView& S, const HStack& hs, int x, float time) {
+    x = wave_uniform(x);
     cref<DNodeHot> X = S.nodes[x];
     {
         f3 ro, rd;
@@ -1354,8 +1363,11 @@ RTX_HD bool diff_shadow(const SceneView& S, const HStack& hs, int x, float time)
 #pragma unroll 1
     for (int k = 0; k < 2; ++k) {
         const int mine = k ? c1 : c0, other = k ? c0 : c1;
-        auto take = [&](double, f3 pos, f3, int32_t, int32_t) { found = is_inside(S, hs, other, pos, time) == (k != 0); };
-        hier_enum<MESH>(S, hs, mine, time, want, take, cap);
+        auto take = [&](double, f3 pos, f3, int32_t, int32_t) {
+            found = is_inside(S, hs, wave_uniform(other), pos, time) == (k != 0);
+        };
+        // (a shadow needs where the hit is, not its normal or material)
+        hier_enum<MESH, decltype(want), decltype(take), decltype(cap), false>(S, hs, mine, time, want, take, cap);
     }
     return found;
 }
@@ -1369,6 +1381,10 @@ RTX_HD bool diff_shadow(const SceneView& S, const HStack& hs, int x, float time)
 #endif
 template <bool MESH>
 RTX_HY bool hier_shadow(const SceneView& S, const HStack& hs, int r, f3 o, f3 d, double t_max, float time) {
+    // the traversal state is wave-uniform by construction (every branch on it is a wave
+    // vote); readfirstlane says so to the compiler, which otherwise keeps node indices in
+    // VGPRs and loads the node records per lane
+    r = wave_uniform(r);
     hs.put_ray(0, o, d);
     if (!RTX_ANY(ray_meets(S.sbox[r].lo, S.sbox[r].hi, o, d, INFINITY))) return false;
     cref<DNodeHot> R = S.nodes[r];
@@ -1404,6 +1420,7 @@ RTX_HY bool hier_shadow(const SceneView& S, const HStack& hs, int r, f3 o, f3 d,
             open = oparent;
             okind = Pn.kind; odepth = Pn.depth; oend = Pn.end; oparent = Pn.parent; ocidx = Pn.cidx;
         }
+        i = wave_uniform(i);
         cref<DNodeHot> c = S.nodes[i];
         if (hdecided(acc, okind, odepth, c.cidx)) { i = oend; continue; }
         bool live;
