@@ -39,7 +39,7 @@ struct alignas(16) ShadePt {
     int32_t next;   // the record of the child's hit, or -1 (black child / none)
     uint32_t flags; // kSpHit | kSpChain
     uint32_t occ;   // B: bit li = light li's shadow ray is occluded
-    int32_t pad;
+    int32_t prev;   // the parent's record (the hit whose reflect/refract ray this is), or -1
 };
 constexpr uint32_t kSpHit = 1u, kSpChain = 2u;
 
@@ -131,7 +131,7 @@ RTX_HD void trace_sample(const KParams& P, const Launch& L, const SplitBuf& sb, 
         r.next = -1;
         r.flags = kSpHit | (chain ? kSpChain : 0u);
         r.occ = 0u;
-        r.pad = 0;
+        r.prev = (int32_t)parent;
         sb.rec[slot] = r;
         if (!SEC || !chain || tir) return;
         in_shape = m.type == MAT_REFRACTIVE ? !in_shape : false;
@@ -165,38 +165,38 @@ RTX_HD uint32_t shadow_record(const SceneView& S, const ShadePt& R, Tally& tl, c
     return occm;
 }
 
-// Pass C for the sample whose level-0 record is r: the lighting of every record of its
-// chain (no ray traced) and the unwinding (cast_ray, scene.py:97-116).
-template <bool MESH, bool SEC>
-RTX_HD f3 shade_sample(const SceneView& S, const SplitBuf& sb, int64_t r, const FrameStack& fs) {
+// The lighting of one record (scene.py:140-187 with its occlusion mask; no ray traced).
+template <bool MESH>
+RTX_HD f3 record_lighting(const SceneView& S, const ShadePt& R, const DMat& m) {
     Tally tl = {};
     const HStack hs{nullptr, 1};
-    int nfr = 0;
+    const f3 pos = mk(R.pos[0], R.pos[1], R.pos[2]);
+    const f3 diffuse = R.gobj >= 0 ? get_diffuse(S, S.objs[R.gobj], pos, R.time) : ld3(m.diffuse);
+    return regular_lighting<MESH, true, false>(S, mk(R.d[0], R.d[1], R.d[2]), pos, mk(R.n[0], R.n[1], R.n[2]), m,
+                                               diffuse, R.time, tl, hs, (int64_t)R.occ);
+}
+
+// Pass C for the sample whose level-0 record is r: cast_ray's value (scene.py:97-116)
+// from its chain of records. The chain is walked to its deepest record by the `next`
+// links, then back up by the `prev` links, lighting each record on the way up and
+// blending it into the child's colour -- the unwinding order, with no frame stack.
+template <bool MESH, bool SEC>
+RTX_HD f3 shade_sample(const SceneView& S, const SplitBuf& sb, int64_t r) {
+    if (!(sb.rec[r].flags & kSpHit)) return mk(0.0f, 0.0f, 0.0f);  // miss -> black
+    if (SEC)
+        for (int32_t nx = sb.rec[r].next; nx >= 0; nx = sb.rec[r].next) r = nx;
+    // from the deepest record up: a diffuse hit ends the chain with its own clamped
+    // colour; a mirror / refractive one blends its lighting with its child's colour (black
+    // when the child ray was not traced or missed: TIR, the depth limit)
     f3 tail = mk(0.0f, 0.0f, 0.0f);
-    for (int level = 0; level < (SEC ? kMaxDepth : 1); ++level) {
-        const ShadePt R = sb.rec[r];
-        if (!(R.flags & kSpHit)) break;  // miss -> black
+    bool deepest = true;
+    for (int64_t p = r; p >= 0;) {
+        const ShadePt R = sb.rec[p];
         const DMat m = RTX_MAT(S, R.mat);
-        const f3 pos = mk(R.pos[0], R.pos[1], R.pos[2]);
-        const f3 diffuse = R.gobj >= 0 ? get_diffuse(S, S.objs[R.gobj], pos, R.time) : ld3(m.diffuse);
-        const f3 Lc = regular_lighting<MESH, true, false>(S, mk(R.d[0], R.d[1], R.d[2]), pos,
-                                                          mk(R.n[0], R.n[1], R.n[2]), m, diffuse, R.time, tl, hs,
-                                                          (int64_t)R.occ);
-        if (!SEC || !(R.flags & kSpChain)) {
-            tail = clamp01(Lc);
-            break;
-        }
-        fs.put(nfr++, Lc, R.mat);
-        if (R.next < 0) break;  // TIR, the depth limit or a missed child: black child
-        r = R.next;
-    }
-    if (SEC) {
-        for (int k = nfr - 1; k >= 0; --k) {
-            int32_t mi;
-            const f3 Lk = fs.get(k, mi);
-            const DMat m = RTX_MAT(S, mi);
-            tail = clamp01(add(scale(Lk, m.tint), scale(tail, m.omt)));
-        }
+        const f3 L = record_lighting<MESH>(S, R, m);
+        tail = (deepest && !(R.flags & kSpChain)) ? clamp01(L) : clamp01(add(scale(L, m.tint), scale(tail, m.omt)));
+        deepest = false;
+        p = SEC ? R.prev : -1;
     }
     return tail;
 }
@@ -267,9 +267,7 @@ __device__ __forceinline__ void split_shade(const KParams* __restrict__ Pp, cons
     const int PPB = spp_pixels_per_block(Sn, B);
     const int rounds = (PPB * Sn + B - 1) / B;
     const float rS = 1.0f / (float)Sn;  // (a block's samples < 2^22: udiv_small)
-    __shared__ float frames[SEC ? kFrameLds * kFrameWords * B : 1];
     __shared__ float sbuf[3 * B];
-    const FrameStack fs{frames + threadIdx.x, B};
     const int64_t npix = sb.nsamp / Sn;  // the chunk's pixels
     const int64_t pix0 = (int64_t)blockIdx.x * PPB;
     const int tid = threadIdx.x;
@@ -280,7 +278,7 @@ __device__ __forceinline__ void split_shade(const KParams* __restrict__ Pp, cons
         const int lp = udiv_small(flat, Sn, rS, s);
         const int64_t p = pix0 + lp;
         f3 c = mk(0.0f, 0.0f, 0.0f);
-        if (lp < PPB && p < npix) c = shade_sample<MESH, SEC>(P.S, sb, p * Sn + s, fs);
+        if (lp < PPB && p < npix) c = shade_sample<MESH, SEC>(P.S, sb, p * Sn + s);
         sbuf[tid] = c.x;
         sbuf[B + tid] = c.y;
         sbuf[2 * B + tid] = c.z;

@@ -479,12 +479,10 @@ static void split_frame(const KParams& k, const Launch& L0, int64_t npix, int sp
                 loc[RTX_CNT_SHADE] += tl.shade;
                 loc[RTX_CNT_TRI] += tl.tri;
             }
-            float frames[kMaxDepth * 4];
-            const FrameStack fs{frames, 1};
 #pragma omp for schedule(dynamic, 16)
             for (int64_t p = 0; p < np; ++p) {
                 f3 colour = mk(0.0f, 0.0f, 0.0f);
-                for (int s = 0; s < spp; ++s) colour = add(colour, shade_sample<MESH, SEC>(k.S, sb, p * spp + s, fs));
+                for (int s = 0; s < spp; ++s) colour = add(colour, shade_sample<MESH, SEC>(k.S, sb, p * spp + s));
                 const int64_t o = 3 * (p0 + p);
                 fb[o] = sample_mean(k, colour.x);
                 fb[o + 1] = sample_mean(k, colour.y);
