@@ -1215,6 +1215,12 @@ int persist_waves() {
     return (e && *e) ? std::max(0, atoi(e)) : 0;
 }
 
+// Host-computed origin terms of primary rays (RTX_PRIM_ORIGIN); $RTX_PRIM_ORIGIN=0: off.
+bool prim_origin_enabled() {
+    const char* e = getenv("RTX_PRIM_ORIGIN");
+    return !(e && e[0] == '0');
+}
+
 // The measured tile schedule (tile_schedule); $RTX_TILE_SCHED=0: off.
 bool tile_sched_enabled() {
     const char* e = getenv("RTX_TILE_SCHED");
@@ -1369,6 +1375,7 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
     if (uniform_hard >= 0) opts.push_back("-DRTX_FIXED_HARD=" + std::to_string(uniform_hard));
     if (!spp && persist_waves() > 0) opts.push_back("-DRTX_PERSIST=1");
     if (!spp && !ext && kp.tile_time != nullptr) opts.push_back("-DRTX_TILE_SCHED=1");
+    if (!spp && !ext && kp.po_valid) opts.push_back("-DRTX_PRIM_ORIGIN=1");
     if (out8) opts.push_back("-DRTX_OUT8=1");  // uint8 framebuffer (rtx_render_rgb8)
     // secondary-ray frames keep their material index in a register: 3 LDS words per frame
     if (sec && v.n_mats <= 64) opts.push_back("-DRTX_FRAME_MATBITS=6");
@@ -1816,6 +1823,27 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     k.aa_o = (cptr<float>)s->d_aa; k.times = (cptr<float>)s->d_times; k.noise = (cptr<float>)s->d_noise;
     if (const char* e = getenv("RTX_WAVE_LOG_PTR"))  // tools/wave_timeline.py (RTX_WAVE_LOG kernels)
         k.wave_log = reinterpret_cast<unsigned long long*>((uintptr_t)strtoull(e, nullptr, 0));
+    // one sample, no jitter, static scene: every primary ray starts at aa_o[0], so its
+    // origin-only plane and sphere terms are per-frame constants (closest_hit's fp32
+    // operations, here once; RTX_PRIM_ORIGIN kernels read them)
+    // (flat primary + shadow scenes: TwoSpheresPlane 24.09 -> 23.59 us, TorusMesh -0.6 %;
+    // MirrorRefraction measured 1 % slower with them, profiles/r04/prim_origin/)
+    if (c->n_dof == 1 && c->n_aa == 1 && c->jitter == RTX_JITTER_OFF && !s->traits.any_speed && !s->has_ext &&
+        !s->has_secondary && s->view.n_plane <= 4 && s->view.n_sphere <= 16 && prim_origin_enabled()) {
+        const f3 o = mk(c->aa_origins[0], c->aa_origins[1], c->aa_origins[2]);
+        int oi = 0;
+        for (int q = 0; q < s->view.n_plane; ++q, ++oi) {
+            const DObj& ob = s->h_bins.objs[oi];
+            k.po_pnum[q] = dot(sub(moved(ob, ob.a, 0.0f), o), ld3(ob.b));
+        }
+        for (int q = 0; q < s->view.n_sphere; ++q, ++oi) {
+            const DObj& ob = s->h_bins.objs[oi];
+            const f3 oc = sub(o, moved(ob, ob.a, 0.0f));
+            k.po_soc[q][0] = oc.x; k.po_soc[q][1] = oc.y; k.po_soc[q][2] = oc.z;
+            k.po_sq[q] = dot(oc, oc);
+        }
+        k.po_valid = 1;
+    }
     if (tile_sched_enabled() && !s->has_ext && (s->has_secondary || s->has_mesh)) {
         // the measured tile schedule (tile_schedule): identity order until measured
         const int64_t wpb = kBlock<false> / 64;

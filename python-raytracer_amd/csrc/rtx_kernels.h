@@ -36,7 +36,14 @@ struct KParams {
     // while it is measured, each tile's wave duration (s_memrealtime ticks); tile_n entries
     cptr<int32_t> tile_perm;
     unsigned int* tile_time;
-    int32_t tile_n, pad3;
+    int32_t tile_n;
+    // RTX_PRIM_ORIGIN kernels (one sample, no jitter, static scene: every primary ray starts
+    // at aa_o[0]): its origin-only plane and sphere terms, computed by rtx_camera_set with
+    // closest_hit's fp32 operations (po_valid: computed)
+    int32_t po_valid;
+    float po_pnum[4];
+    float po_soc[16][3];
+    float po_sq[16];
 };
 
 template <bool COUNT>
@@ -219,6 +226,19 @@ RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, 
         return;
     }
     const int j = P.height - 1 - (row0 + rr);  // reference row index (y grows upward)
+#if defined(RTX_PRIM_ORIGIN) && RTX_PRIM_ORIGIN && defined(RTX_FIXED_COUNTS)
+    OriginTerms prim;  // the primary rays' origin-only terms (host-computed)
+#pragma unroll
+    for (int k = 0; k < RTX_FIXED_NP; ++k) prim.pnum[k] = P.po_pnum[k];
+#pragma unroll
+    for (int k = 0; k < RTX_FIXED_NS; ++k) {
+        prim.soc[k] = ld3(P.po_soc[k]);
+        prim.sq[k] = P.po_sq[k];
+    }
+    const OriginTerms* primp = &prim;
+#else
+    const OriginTerms* primp = nullptr;
+#endif
     f3 colour = mk(0.0f, 0.0f, 0.0f);
     f3 jr_odd = mk(0.0f, 0.0f, 0.0f);  // the odd sample's jitter uniforms of the current pair
     // pinned counts must not unroll the loops (one cast_ray body per sample)
@@ -249,7 +269,7 @@ RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, 
 #pragma unroll 1
             for (int kt = 0; kt < RTX_NTIMES(P); ++kt)
                 colour = add(colour, cast_ray<MESH, SEC, X, COUNT>(sample_scene<X>(P.S), o, ddir, P.times[kt], tl, fs, hs,
-                                                                   bin));
+                                                                   bin, primp));
         }
     }
     colour = mk(sample_mean(P, colour.x), sample_mean(P, colour.y), sample_mean(P, colour.z));

@@ -1659,9 +1659,24 @@ __device__ __forceinline__ void coop_mesh(const SceneView& S, const DObj& ob, in
 }
 #endif
 
+// Origin-only terms of the plane and sphere shadow tests -- dot(p0 - o, n) per plane,
+// oc = o - c and dot(oc, oc) per sphere -- computed once per shading point and shared by
+// its lights (the same operations, once instead of per light). Scene-specialized kernels
+// only (fixed counts size the arrays); the generic kernels compute them per light.
+struct OriginTerms {
+#ifdef RTX_FIXED_COUNTS
+    float pnum[RTX_FIXED_NP > 0 ? RTX_FIXED_NP : 1];
+    f3 soc[RTX_FIXED_NS > 0 ? RTX_FIXED_NS : 1];
+    float sq[RTX_FIXED_NS > 0 ? RTX_FIXED_NS : 1];
+#endif
+};
+
 template <bool MESH, bool X, bool COUNT>
+// prim (primary rays of one-sample unjittered static cameras, RTX_PRIM_ORIGIN): the
+// origin-only terms of the planes and spheres, computed once on the host (rtx_camera_set,
+// the same fp32 operations) instead of in every wave.
 RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const HStack& hs, HHit& hh,
-                       int32_t bin = -1) {
+                       int32_t bin = -1, const OriginTerms* prim = nullptr) {
     Hit h{INFINITY, -1, 0};
     int oi = 0;
     for (int k = 0; k < RTX_NPLANE(S); ++k, ++oi) {  // simple_geometry.py:105-120
@@ -1669,7 +1684,11 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
         const DObj ob = S.objs[oi];
         const f3 n = ld3(ob.b);
         const float denom = dot(d, n);
+#ifdef RTX_FIXED_COUNTS
+        const float num = prim ? prim->pnum[k] : dot(sub(moved(ob, ob.a, time), o), n);
+#else
         const float num = dot(sub(moved(ob, ob.a, time), o), n);
+#endif
         const float t32 = num / denom;
         // abs(denom) > epsilon and t >= 0
         const bool valid = fabsf(denom) >= kEps4Up && quot_nonneg(t32, num, denom);
@@ -1690,9 +1709,16 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
         bool valid = false;
         float t32 = INFINITY;
         int32_t root = 0;
-        if (sphere_disc_sign(o, d, ctr, ob.r2f) >= 0) {  // fp64 only where a hit is possible
+#ifdef RTX_FIXED_COUNTS
+        const f3 oc = prim ? prim->soc[k] : sub(o, ctr);
+        const float q = prim ? prim->sq[k] : dot(oc, oc);
+#else
+        const f3 oc = sub(o, ctr);
+        const float q = dot(oc, oc);
+#endif
+        if (sphere_disc_sign_oc(d, oc, q, ob.r2f) >= 0) {  // fp64 only where a hit is possible
             double b, s, two_a;
-            if (sphere_roots(o, d, ctr, ob.r2, b, s, two_a)) {
+            if (RTX_ABLATE == 4 ? sphere_roots(o, d, ctr, ob.r2, b, s, two_a) : sphere_roots_oc(d, oc, q, ob.r2, b, s, two_a)) {
                 double t = (-b - s) / two_a;
                 const bool near = t > 0.0;
                 // the far root only where some lane needs it (a ray from inside the sphere)
@@ -1779,17 +1805,6 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
 }
 
 // ------------------------------------------------------------------ shadow any-hit
-// Origin-only terms of the plane and sphere shadow tests -- dot(p0 - o, n) per plane,
-// oc = o - c and dot(oc, oc) per sphere -- computed once per shading point and shared by
-// its lights (the same operations, once instead of per light). Scene-specialized kernels
-// only (fixed counts size the arrays); the generic kernels compute them per light.
-struct OriginTerms {
-#ifdef RTX_FIXED_COUNTS
-    float pnum[RTX_FIXED_NP > 0 ? RTX_FIXED_NP : 1];
-    f3 soc[RTX_FIXED_NS > 0 ? RTX_FIXED_NS : 1];
-    float sq[RTX_FIXED_NS > 0 ? RTX_FIXED_NS : 1];
-#endif
-};
 RTX_HD void origin_terms(const SceneView& S, f3 o, float time, OriginTerms& T) {
 #ifdef RTX_FIXED_COUNTS
     int oi = 0;
@@ -2244,7 +2259,7 @@ struct FrameStack {
 
 template <bool MESH, bool SEC, bool X, bool COUNT>
 RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const FrameStack& fs, const HStack& hs,
-                   int32_t bin = -1) {
+                   int32_t bin = -1, const OriginTerms* prim = nullptr) {
     int nfr = 0;
     uint64_t fmats = 0;  // RTX_FRAME_MATBITS: the frames' material indices
     f3 deep[kMaxDepth - kFrameLds > 0 ? kMaxDepth - kFrameLds : 1];  // frames kFrameLds.. (private)
@@ -2255,7 +2270,8 @@ RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const 
         if (COUNT) tl.cast[level]++;
         if (RTX_ABLATE == 8) { tail = d; break; }  // cost probe: camera + store only
         HHit hh;
-        const Hit h = closest_hit<MESH, X, COUNT>(S, o, d, time, tl, hs, hh, level == 0 ? bin : -1);
+        const Hit h = closest_hit<MESH, X, COUNT>(S, o, d, time, tl, hs, hh, level == 0 ? bin : -1,
+                                                  level == 0 ? prim : nullptr);
         if (h.obj == -1) break;  // miss -> black
         const Surface sf = resolve_hit<MESH, X>(S, h, hh, o, d, time);
         const DMat m = RTX_MAT(S, sf.mat);
