@@ -766,6 +766,12 @@ int convert_camera(const rtx_camera_desc* c, KParams& k) {
     return RTX_OK;
 }
 
+// $RTX_LENS_BINS=0: lens cameras get no primary-ray bins (experiment, A/B)
+bool lens_bins_disabled() {
+    const char* e = getenv("RTX_LENS_BINS");
+    return e && e[0] == '0';
+}
+
 // Primary-ray bins. With one sample per pixel, no lens (dof origin == camera position)
 // and no jitter, every primary ray leaves the same origin o (the AA origin, scene.py:60-61)
 // in the direction of x u + y v - d w (scene.py:54): a pinhole projection. An object whose
@@ -782,15 +788,47 @@ int convert_camera(const rtx_camera_desc* c, KParams& k) {
 //     nearest first, with a lower bound of their hit t (depth <= t).
 // Other tiles and secondary/shadow rays walk everything. Returns false when the camera
 // does not qualify, or a mesh face lies near or behind the origin's plane.
+//
+// Lens cameras (DOF samples, AA spreads, jitter: scene.py:56-65) get object bins from a
+// "thick" pinhole. Sample ray k of a pixel leaves S = aa_o + jitter toward the pixel's
+// focal point F = P + f bdir from its DOF origin D: X(l) = S + l (F - D). The pinhole ray
+// of the pixel from the camera position P is Y(l) = P + l (F - P), and
+//   X(l) - Y(l) = (S - D) + (1 - l) (D - P),  |X - Y| <= R1 + |1 - l| A,
+// with A = max |D - P| (the aperture spread) and R1 = max |aa_o - D| + jitter_scale. A hit
+// at depth z (along -w from P) has l = (z - (S - P).(-w)) / (F - D).(-w), where
+// (F - D).(-w) lies in [f cmin - A, f + A] (cmin: the smallest bdir.(-w) of the strip's
+// pixel table) and |(S - P).(-w)| <= A + R1: so l, and the deviation, are bounded by the
+// object's depth range. An object grown by that deviation contains a point of the
+// pinhole ray of every pixel some sample of which hits it, and its pinhole projection
+// from P bins the tile as above. The mesh faces keep no bins (their t lower bounds hold
+// for one origin only).
 bool primary_bins(const HostScene& H, const rtx_camera_desc* c, std::vector<int32_t>& start,
                   std::vector<int32_t>& faces, std::vector<float>& zmin, std::vector<uint32_t>& objmask,
                   int32_t& bins_x, int32_t& mesh_bins) {
-    if (c->n_dof != 1 || c->n_aa != 1 || c->jitter != RTX_JITTER_OFF) return false;
     if (c->ncols < 2 || c->height < 2) return false;
-    if (c->dof_origins[0] != c->position[0] || c->dof_origins[1] != c->position[1] ||
-        c->dof_origins[2] != c->position[2])
-        return false;
-    const double o[3] = {c->aa_origins[0], c->aa_origins[1], c->aa_origins[2]};
+    const bool pinhole = c->n_dof == 1 && c->n_aa == 1 && c->jitter == RTX_JITTER_OFF &&
+                         c->dof_origins[0] == c->position[0] && c->dof_origins[1] == c->position[1] &&
+                         c->dof_origins[2] == c->position[2];
+    if (!pinhole && lens_bins_disabled()) return false;
+    const double o[3] = {pinhole ? c->aa_origins[0] : c->position[0], pinhole ? c->aa_origins[1] : c->position[1],
+                         pinhole ? c->aa_origins[2] : c->position[2]};
+    double lensA = 0.0, lensR1 = 0.0;  // the lens bounds A and R1 (above)
+    if (!pinhole) {
+        for (int32_t kd = 0; kd < c->n_dof; ++kd) {
+            const float* D = c->dof_origins + 3 * kd;
+            double a2 = 0.0;
+            for (int a = 0; a < 3; ++a) a2 += ((double)D[a] - o[a]) * ((double)D[a] - o[a]);
+            lensA = std::max(lensA, std::sqrt(a2));
+            for (int32_t ka = 0; ka < c->n_aa; ++ka) {
+                const float* S = c->aa_origins + 3 * ((size_t)kd * c->n_aa + ka);
+                double r2 = 0.0;
+                for (int a = 0; a < 3; ++a) r2 += ((double)S[a] - D[a]) * ((double)S[a] - D[a]);
+                lensR1 = std::max(lensR1, std::sqrt(r2));
+            }
+        }
+        if (c->jitter != RTX_JITTER_OFF) lensR1 += std::fabs(c->jitter_scale) * (1.0 + 1e-5);
+        if (!std::isfinite(lensA) || !std::isfinite(lensR1)) return false;
+    }
     const int32_t W = c->ncols, Hh = c->height;
     const double dx = ((double)c->xs[W - 1] - (double)c->xs[0]) / (W - 1);
     const double dy = ((double)c->ys[Hh - 1] - (double)c->ys[0]) / (Hh - 1);
@@ -799,6 +837,22 @@ bool primary_bins(const HostScene& H, const rtx_camera_desc* c, std::vector<int3
         if (!(c->xs[i] > c->xs[i - 1])) return false;
     for (int32_t j = 1; j < Hh; ++j)
         if (!(c->ys[j] > c->ys[j - 1])) return false;
+    // lens cameras: the deviation bound R1 + |1 - l| A of a hit at depths [zlo, zhi], padded
+    // by 1e-5 of the magnitudes (the fp32 ray setup: origins, focal point, direction)
+    const double xm = std::max(std::fabs((double)c->xs[0]), std::fabs((double)c->xs[W - 1]));
+    const double ym = std::max(std::fabs((double)c->ys[0]), std::fabs((double)c->ys[Hh - 1]));
+    const double cmin = c->d / std::sqrt(xm * xm + ym * ym + c->d * c->d) * (1.0 - 1e-6);
+    const double f = c->focal_length, den_lo = f * cmin - lensA, den_hi = f + lensA;
+    const double omag = std::sqrt(o[0] * o[0] + o[1] * o[1] + o[2] * o[2]);
+    if (!pinhole && !(den_lo > 0.05 * f * cmin)) return false;  // aperture too wide for the bound
+    auto lens_pad = [&](double zlo, double zhi) {
+        if (pinhole) return 0.0;
+        const double R2 = lensA + lensR1, nlo = zlo - R2, nhi = zhi + R2;
+        const double lmin = nlo > 0.0 ? nlo / den_hi : 0.0;
+        const double lmax = nhi > 0.0 ? nhi / den_lo : 0.0;
+        const double m = std::max(std::fabs(1.0 - lmin), std::fabs(1.0 - lmax));
+        return (lensR1 + m * lensA) * (1.0 + 1e-5) + 1e-5 * (lmax * den_hi + omag + R2 + f);
+    };
     // fractional index of a screen coordinate in the camera's own (fp32) pixel table: the
     // rays use those very values, so no spacing estimate accumulates error across the image
     auto table_pos = [](const float* t, int32_t n, double x) {
@@ -862,9 +916,14 @@ bool primary_bins(const HostScene& H, const rtx_camera_desc* c, std::vector<int3
     for (int32_t k = 0; k < H.n_sphere; ++k) {
         const DObj& ob = H.objs[H.n_plane + k];
         const uint32_t bit = 1u << (k & 15);
-        double pts[8][3], lo[3], hi[3], oc2 = 0.0, z;
-        for (int a = 0; a < 3; ++a) oc2 += ((double)ob.a[a] - o[a]) * ((double)ob.a[a] - o[a]);
-        const double re = ob.radius + 0x1p-8 * (std::sqrt(oc2) + std::fabs(ob.radius));
+        double pts[8][3], lo[3], hi[3], oc2 = 0.0, zc = 0.0, z;
+        for (int a = 0; a < 3; ++a) {
+            oc2 += ((double)ob.a[a] - o[a]) * ((double)ob.a[a] - o[a]);
+            zc -= ((double)ob.a[a] - o[a]) * c->w[a];
+        }
+        // lens: every sample origin lies within A + R1 of o
+        const double re0 = ob.radius + 0x1p-8 * (std::sqrt(oc2) + lensA + lensR1 + std::fabs(ob.radius));
+        const double re = re0 + lens_pad(zc - re0, zc + re0);
         for (int a = 0; a < 3; ++a) { lo[a] = ob.a[a] - re; hi[a] = ob.a[a] + re; }
         box_corners(lo, hi, pts);
         Rect R;
@@ -881,6 +940,18 @@ bool primary_bins(const HostScene& H, const rtx_camera_desc* c, std::vector<int3
             hi[a] = std::max((double)ob.a[a], (double)ob.b[a]) + p;
         }
         box_corners(lo, hi, pts);
+        if (!pinhole) {  // grow by the lens deviation over the box's depth range
+            double zlo = INFINITY, zhi = -INFINITY;
+            for (int q = 0; q < 8; ++q) {
+                double zq = 0.0;
+                for (int a = 0; a < 3; ++a) zq -= (pts[q][a] - o[a]) * c->w[a];
+                zlo = std::min(zlo, zq);
+                zhi = std::max(zhi, zq);
+            }
+            const double g = lens_pad(zlo, zhi);
+            for (int a = 0; a < 3; ++a) { lo[a] -= g; hi[a] += g; }
+            box_corners(lo, hi, pts);
+        }
         Rect R;
         if (H.n_box > 16 || ob.has_speed || !rect_of(pts, 8, R, z)) R = all;
         mark(R, bit);
@@ -889,7 +960,7 @@ bool primary_bins(const HostScene& H, const rtx_camera_desc* c, std::vector<int3
     start.assign(nb + 1, 0);
     faces.clear();
     zmin.clear();
-    if (H.n_mesh != 1) return true;
+    if (H.n_mesh != 1 || !pinhole) return true;
     const DObj& m = H.objs[H.n_plane + H.n_sphere + H.n_box];
     std::vector<Rect> rects(m.tri_count);
     // A hit point P = o + t d (|d| = 1 up to rounding) has depth (P - o).(-w) <= t, and a

@@ -128,6 +128,25 @@ def occluded_light(scene, o, light, grids):
     return occ.astype(bool), cells
 
 
+def bins(scene, subimage=0, tasks=1):
+    """The primary-ray bins rtx_camera_set builds (rtx_api.hip primary_bins): the object
+    mask (uint32 [bins_y, bins_x]: spheres bits 0-15, boxes 16-31) and mesh-face count per
+    8x8 bin, or None when the camera has no bins."""
+    sd = scene.scene_desc()
+    cd, tables = scene.camera_desc(subimage, tasks)
+    bx, by = (cd.ncols + 7) // 8, (cd.height + 7) // 8
+    mask = np.zeros(bx * by, np.uint32)
+    nf = np.zeros(bx * by, np.int32)
+    f = lib().rtx_hostemu_bins
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
+    f.restype = C.c_int64
+    n = f(C.addressof(sd), C.addressof(cd), mask.ctypes.data, nf.ctypes.data, bx * by)
+    if n == 0:
+        return None
+    assert n == bx * by, n
+    return mask.reshape(by, bx), nf.reshape(by, bx)
+
+
 def philox(ctr, key):
     """The device's Philox4x32-10 of one counter (4 uint32) and key (k0, k1)."""
     c = np.ascontiguousarray(np.asarray(ctr, np.uint32))

@@ -275,11 +275,13 @@ def obj_bounds(path):
     return v.min(axis=0), v.max(axis=0)
 
 
-def bins_scene(seed, res=(41, 23)):
+def bins_scene(seed, res=(41, 23), lens=False):
     """Scenes that stress the primary-ray bins (rtx_api.hip primary_bins): one sample per
-    pixel, no lens or jitter (so bins apply), wide and narrow fields of view, spheres and
+    pixel, no lens or jitter (the pinhole bins), wide and narrow fields of view, spheres and
     boxes around, beside, behind and enclosing the camera, tiny far spheres (the fp32
-    discriminant's fuzz), moving objects, and sometimes the torus mesh up close."""
+    discriminant's fuzz), moving objects, and sometimes the torus mesh up close. lens=True:
+    the same scenes seen through a lens (DOF samples, apertures up to 1.5, near and far
+    focal lengths) with AA samples and jitter (the thick bins)."""
     rng = np.random.RandomState(1000 + seed)
     r = lambda lo, hi, n=None: np.round(rng.uniform(lo, hi, n), 3).tolist()  # noqa: E731
     mats = [{"name": "m%d" % i, "ID": i, "diffuse": r(0, 1, 3), "specular": r(0, 1, 3), "hardness": 16,
@@ -324,4 +326,9 @@ def bins_scene(seed, res=(41, 23)):
                       "power": 1.0}]}
     if rng.rand() < 0.3:
         sc["motion"] = {"time": 1.0, "samples": 2, "final": 1}
+    if lens:  # the lens cameras' "thick" bins: DOF spread, AA spread, jitter
+        lr = np.random.RandomState(5000 + seed)
+        sc["DOF"] = {"aperture": float(np.round(lr.choice([0.02, 0.2, 0.6, 1.5]), 3)),
+                     "focal_length": float(np.round(lr.uniform(0.5, 12.0), 3)), "samples": int(lr.randint(1, 9))}
+        sc["AA"] = {"jitter": bool(lr.rand() < 0.8), "samples": int(lr.randint(1, 4))}
     return sc

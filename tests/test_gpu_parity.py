@@ -531,6 +531,38 @@ def test_primary_bins_equal_walk(seed, monkeypatch):
     assert torch.equal(on.render_device(row0=13, nrows=30), a[13:43])
 
 
+@pytest.mark.parametrize("seed", range(16))
+def test_lens_bins_equal_walk(seed, monkeypatch):
+    """Lens cameras' thick primary-ray bins (rtx_api.hip primary_bins: DOF samples, AA
+    spreads, Philox jitter) change no pixel: binned == walk on 160x96 frames, == the oracle
+    (restated Philox stream) on every fourth."""
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import bins_scene
+    d = bins_scene(seed, res=(160, 96), lens=True)
+    on = product_scene_dict(d)
+    a = on.render_device().clone()
+    monkeypatch.setenv("RTX_BINS", "0")
+    b = product_scene_dict(d).render_device().clone()
+    monkeypatch.delenv("RTX_BINS")
+    assert torch.equal(a, b)
+    if seed % 4 == 0:
+        img = np.ascontiguousarray(np.transpose(a.cpu().numpy()[::-1], (1, 0, 2))).astype(np.float64)
+        noise = _philox_noise(on, 0, 160) if on.jitter else None
+        assert_parity(img, oracle_render_dict(d, noise=noise), "lens bins seed %d" % seed)
+
+
+def test_lens_bins_config5_full_frame(monkeypatch):
+    """BASELINE config 5 (DepthOfField 3840x2160, AA 2 x DOF 32, Philox jitter) with its
+    thick bins and without (RTX_LENS_BINS=0): the same 8.3 M pixels, bit for bit."""
+    edits = {"AA": {"jitter": True, "samples": 2}}
+    res = (3840, 2160)
+    a = product_scene("DepthOfField", res, **edits).render_device().clone()
+    monkeypatch.setenv("RTX_LENS_BINS", "0")
+    b = product_scene("DepthOfField", res, **edits).render_device().clone()
+    torch.cuda.synchronize()
+    assert torch.equal(a, b), float((a != b).float().mean())
+
+
 @pytest.mark.parametrize("case", ["blob", "blob_walk", "random0", "random3", "random6", "bins0", "bins5", "bins8"])
 def test_wave_cooperative_mesh_matches_oracle(case, tmp_path, monkeypatch):
     """The wave-cooperative mesh variant (experiment -DRTX_WCOOP=1, off by default; DESIGN

@@ -442,6 +442,120 @@ def test_hostemu_primary_bins_wide_frame(seed, monkeypatch):
         assert_parity(img, oracle_render_dict(d, k, 8), "wide bins seed %d strip %d" % (seed, k))
 
 
+def _lens_noise(sc, subimage=0, tasks=1):
+    """The oracle's jitter stream for a product scene: Philox (oracle/philox.py) or none."""
+    if not sc.jitter:
+        return None
+    from oracle import philox as PH
+    from rtx.scene import strip_columns
+    col0, ncols = strip_columns(sc.vc.width, subimage, tasks)
+    return PH.jitter_noise(sc.seed, col0, ncols, sc.vc.height, sc.vc.dof_samples, sc.samples)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_hostemu_lens_bins_equal_walk(seed, monkeypatch):
+    """Lens cameras' thick primary-ray bins (rtx_api.hip primary_bins: DOF origins, AA
+    spreads and jitter bounded around the pinhole) change no pixel: binned == walk, and
+    == the oracle (with the restated Philox stream) on every fourth scene."""
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import bins_scene
+    d = bins_scene(seed, res=(33, 19), lens=True)
+    sc = product_scene_dict(d)
+    img, _ = hostemu.render(sc)
+    monkeypatch.setenv("RTX_BINS", "0")
+    walk, _ = hostemu.render(sc)
+    monkeypatch.delenv("RTX_BINS")
+    assert np.array_equal(img, walk)
+    if seed % 4 == 0:
+        assert_parity(img, oracle_render_dict(d, noise=_lens_noise(sc)), "lens bins seed %d" % seed)
+
+
+def _lens_ray_scene(seed, pinhole=False):
+    """bins_scene(lens=True) without a mesh (lens cameras keep no face bins), motion, or
+    a sphere around the lens (it would take every ray); pinhole=True: the same camera
+    with no aperture, AA spread or jitter."""
+    from scenegen import bins_scene
+    d = bins_scene(seed, res=(160, 96), lens=True)
+    cam = np.array(d["camera"]["position"])
+    d["objects"] = [o for o in d["objects"] if o["type"] != "mesh" and not (
+        o["type"] == "sphere" and np.linalg.norm(np.array(o["position"]) - cam) < o["radius"] + d["DOF"]["aperture"])]
+    d.pop("motion", None)
+    for o in d["objects"]:
+        o.pop("speed", None)
+    if pinhole:
+        d["DOF"] = {"aperture": 0.0, "focal_length": d["DOF"]["focal_length"], "samples": 1}
+        d["AA"] = {"jitter": False, "samples": 1}
+    return d
+
+
+def _lens_ray_misses(d, mask):
+    """Primary sample rays of scene d's lens camera (the DOF origin's focal direction from
+    the jittered AA origin, scene.py:54-65, set up in fp32 like the device) whose closest
+    hit is a sphere or box missing from their tile's mask: (misses, rays that hit one)."""
+    from common import product_scene_dict
+    sc = product_scene_dict(d)
+    cd, t = sc.camera_desc()
+    W, H, nd, na = cd.ncols, cd.height, sc.vc.dof_samples, sc.samples
+    f32 = np.float32
+    u, v, w = (np.asarray(x, f32) for x in (sc.vc.u, sc.vc.v, sc.vc.w))
+    pos = np.asarray(sc.vc.position, f32)
+    xs, ys = np.asarray(t["xs"], f32), np.asarray(t["ys"], f32)
+    cc, jj = np.meshgrid(np.arange(W), np.arange(H), indexing="ij")  # [W][H], the jitter table's order
+    base = xs[cc][..., None] * u + ys[jj][..., None] * v - w * f32(sc.vc.d)
+    bdir = base / np.linalg.norm(base, axis=-1, keepdims=True).astype(f32)
+    focal = pos + bdir * f32(sc.vc.focal_length)
+    dof = np.asarray(t["dof"], f32).reshape(nd, 3)
+    aa = np.asarray(t["aa"], f32).reshape(nd, na, 3)
+    if sc.jitter:
+        rnd = hostemu.jitter(sc.seed, 0, W, H, nd, na).reshape(W, H, nd, na, 3)
+        jit = rnd / np.linalg.norm(rnd, axis=-1, keepdims=True).astype(f32) * f32(t["jscale"])
+    else:
+        jit = np.zeros((W, H, nd, na, 3), f32)
+    dd = focal[:, :, None, :] - dof[None, None]                     # [W][H][nd][3]
+    dd = dd / np.linalg.norm(dd, axis=-1, keepdims=True).astype(f32)
+    o = (aa[None, None] + jit).reshape(-1, 3)
+    dr = np.broadcast_to(dd[:, :, :, None, :], (W, H, nd, na, 3)).reshape(-1, 3)
+    hit = hostemu.intersect(sc, o, dr)["obj"]
+    kinds = [g["type"] for g in d["objects"]]
+    pc = np.broadcast_to(cc[:, :, None, None], (W, H, nd, na)).ravel()
+    prow = (H - 1 - np.broadcast_to(jj[:, :, None, None], (W, H, nd, na))).ravel()
+    misses = tested = 0
+    for i, k in enumerate(kinds):
+        if k not in ("sphere", "box"):
+            continue
+        bt = (0 if k == "sphere" else 16) + sum(1 for q in kinds[:i] if q == k)
+        sel = hit == i
+        tested += int(sel.sum())
+        misses += int((((mask[prow[sel] >> 3, pc[sel] >> 3] >> bt) & 1) == 0).sum())
+    return misses, tested
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_lens_bins_hold_every_sample_ray(seed):
+    """The thick bins' bound, ray by ray: every primary sample ray of a lens camera whose
+    closest hit is a sphere or box finds that object in its tile's mask. 160 x 96 pixels,
+    every DOF x AA sample (up to 24 per pixel)."""
+    from common import product_scene_dict
+    d = _lens_ray_scene(seed)
+    b = hostemu.bins(product_scene_dict(d))
+    if b is None:  # an aperture too wide for the focal length: no bins (seed 0)
+        assert d["DOF"]["aperture"] > 0.05 * d["DOF"]["focal_length"], d["DOF"]
+        return
+    misses, tested = _lens_ray_misses(d, b[0])
+    assert misses == 0, (misses, tested)
+
+
+def test_lens_ray_check_is_sensitive():
+    """The ray check above fails the pinhole bins (no lens growth) of the same scenes:
+    lens rays do leave the pinhole footprint, so the growth is what holds them."""
+    from common import product_scene_dict
+    bad = 0
+    for seed in range(16):
+        pin = hostemu.bins(product_scene_dict(_lens_ray_scene(seed, pinhole=True)))
+        bad += _lens_ray_misses(_lens_ray_scene(seed), pin[0])[0] > 0
+    assert bad >= 2, bad
+
+
 @pytest.mark.parametrize("name", ["TwoSpheresPlane", "MirrorRefraction", "TorusMesh", "DepthOfField"])
 def test_jit_baked_records_are_the_scene_records(name):
     """The prelude of the one-sample scene-specialized kernels (rtx_api.hip
