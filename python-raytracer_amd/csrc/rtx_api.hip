@@ -1170,6 +1170,148 @@ bool light_grids(const HostScene& H, std::vector<DLGrid>& grids, std::vector<int
     return any;
 }
 
+// Shadow grids of directional lights (DSGrid, rtx_trace.h). Light li's shadow ray from p
+// is the half-line p + t d (d = fl32 -direction, LIGHT.negvec; t > 1e-4 or 1e-3). On two
+// fp32 unit vectors e1, e2 across d, its points project to p.e + t d.e: a hit point x of a
+// sphere or box (|x| <= Rx) projects within t |d.e| <= (Rx + |p|) |d.e| / |d| of p's
+// projection. So p's projection lies in the object's footprint (the projection of its
+// bounding box; of a sphere: c.e +- r |e|) grown by that drift, by the fuzz of the fp32
+// sphere discriminant (a ray can "hit" a sphere it misses by ~2^-10.5 |p - c|; grown by
+// 2^-8 (|p| + |c| + r), as primary_bins) and by 2^-18 of the magnitudes (the device's fp32
+// dot products and cell arithmetic); every cell the grown footprint meets, widened by one
+// cell, lists the object. The grid spans the footprints' union (with two spare cells a
+// side) for origins with max |p_i| <= pmax (5/4 of the objects' extent + 1); moving
+// objects, and objects beyond the 16th of a kind, are `always` tested.
+bool dir_shadow_grids(const HostScene& H, std::vector<DSGrid>& grids, std::vector<uint32_t>& masks) {
+    grids.assign(H.lights.size(), DSGrid{});
+    masks.clear();
+    struct Ob {
+        double lo[3], hi[3];  // bounding box
+        double c[3], r;       // sphere: centre and radius (r < 0: a box)
+        uint32_t bit;
+    };
+    std::vector<Ob> obs;
+    uint32_t always = 0;
+    double R = 0.0;  // the largest |coordinate| of a static sphere's or box's bounds
+    for (int32_t k = 0; k < H.n_sphere + H.n_box; ++k) {
+        const bool sphere = k < H.n_sphere;
+        const DObj& ob = H.objs[H.n_plane + k];
+        const int32_t j = sphere ? k : k - H.n_sphere;
+        const uint32_t bit = 1u << ((sphere ? 0 : 16) + (j & 15));
+        Ob o{};
+        o.bit = bit;
+        o.r = sphere ? ob.radius : -1.0;
+        for (int a = 0; a < 3; ++a) {
+            if (sphere) {
+                o.c[a] = ob.a[a];
+                o.lo[a] = ob.a[a] - ob.radius;
+                o.hi[a] = ob.a[a] + ob.radius;
+            } else {
+                o.lo[a] = std::min((double)ob.a[a], (double)ob.b[a]);
+                o.hi[a] = std::max((double)ob.a[a], (double)ob.b[a]);
+            }
+        }
+        bool ok = !ob.has_speed && j < 16 && (sphere ? H.n_sphere : H.n_box) <= 16;
+        for (int a = 0; a < 3; ++a) ok = ok && std::isfinite(o.lo[a]) && std::isfinite(o.hi[a]);
+        if (!ok) {
+            always |= bit;
+            continue;
+        }
+        for (int a = 0; a < 3; ++a) R = std::max(R, std::max(std::fabs(o.lo[a]), std::fabs(o.hi[a])));
+        obs.push_back(o);
+    }
+    if (obs.empty()) return false;
+    int32_t G = 64;
+    if (const char* eg = getenv("RTX_DSGRID_G"); eg && atoi(eg) > 0) G = std::min(1024, atoi(eg));  // tuning
+    const double pmax = 1.25 * R + 1.0, pm = std::sqrt(3.0) * pmax;  // pm >= |p| of a gridded origin
+    bool any = false;
+    for (size_t li = 0; li < H.lights.size(); ++li) {
+        const DLight& Lt = H.lights[li];
+        if (Lt.type != LIGHT_DIRECTIONAL) continue;
+        const double d[3] = {Lt.negvec[0], Lt.negvec[1], Lt.negvec[2]};
+        const double dn = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+        if (!(dn > 0.0) || !std::isfinite(dn)) continue;
+        // e1, e2: unit vectors across d, rounded to the fp32 values the device uses
+        const double a[3] = {d[0] / dn, d[1] / dn, d[2] / dn};
+        const int ax = std::fabs(a[0]) <= std::fabs(a[1]) && std::fabs(a[0]) <= std::fabs(a[2]) ? 0
+                       : std::fabs(a[1]) <= std::fabs(a[2]) ? 1 : 2;
+        double x[3] = {0.0, 0.0, 0.0};
+        x[ax] = 1.0;
+        double e1[3] = {a[1] * x[2] - a[2] * x[1], a[2] * x[0] - a[0] * x[2], a[0] * x[1] - a[1] * x[0]};
+        double n1 = std::sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
+        float f1[3], f2[3];
+        for (int q = 0; q < 3; ++q) f1[q] = (float)(e1[q] / n1);
+        double e2[3] = {a[1] * f1[2] - a[2] * f1[1], a[2] * f1[0] - a[0] * f1[2], a[0] * f1[1] - a[1] * f1[0]};
+        const double n2 = std::sqrt(e2[0] * e2[0] + e2[1] * e2[1] + e2[2] * e2[2]);
+        for (int q = 0; q < 3; ++q) f2[q] = (float)(e2[q] / n2);
+        const double g1[3] = {f1[0], f1[1], f1[2]}, g2[3] = {f2[0], f2[1], f2[2]};
+        auto dot3 = [](const double* p, const double* q) { return p[0] * q[0] + p[1] * q[1] + p[2] * q[2]; };
+        const double drift_rel = std::max(std::fabs(dot3(d, g1)), std::fabs(dot3(d, g2))) / dn * (1.0 + 1e-9);
+        const double len1 = std::sqrt(dot3(g1, g1)), len2 = std::sqrt(dot3(g2, g2));
+        // grown footprints
+        std::vector<double> fp(4 * obs.size());
+        double U0 = INFINITY, U1 = -INFINITY, V0 = INFINITY, V1 = -INFINITY;
+        for (size_t i = 0; i < obs.size(); ++i) {
+            const Ob& o = obs[i];
+            double rx = 0.0;
+            for (int q = 0; q < 3; ++q) rx += std::max(o.lo[q] * o.lo[q], o.hi[q] * o.hi[q]);
+            rx = std::sqrt(rx);  // >= |x| of every point of the box
+            double pad = (rx + pm) * drift_rel + 0x1p-18 * (rx + pm);
+            double u0, u1, v0, v1;
+            if (o.r >= 0.0) {
+                const double cm = std::sqrt(dot3(o.c, o.c));
+                pad += 0x1p-8 * (pm + cm + o.r);
+                const double cu = dot3(o.c, g1), cv = dot3(o.c, g2);
+                u0 = cu - o.r * len1; u1 = cu + o.r * len1;
+                v0 = cv - o.r * len2; v1 = cv + o.r * len2;
+            } else {
+                pad += 1e-5 * (pm + rx);
+                u0 = v0 = INFINITY;
+                u1 = v1 = -INFINITY;
+                for (int q = 0; q < 8; ++q) {
+                    const double p[3] = {q & 1 ? o.hi[0] : o.lo[0], q & 2 ? o.hi[1] : o.lo[1], q & 4 ? o.hi[2] : o.lo[2]};
+                    const double pu = dot3(p, g1), pv = dot3(p, g2);
+                    u0 = std::min(u0, pu); u1 = std::max(u1, pu);
+                    v0 = std::min(v0, pv); v1 = std::max(v1, pv);
+                }
+            }
+            double* F = &fp[4 * i];
+            F[0] = u0 - pad; F[1] = u1 + pad; F[2] = v0 - pad; F[3] = v1 + pad;
+            U0 = std::min(U0, F[0]); U1 = std::max(U1, F[1]);
+            V0 = std::min(V0, F[2]); V1 = std::max(V1, F[3]);
+        }
+        if (!std::isfinite(U0 + U1 + V0 + V1)) continue;
+        // two spare cells a side: the device's rounding cannot carry an origin from off the
+        // grid into a footprint
+        const double wu = (U1 - U0) * (1.0 + 1e-6) + 1e-9, wv = (V1 - V0) * (1.0 + 1e-6) + 1e-9;
+        DSGrid g{};
+        for (int q = 0; q < 3; ++q) { g.e1[q] = f1[q]; g.e2[q] = f2[q]; }
+        g.G = G;
+        g.pmax = (float)pmax;
+        if ((double)g.pmax > pmax) g.pmax = std::nextafter(g.pmax, 0.0f);
+        g.su = (float)((G - 4) / wu);
+        g.sv = (float)((G - 4) / wv);
+        g.u0 = (float)(U0 - 2.0 / g.su);
+        g.v0 = (float)(V0 - 2.0 / g.sv);
+        g.off = (int32_t)masks.size();
+        g.always = always;
+        masks.resize(masks.size() + (size_t)G * G, 0u);
+        auto cell = [&](double u, double o0, double s) {  // as the device maps it, +-1 below
+            return (int32_t)std::floor((u - o0) * s);
+        };
+        for (size_t i = 0; i < obs.size(); ++i) {
+            const double* F = &fp[4 * i];
+            const int32_t i0 = std::max(0, cell(F[0], g.u0, g.su) - 1), i1 = std::min(G - 1, cell(F[1], g.u0, g.su) + 1);
+            const int32_t j0 = std::max(0, cell(F[2], g.v0, g.sv) - 1), j1 = std::min(G - 1, cell(F[3], g.v0, g.sv) + 1);
+            for (int32_t jy = j0; jy <= j1; ++jy)
+                for (int32_t ix = i0; ix <= i1; ++ix) masks[(size_t)g.off + (size_t)jy * G + ix] |= obs[i].bit;
+        }
+        grids[li] = g;
+        any = true;
+    }
+    return any;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ scene-specialized kernels
@@ -1452,6 +1594,7 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
     if (sec && v.n_mats <= 64) opts.push_back("-DRTX_FRAME_MATBITS=6");
     opts.push_back(std::string("-DRTX_PRIMARY_BINS=") + (kp.S.bins_on ? "1" : "0"));
     opts.push_back(std::string("-DRTX_LIGHT_GRIDS=") + (v.lgrid_on ? "1" : "0"));
+    opts.push_back(std::string("-DRTX_DIR_GRIDS=") + (v.dsg_on ? "1" : "0"));
     if (!ext && !spp) {  // experiment: per-lane object / material gathers from LDS (RTX_LDS_RECORDS=1)
         const char* e = getenv("RTX_LDS_RECORDS");
         const size_t bytes = (size_t)v.n_objs_all * sizeof(DObj) + (size_t)v.n_mats * sizeof(DMat);
@@ -1622,6 +1765,8 @@ struct rtx_scene {
     float* d_bin_zmin = nullptr;
     uint32_t* d_bin_mask = nullptr;
     void* d_lgrid = nullptr;        // light grids (per scene: lights and mesh are static)
+    void* d_dsgrid = nullptr;       // directional lights' shadow grids (per scene)
+    void* d_dsg_mask = nullptr;
     void* d_lg_start = nullptr;
     void* d_lg_faces = nullptr;
     void* d_lg_d2 = nullptr;
@@ -1716,7 +1861,8 @@ void free_scene(rtx_scene* s) {
     (void)hipFree(s->d_split);
     (void)hipFree(s->d_split_count);
     for (void* p : {s->d_objs, s->d_tris, s->d_trins, s->d_fboxes, s->d_mats, s->d_lights, s->d_leaves, s->d_tri_orig, s->d_nodes, s->d_nmat,
-                    s->d_texels, s->d_lut, s->d_bounds_abi, s->d_lgrid, s->d_lg_start, s->d_lg_faces, s->d_lg_d2})
+                    s->d_texels, s->d_lut, s->d_bounds_abi, s->d_lgrid, s->d_lg_start, s->d_lg_faces, s->d_lg_d2,
+                    s->d_dsgrid, s->d_dsg_mask})
         (void)hipFree(p);
     delete s;
 }
@@ -1823,6 +1969,20 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
             v.lg_faces = (cptr<int32_t>)s->d_lg_faces;
             v.lg_d2 = (cptr<float>)s->d_lg_d2;
             v.lgrid_on = 1;
+        }
+    }
+    {  // shadow grids of directional lights (RTX_DSGRID=0: test every sphere and box)
+        std::vector<DSGrid> grids;
+        std::vector<uint32_t> masks;
+        const char* e = getenv("RTX_DSGRID");
+        if (!(e && e[0] == '0') && dir_shadow_grids(H, grids, masks)) {
+            if ((rc = upload(&s->d_dsgrid, grids)) || (rc = upload(&s->d_dsg_mask, masks))) {
+                free_scene(s);
+                return rc;
+            }
+            v.dsgrid = (cptr<DSGrid>)s->d_dsgrid;
+            v.dsg_mask = (cptr<uint32_t>)s->d_dsg_mask;
+            v.dsg_on = 1;
         }
     }
     *out = s;

@@ -264,6 +264,23 @@ struct alignas(16) DLGrid {
     int32_t start_off, pad0;  // this light's G*G + 1 entries of lg_start
 };
 
+// Shadow grid of a directional light (rtx_api.hip dir_shadow_grids). The light's shadow
+// rays are parallel, so the spheres and boxes one of them can meet follow from where its
+// origin p projects on a plane across the light: cell (floor((p.e1 - u0) su),
+// floor((p.e2 - v0) sv)) of G x G lists them (bits: spheres 0-15, boxes 16-31). `always`:
+// objects every ray tests (moving ones, beyond 16 of a kind); origins off the grid test
+// only those, origins with max |p_i| > pmax test everything.
+struct alignas(16) DSGrid {
+    float e1[3];
+    int32_t G;  // cells per side; 0 = no grid for this light
+    float e2[3];
+    float pmax;
+    float u0, v0, su, sv;
+    int32_t off;  // this light's G * G masks in dsg_mask
+    uint32_t always;
+    int32_t pad0, pad1;
+};
+
 template <class T>
 using cptr = const T RTX_CONST*;
 template <class T>
@@ -304,6 +321,10 @@ struct SceneView {
     cptr<int32_t> lg_faces;          // stored face indices (within the mesh), by lg_d2
     cptr<float> lg_d2;               // per entry: (a lower bound of the face's distance along a)^2
     int32_t lgrid_on, pad8, pad9, pad10;
+    // Shadow grids (per light; directional lights against the spheres and boxes)
+    cptr<DSGrid> dsgrid;
+    cptr<uint32_t> dsg_mask;
+    int32_t dsg_on, pad11, pad12, pad13;
 };
 
 // Mesh records read by the hot BVH walks (closest_hit / occluded). Scene-specialized
@@ -1871,6 +1892,22 @@ RTX_HD int32_t first_where(int32_t v, bool pred) {
 #endif
 }
 
+// The spheres and boxes directional light `light`'s shadow ray from p may meet (DSGrid);
+// ~0: all.
+RTX_HD uint32_t dir_shadow_mask(const SceneView& S, int light, f3 p) {
+    cref<DSGrid> g = S.dsgrid[light];
+    const int32_t G = g.G;
+    if (G == 0) return ~0u;
+    const float m = fmaxf(fabsf(p.x), fmaxf(fabsf(p.y), fabsf(p.z)));
+    if (!(m <= g.pmax)) return ~0u;  // (NaN too)
+    const float fx = (dot(p, mk(g.e1[0], g.e1[1], g.e1[2])) - g.u0) * g.su;
+    const float fy = (dot(p, mk(g.e2[0], g.e2[1], g.e2[2])) - g.v0) * g.sv;
+    uint32_t msk = g.always;
+    if (fx >= 0.0f && fx < (float)G && fy >= 0.0f && fy < (float)G)
+        msk |= S.dsg_mask[g.off + (int32_t)fy * G + (int32_t)fx];
+    return msk;
+}
+
 #ifndef RTX_PLANE_SHADOW_RCP
 #define RTX_PLANE_SHADOW_RCP 1
 #endif
@@ -1926,8 +1963,15 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
         occ = occ || hit;
     }
     if (RTX_ALL(occ)) return true;
+    // the spheres and boxes this lane's ray may meet: a directional light's shadow grid
+    uint32_t smask = ~0u;
+#if !(defined(RTX_DIR_GRIDS) && !RTX_DIR_GRIDS)
+    if (light >= 0 && S.dsg_on && RTX_NSPHERE(S) + RTX_NBOX(S) > 0) smask = dir_shadow_mask(S, light, o);
+#endif
     for (int k = 0; k < RTX_NSPHERE(S); ++k, ++oi) {  // simple_geometry.py:48-72 (shadow_epsilon 1e-3)
         if (RTX_ABLATE == 19) continue;  // cost probe: spheres never occlude
+        const bool sl = ((smask >> (k & 15)) & 1u) != 0u;
+        if (!RTX_ANY(sl && !occ)) continue;
         const DObj ob = S.objs[oi];
         const f3 ctr = moved(ob, ob.a, time);
 #ifdef RTX_FIXED_COUNTS
@@ -1940,9 +1984,9 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
         int dec = -1;
         if (RTX_SHADOW_F32 && RTX_ABLATE != 4) {
             dec = sphere_shadow_f32(d, oc, q, ob.r2f, tmax_dn, tmax_up);
-            if (!occ && dec >= 0) occ = dec == 1;
+            if (!occ && sl && dec >= 0) occ = dec == 1;
         }
-        if (!occ && dec < 0 && sphere_disc_sign_oc(d, oc, q, ob.r2f) >= 0) {
+        if (!occ && sl && dec < 0 && sphere_disc_sign_oc(d, oc, q, ob.r2f) >= 0) {
             double b, s, two_a;
             if (RTX_ABLATE == 4 ? sphere_roots(o, d, ctr, ob.r2, b, s, two_a)
                                 : sphere_roots_oc(d, oc, q, ob.r2, b, s, two_a)) {
@@ -1961,19 +2005,27 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
     }
     if (RTX_ALL(occ)) return true;
     RayInv ri{};
-    if (RTX_NBOX(S) > 0) ri = ray_inv(o, d);  // meshes: only once a lane passes a bounding volume
+    // the reciprocals once some lane's ray may meet a box (meshes: once a lane passes a
+    // bounding volume)
+    bool have_ri = false;
+    if (RTX_NBOX(S) > 0 && RTX_ANY(!occ && (smask >> 16) != 0u)) {
+        ri = ray_inv(o, d);
+        have_ri = true;
+    }
     for (int k = 0; k < RTX_NBOX(S); ++k, ++oi) {  // simple_geometry.py:251-294
         if (RTX_ABLATE == 20) continue;  // cost probe: boxes never occlude
+        const bool sl = ((smask >> (16 + (k & 15))) & 1u) != 0u;
+        if (!RTX_ANY(sl && !occ)) continue;
         const DObj ob = S.objs[oi];
         const f3 mn = moved(ob, ob.a, time), mx = moved(ob, ob.b, time);
         if (RTX_BOX_IV_CULL) {
             if (RTX_ALL(occ)) break;
             const SlabIv iv = box_slabs_iv(o, d, mn, mx, &ri);
-            const bool maybe = !occ && !box_iv_out(iv, INFINITY);
+            const bool maybe = !occ && sl && !box_iv_out(iv, INFINITY);
             if (!RTX_ANY(maybe)) continue;
             if (maybe) occ = box_shadow_iv(o, d, mn, mx, iv, t_max);
         } else {
-            const bool maybe = !occ && box_maybe_hit_obj(ob, mn, mx, o, ri, INFINITY);
+            const bool maybe = !occ && sl && box_maybe_hit_obj(ob, mn, mx, o, ri, INFINITY);
             if (!RTX_ANY(maybe)) continue;
             if (maybe) occ = box_shadow(o, d, mn, mx, t_max, &ri);
         }
@@ -1982,7 +2034,10 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
         for (int k = 0; k < RTX_NMESH(S); ++k, ++oi) {  // mesh.py:121-153 (no t_max test)
             const DObj ob = S.objs[oi];
             if (RTX_ALL(occ) || RTX_ABLATE == 16) break;  // 16: cost probe, meshes never occlude
-            if (RTX_NBOX(S) == 0 && k == 0) ri = ray_inv(o, d);
+            if (!have_ri) {
+                ri = ray_inv(o, d);
+                have_ri = true;
+            }
             bool live = !occ && bv_maybe(ob, o, ri, INFINITY);  // conservative pre-test
             if (!RTX_ANY(live)) continue;
             if (RTX_ABLATE == 13) continue;  // cost probe: the padded box pre-test only

@@ -147,6 +147,23 @@ def bins(scene, subimage=0, tasks=1):
     return mask.reshape(by, bx), nf.reshape(by, bx)
 
 
+def dir_shadow_mask(scene, p, light):
+    """The spheres (bits 0-15) and boxes (16-31) directional light ``light``'s shadow rays
+    from points p may meet by its shadow grid (uint32 per point, ~0: all), or None when the
+    light has no grid."""
+    sd = scene.scene_desc()
+    p = np.ascontiguousarray(np.asarray(p, np.float32).reshape(-1, 3).T)
+    n = p.shape[1]
+    out = np.zeros(n, np.uint32)
+    f = lib().rtx_hostemu_dir_shadow_mask
+    f.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_void_p]
+    rc = f(C.addressof(sd), n, p.ctypes.data, light, out.ctypes.data)
+    if rc == -1:
+        return None
+    _chk(rc)
+    return out
+
+
 def philox(ctr, key):
     """The device's Philox4x32-10 of one counter (4 uint32) and key (k0, k1)."""
     c = np.ascontiguousarray(np.asarray(ctr, np.uint32))

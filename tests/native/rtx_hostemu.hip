@@ -68,6 +68,19 @@ struct Grids {
     }
 };
 
+// The directional lights' shadow grids rtx_scene_create builds (RTX_DSGRID=0: none).
+struct DirGrids {
+    std::vector<DSGrid> grids;
+    std::vector<uint32_t> masks;
+    void bind(const HostScene& H, SceneView& v) {
+        const char* e = getenv("RTX_DSGRID");
+        if ((e && e[0] == '0') || !dir_shadow_grids(H, grids, masks)) return;
+        v.dsgrid = (cptr<DSGrid>)grids.data();
+        v.dsg_mask = (cptr<uint32_t>)masks.data();
+        v.dsg_on = 1;
+    }
+};
+
 // Dispatch over the kernel template flags, as rtx_render's launch switch does.
 template <bool MESH, bool SEC, bool X>
 void pixel_jit(const KParams& k, float* fb, int32_t row0, int32_t rr, int32_t cc, Tally& tl, const FrameStack& fs,
@@ -105,6 +118,8 @@ extern "C" int rtx_hostemu_render(const rtx_scene_desc* sd, const rtx_camera_des
     bind_view(H, k.S);
     Grids lg;
     lg.bind(H, k.S);
+    DirGrids dg;
+    dg.bind(H, k.S);
     std::vector<float> times(cd->n_times);
     for (int i = 0; i < cd->n_times; ++i) times[i] = (float)cd->times[i];
     const auto mm = std::minmax_element(times.begin(), times.end());
@@ -171,6 +186,8 @@ extern "C" int rtx_hostemu_render_rows(const rtx_scene_desc* sd, const rtx_camer
     bind_view(H, k.S);
     Grids lg;
     lg.bind(H, k.S);
+    DirGrids dg;
+    dg.bind(H, k.S);
     std::vector<float> times(cd->n_times);
     for (int i = 0; i < cd->n_times; ++i) times[i] = (float)cd->times[i];
     const auto mm = std::minmax_element(times.begin(), times.end());
@@ -302,6 +319,24 @@ extern "C" int rtx_hostemu_occluded_light(const rtx_scene_desc* sd, int64_t n, c
     return RTX_OK;
 }
 
+// The spheres and boxes directional light `light`'s shadow rays from points ro may meet,
+// by its shadow grid (rtx_trace.h dir_shadow_mask; rtx_api.hip dir_shadow_grids): bits per
+// point, ~0 where every object is tested. Returns -1 if the light has no grid.
+extern "C" int rtx_hostemu_dir_shadow_mask(const rtx_scene_desc* sd, int64_t n, const float* ro, int32_t light,
+                                           uint32_t* mask) {
+    HostScene H;
+    int rc = convert_scene(sd, H);
+    if (rc) return rc;
+    if (light < 0 || light >= (int32_t)H.lights.size()) return fail(RTX_ERR_INVALID, "bad light");
+    SceneView v{};
+    bind_view(H, v);
+    DirGrids dg;
+    dg.bind(H, v);
+    if (!v.dsg_on || dg.grids[light].G == 0) return -1;
+    for (int64_t i = 0; i < n; ++i) mask[i] = dir_shadow_mask(v, light, mk(ro[i], ro[n + i], ro[2 * n + i]));
+    return RTX_OK;
+}
+
 // Light grid statistics (tests and tuning): per light G, list entries, the longest list
 // and the non-empty cells; zeros for a light without a grid.
 extern "C" int rtx_hostemu_lgrid_stats(const rtx_scene_desc* sd, int64_t* out) {
@@ -410,6 +445,8 @@ extern "C" int64_t rtx_hostemu_jit_spec(const rtx_scene_desc* sd, const rtx_came
     k.S.n_leaves = (int32_t)H.leaves.size();
     Grids lg;
     lg.bind(H, k.S);
+    DirGrids dg;
+    dg.bind(H, k.S);
     std::vector<int32_t> bstart, bfaces;
     std::vector<float> bz;
     std::vector<uint32_t> bmask;
@@ -507,6 +544,8 @@ extern "C" int rtx_hostemu_render_split(const rtx_scene_desc* sd, const rtx_came
     bind_view(H, k.S);
     Grids lg;
     lg.bind(H, k.S);
+    DirGrids dg;
+    dg.bind(H, k.S);
     std::vector<float> times(cd->n_times);
     for (int i = 0; i < cd->n_times; ++i) times[i] = (float)cd->times[i];
     const auto mm = std::minmax_element(times.begin(), times.end());

@@ -61,6 +61,50 @@ def random_scene(seed, res=(48, 36), mesh=False):
     return sc
 
 
+def shadow_scene(seed, res=(40, 30)):
+    """Scenes for the directional lights' shadow grids (rtx_api.hip dir_shadow_grids):
+    spheres from tiny to large, near and far, boxes (some given by swapped corners), some
+    moving, under one to three directional lights -- axis-aligned, diagonal, grazing and
+    random directions."""
+    rng = np.random.RandomState(7000 + seed)
+    r = lambda lo, hi, n=None: np.round(rng.uniform(lo, hi, n), 3).tolist()  # noqa: E731
+    mats = [{"name": "m%d" % i, "ID": i, "diffuse": r(0, 1, 3), "specular": r(0, 1, 3), "hardness": 16,
+             "type": "mirror" if i == 3 else "diffuse", "tint": 0.3} for i in range(4)]
+    objs = [{"name": "ground", "type": "plane", "normal": [0.0, 1.0, 0.0], "position": [0.0, -1.0, 0.0],
+             "materials": [0, 1]}]
+    for k in range(rng.randint(2, 9)):
+        far = rng.rand() < 0.15
+        o = {"name": "s%d" % k, "type": "sphere", "radius": float(r(0.02, 0.3) if rng.rand() < 0.3 else r(0.3, 1.5)),
+             "position": r(-40, 40, 3) if far else r(-4, 4, 3), "materials": [int(rng.randint(4))]}
+        if rng.rand() < 0.15:
+            o["speed"] = r(-0.5, 0.5, 3)
+        objs.append(o)
+    for k in range(rng.randint(0, 5)):
+        o = {"name": "b%d" % k, "type": "box", "position": r(-4, 4, 3), "size": r(0.1, 2.5, 3),
+             "materials": [int(rng.randint(4))]}
+        if rng.rand() < 0.3:
+            c, sz = np.array(o.pop("position")), np.array(o.pop("size"))
+            mn, mx = c - sz / 2, c + sz / 2
+            sw = rng.rand(3) < 0.4
+            mn[sw], mx[sw] = mx[sw].copy(), mn[sw].copy()
+            o["min"], o["max"] = np.round(mn, 3).tolist(), np.round(mx, 3).tolist()
+        if rng.rand() < 0.15:
+            o["speed"] = r(-0.5, 0.5, 3)
+        objs.append(o)
+    dirs = [[0.0, -1.0, 0.0], [1.0, -1.0, -1.0], [-1.0, 0.0, -1.0], [1.0, -0.01, 0.3], r(-1, 1, 3), r(-1, 1, 3)]
+    lights = [{"name": "d%d" % i, "type": "directional", "direction": dirs[int(j)], "colour": r(0.3, 1, 3),
+               "power": 0.7} for i, j in enumerate(rng.choice(len(dirs), rng.randint(1, 4), replace=False))]
+    if rng.rand() < 0.3:
+        lights.append({"name": "p", "type": "point", "position": r(-5, 5, 3), "colour": r(0.3, 1, 3), "power": 1.0})
+    sc = {"resolution": list(res), "AA": {"jitter": False, "samples": 1}, "ambient": [0.1, 0.1, 0.1],
+          "camera": {"position": [float(r(-2, 2)), float(r(2, 5)), float(r(7, 10))], "lookAt": [0.0, 0.0, 0.0],
+                     "up": [0.0, 1.0, 0.0], "fov": float(rng.choice([45.0, 70.0, 100.0]))},
+          "materials": mats, "objects": objs, "lights": lights}
+    if rng.rand() < 0.3:
+        sc["motion"] = {"time": 1.0, "samples": 2, "final": 1}
+    return sc
+
+
 def tie_scene(res=(40, 30)):
     """Coincident geometry: the first object in scene order must win closest-hit ties."""
     return {"resolution": list(res), "ambient": [0.1, 0.1, 0.1],

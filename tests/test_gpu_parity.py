@@ -563,6 +563,35 @@ def test_lens_bins_config5_full_frame(monkeypatch):
     assert torch.equal(a, b), float((a != b).float().mean())
 
 
+@pytest.mark.parametrize("seed", range(12))
+def test_dir_shadow_grids_equal_walk(seed, monkeypatch):
+    """Directional lights' shadow grids (a shadow ray tests only the spheres and boxes its
+    origin's cell lists; rtx_api.hip dir_shadow_grids) change no pixel: grid == every
+    object (RTX_DSGRID=0) == oracle, 160x120 frames."""
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import shadow_scene
+    d = shadow_scene(seed, res=(160, 120))
+    a = product_scene_dict(d).render_device().clone()
+    monkeypatch.setenv("RTX_DSGRID", "0")
+    b = product_scene_dict(d).render_device().clone()
+    monkeypatch.delenv("RTX_DSGRID")
+    assert torch.equal(a, b)
+    img = np.ascontiguousarray(np.transpose(a.cpu().numpy()[::-1], (1, 0, 2))).astype(np.float64)
+    assert_parity(img, oracle_render_dict(d), "shadow grids seed %d" % seed)
+
+
+@pytest.mark.parametrize("name,res,edits", [("DepthOfField", (3840, 2160), {"AA": {"jitter": True, "samples": 2}}),
+                                            ("MirrorRefraction", (1920, 1080), {})])
+def test_dir_shadow_grids_full_frames(name, res, edits, monkeypatch):
+    """The BASELINE configs with directional lights, with their shadow grids and without:
+    the same frames, bit for bit."""
+    a = product_scene(name, res, **edits).render_device().clone()
+    monkeypatch.setenv("RTX_DSGRID", "0")
+    b = product_scene(name, res, **edits).render_device().clone()
+    torch.cuda.synchronize()
+    assert torch.equal(a, b), float((a != b).float().mean())
+
+
 @pytest.mark.parametrize("case", ["blob", "blob_walk", "random0", "random3", "random6", "bins0", "bins5", "bins8"])
 def test_wave_cooperative_mesh_matches_oracle(case, tmp_path, monkeypatch):
     """The wave-cooperative mesh variant (experiment -DRTX_WCOOP=1, off by default; DESIGN

@@ -556,6 +556,105 @@ def test_lens_ray_check_is_sensitive():
     assert bad >= 2, bad
 
 
+def _shadow_probe_points(d, rng, n_obj=400):
+    """Points that stress a directional shadow grid: on and just off each sphere's and box's
+    surface, upstream of them along every light (shadow rays grazing the silhouettes), on
+    the floor, scattered, and far away (beyond the grid's pmax)."""
+    pts = []
+    dirs = [np.asarray(l["direction"], np.float64) for l in d["lights"] if l["type"] == "directional"]
+    for o in d["objects"]:
+        if o["type"] == "sphere":
+            c, rad = np.asarray(o["position"], np.float64), o["radius"]
+            n = rng.normal(size=(n_obj, 3))
+            n /= np.linalg.norm(n, axis=1, keepdims=True)
+            surf = c + n * rad * (1.0 + rng.choice([-1e-3, 0.0, 1e-6, 1e-3, 0.05], (n_obj, 1)))
+        elif o["type"] == "box":
+            if "min" in o:
+                mn, mx = np.minimum(o["min"], o["max"]), np.maximum(o["min"], o["max"])
+            else:
+                c, sz = np.asarray(o["position"]), np.asarray(o["size"])
+                mn, mx = c - sz / 2, c + sz / 2
+            surf = rng.uniform(mn, mx, (n_obj, 3))
+            ax = rng.randint(3, size=n_obj)
+            side = rng.rand(n_obj) < 0.5
+            surf[np.arange(n_obj), ax] = np.where(side, mn[ax], mx[ax]) + rng.choice([-1e-3, 0.0, 1e-3], n_obj)
+        else:
+            continue
+        pts.append(surf)
+        for dv in dirs:  # upstream of the surface: the ray from there grazes or crosses it
+            u = -dv / np.linalg.norm(dv)
+            pts.append(surf - u * rng.uniform(0.001, 12.0, (n_obj, 1)))
+    pts.append(np.c_[rng.uniform(-10, 10, (2000, 1)), np.full((2000, 1), -1.0), rng.uniform(-10, 10, (2000, 1))])
+    pts.append(rng.uniform(-12, 12, (3000, 3)))
+    pts.append(rng.uniform(-300, 300, (500, 3)))
+    return np.concatenate(pts).astype(np.float32)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_hostemu_dir_shadow_grids_hold_every_ray(seed):
+    """Directional shadow grids, ray by ray: wherever a sphere or box alone occludes a
+    directional light's shadow ray (the device's own test, objects one at a time), the
+    grid's mask for the ray's origin lists it; moving objects are listed everywhere."""
+    import copy
+    from common import product_scene_dict
+    from scenegen import shadow_scene
+    d = shadow_scene(seed)
+    sc = product_scene_dict(d)
+    rng = np.random.RandomState(seed)
+    p = _shadow_probe_points(d, rng)
+    sd = sc.scene_desc()
+    kinds = [o["type"] for o in d["objects"]]
+    checked = 0
+    for li, l in enumerate(d["lights"]):
+        if l["type"] != "directional":
+            continue
+        mask = hostemu.dir_shadow_mask(sc, p, li)
+        assert mask is not None
+        dvec = -np.asarray(sd.lights[li].vector[:3], np.float32)  # the light's negvec, as the device casts it
+        for i, o in enumerate(d["objects"]):
+            if o["type"] not in ("sphere", "box"):
+                continue
+            bt = (0 if o["type"] == "sphere" else 16) + sum(1 for q in kinds[:i] if q == o["type"])
+            has = ((mask >> np.uint32(bt)) & 1).astype(bool)
+            if "speed" in o:
+                assert has.all(), (seed, li, i)
+                continue
+            one = copy.deepcopy(d)
+            one["objects"] = [copy.deepcopy(o)]
+            one.pop("motion", None)
+            occ = hostemu.occluded(product_scene_dict(one), p, np.broadcast_to(dvec, p.shape), np.inf, 0.0)
+            assert not (occ & ~has).any(), (seed, li, i, int((occ & ~has).sum()), int(occ.sum()))
+            checked += int(occ.sum())
+    assert checked > 0
+
+
+def test_hostemu_dir_shadow_grids_skip_most_rays():
+    """The grids are tight enough to pay: on DepthOfField and MirrorRefraction most
+    floor points' shadow rays test no sphere or box."""
+    for name in ("DepthOfField", "MirrorRefraction"):
+        sc = product_scene(name, (8, 8))
+        rng = np.random.RandomState(1)
+        p = np.c_[rng.uniform(-6, 6, (4000, 1)), np.zeros((4000, 1)), rng.uniform(-8, 3, (4000, 1))].astype(np.float32)
+        m = hostemu.dir_shadow_mask(sc, p, 0)
+        assert m is not None
+        assert (m == 0).mean() > 0.6, (name, float((m == 0).mean()))
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_hostemu_dir_shadow_grids_equal_walk(seed, monkeypatch):
+    """Frames with the directional shadow grids == without (RTX_DSGRID=0) == the oracle."""
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import shadow_scene
+    d = shadow_scene(seed)
+    img, cnt = hostemu.render(product_scene_dict(d))
+    monkeypatch.setenv("RTX_DSGRID", "0")
+    walk, cnt2 = hostemu.render(product_scene_dict(d))
+    monkeypatch.delenv("RTX_DSGRID")
+    assert np.array_equal(img, walk)
+    assert np.array_equal(cnt, cnt2)
+    assert_parity(img, oracle_render_dict(d), "shadow grids seed %d" % seed)
+
+
 @pytest.mark.parametrize("name", ["TwoSpheresPlane", "MirrorRefraction", "TorusMesh", "DepthOfField"])
 def test_jit_baked_records_are_the_scene_records(name):
     """The prelude of the one-sample scene-specialized kernels (rtx_api.hip
