@@ -780,10 +780,12 @@ bool lens_bins_disabled() {
 // holds every pixel whose primary ray can hit the object. Rectangles are binned into 8x8
 // pixel bins aligned with the strip's columns and the image rows, so a tile that starts
 // on a multiple of 8 rows finds in its bin (rtx_kernels.h primary_bin):
-//   * objmask: the static spheres (bits 0-15) and boxes (16-31) it may hit; spheres are
-//     inflated by 2^-8 (|o - c| + r), beyond the fuzz of the reference's fp32 discriminant
-//     (a ray can "hit" a sphere it misses by ~2^-10.5 |o - c|); moving objects, or more
-//     than 16 of a kind, are always tested;
+//   * objmask: the spheres (bits 0-15) and boxes (16-31) it may hit; spheres are inflated
+//     by 2^-8 (|o - c| + r), beyond the fuzz of the reference's fp32 discriminant (a ray
+//     can "hit" a sphere it misses by ~2^-10.5 |o - c|); moving objects by their sweep over
+//     the frame's times; objects beyond the 16th of a kind are always tested;
+//   * rootmask: the hierarchy roots (bit q: the q-th of the first 32) whose hit box
+//     (compute_bounds' h over the frame's times) it may meet;
 //   * the faces of the scene's one top-level mesh (if it has exactly one) it may hit,
 //     nearest first, with a lower bound of their hit t (depth <= t).
 // Other tiles and secondary/shadow rays walk everything. Returns false when the camera
@@ -802,9 +804,10 @@ bool lens_bins_disabled() {
 // pinhole ray of every pixel some sample of which hits it, and its pinhole projection
 // from P bins the tile as above. The mesh faces keep no bins (their t lower bounds hold
 // for one origin only).
-bool primary_bins(const HostScene& H, const rtx_camera_desc* c, std::vector<int32_t>& start,
-                  std::vector<int32_t>& faces, std::vector<float>& zmin, std::vector<uint32_t>& objmask,
-                  int32_t& bins_x, int32_t& mesh_bins) {
+bool primary_bins(const HostScene& H, const rtx_camera_desc* c, const std::vector<DBound>& nodeb,
+                  std::vector<int32_t>& start, std::vector<int32_t>& faces, std::vector<float>& zmin,
+                  std::vector<uint32_t>& objmask, std::vector<uint32_t>& rootmask, int32_t& bins_x,
+                  int32_t& mesh_bins) {
     if (c->ncols < 2 || c->height < 2) return false;
     const bool pinhole = c->n_dof == 1 && c->n_aa == 1 && c->jitter == RTX_JITTER_OFF &&
                          c->dof_origins[0] == c->position[0] && c->dof_origins[1] == c->position[1] &&
@@ -903,44 +906,37 @@ bool primary_bins(const HostScene& H, const rtx_camera_desc* c, std::vector<int3
         }
         return true;
     };
-    auto mark = [&](const Rect& R, uint32_t bit) {
+    auto mark_in = [&](std::vector<uint32_t>& m, const Rect& R, uint32_t bit) {
         for (int32_t by = R.r0; by <= R.r1; ++by)
-            for (int32_t bx = R.c0; bx <= R.c1; ++bx) objmask[(size_t)by * bins_x + bx] |= bit;
+            for (int32_t bx = R.c0; bx <= R.c1; ++bx) m[(size_t)by * bins_x + bx] |= bit;
     };
+    auto mark = [&](const Rect& R, uint32_t bit) { mark_in(objmask, R, bit); };
     auto box_corners = [](const double lo[3], const double hi[3], double (*pts)[3]) {
         for (int q = 0; q < 8; ++q)
             for (int a = 0; a < 3; ++a) pts[q][a] = (q >> a) & 1 ? hi[a] : lo[a];
     };
     objmask.assign(nb, 0u);
     const Rect all{0, bins_x - 1, 0, bins_y - 1};
-    for (int32_t k = 0; k < H.n_sphere; ++k) {
-        const DObj& ob = H.objs[H.n_plane + k];
-        const uint32_t bit = 1u << (k & 15);
-        double pts[8][3], lo[3], hi[3], oc2 = 0.0, zc = 0.0, z;
-        for (int a = 0; a < 3; ++a) {
-            oc2 += ((double)ob.a[a] - o[a]) * ((double)ob.a[a] - o[a]);
-            zc -= ((double)ob.a[a] - o[a]) * c->w[a];
-        }
-        // lens: every sample origin lies within A + R1 of o
-        const double re0 = ob.radius + 0x1p-8 * (std::sqrt(oc2) + lensA + lensR1 + std::fabs(ob.radius));
-        const double re = re0 + lens_pad(zc - re0, zc + re0);
-        for (int a = 0; a < 3; ++a) { lo[a] = ob.a[a] - re; hi[a] = ob.a[a] + re; }
-        box_corners(lo, hi, pts);
-        Rect R;
-        if (H.n_sphere > 16 || ob.has_speed || !std::isfinite(re) || !rect_of(pts, 8, R, z)) R = all;
-        mark(R, bit);
+    // moving objects: moved() = fl32(p + speed * time) over the frame's times, padded
+    double tlo = INFINITY, thi = -INFINITY;
+    for (int32_t i = 0; i < c->n_times; ++i) {
+        tlo = std::min(tlo, (double)(float)c->times[i]);
+        thi = std::max(thi, (double)(float)c->times[i]);
     }
-    for (int32_t k = 0; k < H.n_box; ++k) {
-        const DObj& ob = H.objs[H.n_plane + H.n_sphere + k];
-        const uint32_t bit = 1u << (16 + (k & 15));
-        double pts[8][3], lo[3], hi[3], z;
+    auto sweep = [&](const DObj& ob, double* lo, double* hi) {
+        if (!ob.has_speed) return;
         for (int a = 0; a < 3; ++a) {
-            const double p = 1e-5 * (std::fabs((double)ob.a[a]) + std::fabs((double)ob.b[a]) + std::fabs(o[a]));
-            lo[a] = std::min((double)ob.a[a], (double)ob.b[a]) - p;
-            hi[a] = std::max((double)ob.a[a], (double)ob.b[a]) + p;
+            const double s0 = (double)ob.speed[a] * tlo, s1 = (double)ob.speed[a] * thi;
+            const double pad = 1e-5 * (std::fabs(lo[a]) + std::fabs(hi[a]) + std::fabs(s0) + std::fabs(s1));
+            lo[a] += std::min(s0, s1) - pad;
+            hi[a] += std::max(s0, s1) + pad;
         }
+    };
+    // the bins of a box, grown for a lens camera by the deviation over its depth range
+    auto box_rect = [&](double* lo, double* hi, Rect& R) {
+        double pts[8][3], z;
         box_corners(lo, hi, pts);
-        if (!pinhole) {  // grow by the lens deviation over the box's depth range
+        if (!pinhole) {
             double zlo = INFINITY, zhi = -INFINITY;
             for (int q = 0; q < 8; ++q) {
                 double zq = 0.0;
@@ -952,9 +948,63 @@ bool primary_bins(const HostScene& H, const rtx_camera_desc* c, std::vector<int3
             for (int a = 0; a < 3; ++a) { lo[a] -= g; hi[a] += g; }
             box_corners(lo, hi, pts);
         }
+        return std::isfinite(lo[0] + lo[1] + lo[2] + hi[0] + hi[1] + hi[2]) && rect_of(pts, 8, R, z);
+    };
+    for (int32_t k = 0; k < H.n_sphere; ++k) {
+        const DObj& ob = H.objs[H.n_plane + k];
+        const uint32_t bit = 1u << (k & 15);
+        double lo[3], hi[3], oc2 = 0.0, sp = 0.0;
+        for (int a = 0; a < 3; ++a) {
+            oc2 += ((double)ob.a[a] - o[a]) * ((double)ob.a[a] - o[a]);
+            if (ob.has_speed) sp += (double)ob.speed[a] * ob.speed[a];
+        }
+        // lens: every sample origin lies within A + R1 of o; moving: the centre within
+        // |speed| max|t| of its place
+        const double mt = std::max(std::fabs(tlo), std::fabs(thi));
+        const double re = ob.radius + 0x1p-8 * (std::sqrt(oc2) + std::sqrt(sp) * mt + lensA + lensR1 + std::fabs(ob.radius));
+        for (int a = 0; a < 3; ++a) { lo[a] = ob.a[a] - re; hi[a] = ob.a[a] + re; }
+        sweep(ob, lo, hi);
         Rect R;
-        if (H.n_box > 16 || ob.has_speed || !rect_of(pts, 8, R, z)) R = all;
+        if (H.n_sphere > 16 || !std::isfinite(re) || !box_rect(lo, hi, R)) R = all;
         mark(R, bit);
+    }
+    for (int32_t k = 0; k < H.n_box; ++k) {
+        const DObj& ob = H.objs[H.n_plane + H.n_sphere + k];
+        const uint32_t bit = 1u << (16 + (k & 15));
+        double lo[3], hi[3];
+        for (int a = 0; a < 3; ++a) {
+            const double p = 1e-5 * (std::fabs((double)ob.a[a]) + std::fabs((double)ob.b[a]) + std::fabs(o[a]));
+            lo[a] = std::min((double)ob.a[a], (double)ob.b[a]) - p;
+            hi[a] = std::max((double)ob.a[a], (double)ob.b[a]) + p;
+        }
+        sweep(ob, lo, hi);
+        Rect R;
+        if (H.n_box > 16 || !box_rect(lo, hi, R)) R = all;
+        mark(R, bit);
+    }
+    // hierarchy roots (rootmask bit q: the q-th root; the device tests later ones always):
+    // their hit boxes (compute_bounds' h over the frame's time range, world frame), padded
+    // like the boxes; an empty one is never hit, an unbounded one may be hit anywhere
+    rootmask.assign(nb, 0u);
+    {
+        int32_t q = 0;
+        for (int32_t r = 0; r < (int32_t)H.nodes.size() && r < (int32_t)nodeb.size(); r = H.nodes[r].end, ++q) {
+            if (q >= 32) break;
+            const DBound& B = nodeb[r];
+            double lo[3], hi[3];
+            bool empty = false, finite = true;
+            for (int a = 0; a < 3; ++a) {
+                empty = empty || !(B.hlo[a] <= B.hhi[a]);
+                finite = finite && std::isfinite(B.hlo[a]) && std::isfinite(B.hhi[a]);
+                const double p = 1e-5 * (std::fabs((double)B.hlo[a]) + std::fabs((double)B.hhi[a]) + std::fabs(o[a]));
+                lo[a] = (double)B.hlo[a] - p;
+                hi[a] = (double)B.hhi[a] + p;
+            }
+            if (empty) continue;
+            Rect R = all;
+            if (finite && !box_rect(lo, hi, R)) R = all;
+            mark_in(rootmask, R, 1u << q);
+        }
     }
     mesh_bins = 0;
     start.assign(nb + 1, 0);
@@ -1170,29 +1220,39 @@ bool light_grids(const HostScene& H, std::vector<DLGrid>& grids, std::vector<int
     return any;
 }
 
-// Shadow grids of directional lights (DSGrid, rtx_trace.h). Light li's shadow ray from p
-// is the half-line p + t d (d = fl32 -direction, LIGHT.negvec; t > 1e-4 or 1e-3). On two
-// fp32 unit vectors e1, e2 across d, its points project to p.e + t d.e: a hit point x of a
-// sphere or box (|x| <= Rx) projects within t |d.e| <= (Rx + |p|) |d.e| / |d| of p's
-// projection. So p's projection lies in the object's footprint (the projection of its
-// bounding box; of a sphere: c.e +- r |e|) grown by that drift, by the fuzz of the fp32
-// sphere discriminant (a ray can "hit" a sphere it misses by ~2^-10.5 |p - c|; grown by
-// 2^-8 (|p| + |c| + r), as primary_bins) and by 2^-18 of the magnitudes (the device's fp32
+// Shadow grids of directional lights (DSGrid, rtx_trace.h), per camera (the motion-time
+// range [tlo, thi] of the frame bounds the moving objects). Light li's shadow ray from p is
+// the half-line p + t d (d = fl32 -direction, LIGHT.negvec; t > 1e-4 or 1e-3). On two
+// fp32 unit vectors e1, e2 across d, its points project to p.e + t d.e: a hit point x of
+// an object (|x| <= Rx) projects within t |d.e| <= (Rx + |p|) |d.e| / |d| of p's
+// projection. So p's projection lies in the object's footprint -- the projection of its
+// bounding box (a sphere: c.e +- r |e|; a moving object: its box swept over the time
+// range; a hierarchy root: its shadow box, compute_bounds' s, outside of which its
+// shadow_intersect is false) -- grown by that drift, by the fuzz of the fp32 sphere
+// discriminant (a ray can "hit" a sphere it misses by ~2^-10.5 |p - c|; grown by 2^-8
+// (|p| + |c| + r), as primary_bins), and by 2^-18 of the magnitudes (the device's fp32
 // dot products and cell arithmetic); every cell the grown footprint meets, widened by one
 // cell, lists the object. The grid spans the footprints' union (with two spare cells a
-// side) for origins with max |p_i| <= pmax (5/4 of the objects' extent + 1); moving
-// objects, and objects beyond the 16th of a kind, are `always` tested.
-bool dir_shadow_grids(const HostScene& H, std::vector<DSGrid>& grids, std::vector<uint32_t>& masks) {
+// side) for origins with max |p_i| <= pmax (5/4 of the objects' extent + 1). Objects
+// beyond the 16th of a kind, and roots with unbounded shadow boxes, are `always` tested;
+// roots with empty ones never. nb: the nodes' bounds for [tlo, thi] (hierarchy scenes).
+bool dir_shadow_grids(const HostScene& H, const std::vector<DBound>& nb, double tlo, double thi,
+                      std::vector<DSGrid>& grids, std::vector<DSCell>& cells) {
     grids.assign(H.lights.size(), DSGrid{});
-    masks.clear();
+    cells.clear();
     struct Ob {
         double lo[3], hi[3];  // bounding box
-        double c[3], r;       // sphere: centre and radius (r < 0: a box)
-        uint32_t bit;
+        double c[3], r;       // a static sphere: centre and radius (r < 0: a box)
+        double fuzz;          // the sphere discriminant's fuzz applies (spheres, moving ones too)
+        uint32_t bit, root;   // DSCell bits
     };
     std::vector<Ob> obs;
-    uint32_t always = 0;
-    double R = 0.0;  // the largest |coordinate| of a static sphere's or box's bounds
+    uint32_t always = 0, always_root = 0;
+    double R = 0.0;  // the largest |coordinate| of the gridded bounds
+    auto keep = [&](Ob& o) {
+        for (int a = 0; a < 3; ++a) R = std::max(R, std::max(std::fabs(o.lo[a]), std::fabs(o.hi[a])));
+        obs.push_back(o);
+    };
     for (int32_t k = 0; k < H.n_sphere + H.n_box; ++k) {
         const bool sphere = k < H.n_sphere;
         const DObj& ob = H.objs[H.n_plane + k];
@@ -1200,25 +1260,55 @@ bool dir_shadow_grids(const HostScene& H, std::vector<DSGrid>& grids, std::vecto
         const uint32_t bit = 1u << ((sphere ? 0 : 16) + (j & 15));
         Ob o{};
         o.bit = bit;
-        o.r = sphere ? ob.radius : -1.0;
+        o.fuzz = sphere ? 1.0 : 0.0;
+        o.r = sphere && !ob.has_speed ? ob.radius : -1.0;
         for (int a = 0; a < 3; ++a) {
+            double lo, hi;
             if (sphere) {
+                lo = ob.a[a] - ob.radius;
+                hi = ob.a[a] + ob.radius;
                 o.c[a] = ob.a[a];
-                o.lo[a] = ob.a[a] - ob.radius;
-                o.hi[a] = ob.a[a] + ob.radius;
             } else {
-                o.lo[a] = std::min((double)ob.a[a], (double)ob.b[a]);
-                o.hi[a] = std::max((double)ob.a[a], (double)ob.b[a]);
+                lo = std::min((double)ob.a[a], (double)ob.b[a]);
+                hi = std::max((double)ob.a[a], (double)ob.b[a]);
             }
+            if (ob.has_speed) {  // moved(): p + speed * time in fp32, swept over [tlo, thi]
+                const double s0 = (double)ob.speed[a] * tlo, s1 = (double)ob.speed[a] * thi;
+                const double pad = 1e-5 * (std::fabs(lo) + std::fabs(hi) + std::fabs(s0) + std::fabs(s1));
+                lo += std::min(s0, s1) - pad;
+                hi += std::max(s0, s1) + pad;
+            }
+            o.lo[a] = lo;
+            o.hi[a] = hi;
         }
-        bool ok = !ob.has_speed && j < 16 && (sphere ? H.n_sphere : H.n_box) <= 16;
+        bool ok = j < 16 && (sphere ? H.n_sphere : H.n_box) <= 16;
         for (int a = 0; a < 3; ++a) ok = ok && std::isfinite(o.lo[a]) && std::isfinite(o.hi[a]);
         if (!ok) {
             always |= bit;
             continue;
         }
-        for (int a = 0; a < 3; ++a) R = std::max(R, std::max(std::fabs(o.lo[a]), std::fabs(o.hi[a])));
-        obs.push_back(o);
+        keep(o);
+    }
+    int32_t q = 0;
+    for (int32_t r = 0; r < (int32_t)H.nodes.size() && r < (int32_t)nb.size(); r = H.nodes[r].end, ++q) {
+        if (q >= 32) break;  // the device tests roots beyond the 32nd always
+        const DBound& B = nb[r];
+        Ob o{};
+        o.root = 1u << q;
+        o.r = -1.0;
+        bool empty = false, finite = true;
+        for (int a = 0; a < 3; ++a) {
+            o.lo[a] = B.slo[a];
+            o.hi[a] = B.shi[a];
+            empty = empty || !(B.slo[a] <= B.shi[a]);
+            finite = finite && std::isfinite(o.lo[a]) && std::isfinite(o.hi[a]);
+        }
+        if (empty) continue;  // shadow_intersect is false for every ray
+        if (!finite) {
+            always_root |= o.root;
+            continue;
+        }
+        keep(o);
     }
     if (obs.empty()) return false;
     int32_t G = 64;
@@ -1256,11 +1346,9 @@ bool dir_shadow_grids(const HostScene& H, std::vector<DSGrid>& grids, std::vecto
             double rx = 0.0;
             for (int q = 0; q < 3; ++q) rx += std::max(o.lo[q] * o.lo[q], o.hi[q] * o.hi[q]);
             rx = std::sqrt(rx);  // >= |x| of every point of the box
-            double pad = (rx + pm) * drift_rel + 0x1p-18 * (rx + pm);
+            double pad = (rx + pm) * drift_rel + 0x1p-18 * (rx + pm) + o.fuzz * 0x1p-8 * (pm + rx);
             double u0, u1, v0, v1;
             if (o.r >= 0.0) {
-                const double cm = std::sqrt(dot3(o.c, o.c));
-                pad += 0x1p-8 * (pm + cm + o.r);
                 const double cu = dot3(o.c, g1), cv = dot3(o.c, g2);
                 u0 = cu - o.r * len1; u1 = cu + o.r * len1;
                 v0 = cv - o.r * len2; v1 = cv + o.r * len2;
@@ -1293,9 +1381,10 @@ bool dir_shadow_grids(const HostScene& H, std::vector<DSGrid>& grids, std::vecto
         g.sv = (float)((G - 4) / wv);
         g.u0 = (float)(U0 - 2.0 / g.su);
         g.v0 = (float)(V0 - 2.0 / g.sv);
-        g.off = (int32_t)masks.size();
+        g.off = (int32_t)cells.size();
         g.always = always;
-        masks.resize(masks.size() + (size_t)G * G, 0u);
+        g.always_root = always_root;
+        cells.resize(cells.size() + (size_t)G * G, DSCell{0u, 0u});
         auto cell = [&](double u, double o0, double s) {  // as the device maps it, +-1 below
             return (int32_t)std::floor((u - o0) * s);
         };
@@ -1304,7 +1393,11 @@ bool dir_shadow_grids(const HostScene& H, std::vector<DSGrid>& grids, std::vecto
             const int32_t i0 = std::max(0, cell(F[0], g.u0, g.su) - 1), i1 = std::min(G - 1, cell(F[1], g.u0, g.su) + 1);
             const int32_t j0 = std::max(0, cell(F[2], g.v0, g.sv) - 1), j1 = std::min(G - 1, cell(F[3], g.v0, g.sv) + 1);
             for (int32_t jy = j0; jy <= j1; ++jy)
-                for (int32_t ix = i0; ix <= i1; ++ix) masks[(size_t)g.off + (size_t)jy * G + ix] |= obs[i].bit;
+                for (int32_t ix = i0; ix <= i1; ++ix) {
+                    DSCell& c = cells[(size_t)g.off + (size_t)jy * G + ix];
+                    c.obj |= obs[i].bit;
+                    c.root |= obs[i].root;
+                }
         }
         grids[li] = g;
         any = true;
@@ -1594,7 +1687,7 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
     if (sec && v.n_mats <= 64) opts.push_back("-DRTX_FRAME_MATBITS=6");
     opts.push_back(std::string("-DRTX_PRIMARY_BINS=") + (kp.S.bins_on ? "1" : "0"));
     opts.push_back(std::string("-DRTX_LIGHT_GRIDS=") + (v.lgrid_on ? "1" : "0"));
-    opts.push_back(std::string("-DRTX_DIR_GRIDS=") + (v.dsg_on ? "1" : "0"));
+    opts.push_back(std::string("-DRTX_DIR_GRIDS=") + (kp.S.dsg_on ? "1" : "0"));
     if (!ext && !spp) {  // experiment: per-lane object / material gathers from LDS (RTX_LDS_RECORDS=1)
         const char* e = getenv("RTX_LDS_RECORDS");
         const size_t bytes = (size_t)v.n_objs_all * sizeof(DObj) + (size_t)v.n_mats * sizeof(DMat);
@@ -1765,8 +1858,8 @@ struct rtx_scene {
     float* d_bin_zmin = nullptr;
     uint32_t* d_bin_mask = nullptr;
     void* d_lgrid = nullptr;        // light grids (per scene: lights and mesh are static)
-    void* d_dsgrid = nullptr;       // directional lights' shadow grids (per scene)
-    void* d_dsg_mask = nullptr;
+    void* d_dsgrid = nullptr;       // directional lights' shadow grids (per camera)
+    void* d_dsg_cells = nullptr;
     void* d_lg_start = nullptr;
     void* d_lg_faces = nullptr;
     void* d_lg_d2 = nullptr;
@@ -1840,6 +1933,9 @@ void free_camera(rtx_scene* s) {
     s->d_bin_mask = nullptr;
     (void)hipFree(s->d_bounds_cam);
     s->d_bounds_cam = nullptr;
+    (void)hipFree(s->d_dsgrid);
+    (void)hipFree(s->d_dsg_cells);
+    s->d_dsgrid = s->d_dsg_cells = nullptr;
     (void)hipFree(s->d_kp);
     (void)hipFree(s->d_tile_perm);
     (void)hipFree(s->d_tile_time);
@@ -1861,8 +1957,7 @@ void free_scene(rtx_scene* s) {
     (void)hipFree(s->d_split);
     (void)hipFree(s->d_split_count);
     for (void* p : {s->d_objs, s->d_tris, s->d_trins, s->d_fboxes, s->d_mats, s->d_lights, s->d_leaves, s->d_tri_orig, s->d_nodes, s->d_nmat,
-                    s->d_texels, s->d_lut, s->d_bounds_abi, s->d_lgrid, s->d_lg_start, s->d_lg_faces, s->d_lg_d2,
-                    s->d_dsgrid, s->d_dsg_mask})
+                    s->d_texels, s->d_lut, s->d_bounds_abi, s->d_lgrid, s->d_lg_start, s->d_lg_faces, s->d_lg_d2})
         (void)hipFree(p);
     delete s;
 }
@@ -1918,6 +2013,8 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
         if (H.n_mesh == 1) s->h_bins.tris = H.tris;
         s->h_bins.n_plane = H.n_plane; s->h_bins.n_sphere = H.n_sphere;
         s->h_bins.n_box = H.n_box; s->h_bins.n_mesh = H.n_mesh;
+        s->h_bins.lights = H.lights;  // and the shadow grids of directional lights
+        s->h_bins.nodes = H.nodes;
     }
     if (!H.nodes.empty()) {
         s->h_nodes = H.nodes;
@@ -1971,20 +2068,6 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
             v.lgrid_on = 1;
         }
     }
-    {  // shadow grids of directional lights (RTX_DSGRID=0: test every sphere and box)
-        std::vector<DSGrid> grids;
-        std::vector<uint32_t> masks;
-        const char* e = getenv("RTX_DSGRID");
-        if (!(e && e[0] == '0') && dir_shadow_grids(H, grids, masks)) {
-            if ((rc = upload(&s->d_dsgrid, grids)) || (rc = upload(&s->d_dsg_mask, masks))) {
-                free_scene(s);
-                return rc;
-            }
-            v.dsgrid = (cptr<DSGrid>)s->d_dsgrid;
-            v.dsg_mask = (cptr<uint32_t>)s->d_dsg_mask;
-            v.dsg_on = 1;
-        }
-    }
     *out = s;
     return RTX_OK;
 }
@@ -2016,20 +2099,32 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     if (c->jitter == RTX_JITTER_REPLAY && (rc = up(&s->d_noise, c->noise, 3 * (size_t)c->ncols * c->height * nsamp)))
         return rc;
     k.S = s->view;
+    const auto mm = std::minmax_element(times.begin(), times.end());
+    std::vector<DBound> nbounds;
     if (!s->h_nodes.empty()) {  // hierarchy bounds over the frame's motion-time range
-        const auto mm = std::minmax_element(times.begin(), times.end());
-        if ((rc = upload(&s->d_bounds_cam,
-                         split_bounds(compute_bounds(s->h_nodes, s->h_objs, s->h_tris, *mm.first, *mm.second)))))
-            return rc;
+        nbounds = compute_bounds(s->h_nodes, s->h_objs, s->h_tris, *mm.first, *mm.second);
+        if ((rc = upload(&s->d_bounds_cam, split_bounds(nbounds)))) return rc;
         bind_boxes(k.S, (const DBox*)s->d_bounds_cam, s->h_nodes.size());
+    }
+    {  // shadow grids of directional lights (RTX_DSGRID=0: every ray tests every object)
+        std::vector<DSGrid> grids;
+        std::vector<DSCell> cells;
+        const char* e = getenv("RTX_DSGRID");
+        if (!(e && e[0] == '0') && dir_shadow_grids(s->h_bins, nbounds, *mm.first, *mm.second, grids, cells)) {
+            if ((rc = upload(&s->d_dsgrid, grids)) || (rc = upload(&s->d_dsg_cells, cells))) return rc;
+            k.S.dsgrid = (cptr<DSGrid>)s->d_dsgrid;
+            k.S.dsg_cells = (cptr<DSCell>)s->d_dsg_cells;
+            k.S.dsg_on = 1;
+        }
     }
     {
         std::vector<int32_t> bstart, bfaces;
         std::vector<float> bz;
-        std::vector<uint32_t> bmask;
+        std::vector<uint32_t> bmask, brmask;
         int32_t bins_x = 0, mesh_bins = 0;
         const char* e = getenv("RTX_BINS");  // experiment: 0 = no primary-ray bins
-        if (!(e && e[0] == '0') && primary_bins(s->h_bins, c, bstart, bfaces, bz, bmask, bins_x, mesh_bins)) {
+        if (!(e && e[0] == '0') &&
+            primary_bins(s->h_bins, c, nbounds, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins)) {
             if (bfaces.empty()) { bfaces.push_back(0); bz.push_back(0.0f); }
             auto upi = [&](int32_t** d, const std::vector<int32_t>& h) -> int {
                 RTX_HIP(hipMalloc((void**)d, sizeof(int32_t) * h.size()));
@@ -2039,9 +2134,11 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
             if ((rc = upi(&s->d_bin_start, bstart)) || (rc = upi(&s->d_bin_faces, bfaces))) return rc;
             RTX_HIP(hipMalloc((void**)&s->d_bin_zmin, sizeof(float) * bz.size()));
             RTX_HIP(hipMemcpy(s->d_bin_zmin, bz.data(), sizeof(float) * bz.size(), hipMemcpyHostToDevice));
+            bmask.insert(bmask.end(), brmask.begin(), brmask.end());  // [object masks | root masks]
             RTX_HIP(hipMalloc((void**)&s->d_bin_mask, sizeof(uint32_t) * bmask.size()));
             RTX_HIP(hipMemcpy(s->d_bin_mask, bmask.data(), sizeof(uint32_t) * bmask.size(), hipMemcpyHostToDevice));
             k.S.bin_objmask = (cptr<uint32_t>)s->d_bin_mask;
+            k.S.bin_rootmask = (cptr<uint32_t>)s->d_bin_mask + brmask.size();
             k.S.mesh_bins = mesh_bins;
             k.S.bin_start = (cptr<int32_t>)s->d_bin_start;
             k.S.bin_faces = (cptr<int32_t>)s->d_bin_faces;

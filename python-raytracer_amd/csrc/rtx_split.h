@@ -86,12 +86,21 @@ RTX_HD void trace_sample(const KParams& P, const Launch& L, const SplitBuf& sb, 
     f3 d = normalize(sub(focal, ld3(P.dof_o + 3 * x.kd)));  // scene.py:58
     f3 o = sample_origin<JIT>(P, x.cc, x.j, x.kd, x.ka);
     const float time = P.times[x.kt];
+    // the primary-ray bin of the wave's pixels when they share one (rtx_api.hip primary_bins)
+    int32_t bin = -1;
+#if !(defined(RTX_PRIMARY_BINS) && !RTX_PRIMARY_BINS)
+    if (S.bins_on) {
+        const int32_t b = (image_row(L, x.rr) >> 3) * S.bins_x + (x.cc >> 3);
+        const int32_t b0 = wave_uniform(b);
+        bin = RTX_ALL(b == b0) ? b0 : -1;
+    }
+#endif
     int64_t slot = q, parent = -1;
     bool in_shape = false;
     for (int level = 0; level < (SEC ? kMaxDepth : 1); ++level) {
         if (COUNT) tl.cast[level]++;
         HHit hh;
-        const Hit h = closest_hit<MESH, true, COUNT>(S, o, d, time, tl, hs, hh);
+        const Hit h = closest_hit<MESH, true, COUNT>(S, o, d, time, tl, hs, hh, level == 0 ? bin : -1);
         const bool hit = h.obj != -1;
         if (level > 0) {  // a deeper hit is appended and linked from its parent
             slot = alloc(hit);

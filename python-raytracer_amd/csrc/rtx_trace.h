@@ -264,21 +264,25 @@ struct alignas(16) DLGrid {
     int32_t start_off, pad0;  // this light's G*G + 1 entries of lg_start
 };
 
-// Shadow grid of a directional light (rtx_api.hip dir_shadow_grids). The light's shadow
-// rays are parallel, so the spheres and boxes one of them can meet follow from where its
-// origin p projects on a plane across the light: cell (floor((p.e1 - u0) su),
-// floor((p.e2 - v0) sv)) of G x G lists them (bits: spheres 0-15, boxes 16-31). `always`:
-// objects every ray tests (moving ones, beyond 16 of a kind); origins off the grid test
-// only those, origins with max |p_i| > pmax test everything.
+// Shadow grid of a directional light (rtx_api.hip dir_shadow_grids, per camera). The
+// light's shadow rays are parallel, so the spheres, boxes and hierarchies one of them can
+// meet follow from where its origin p projects on a plane across the light: cell
+// (floor((p.e1 - u0) su), floor((p.e2 - v0) sv)) of G x G lists them (DSCell: obj bits =
+// spheres 0-15, boxes 16-31; root bits = hierarchy roots 0-31 in order). `always`: what
+// every ray tests (objects beyond the 16th of a kind, roots with unbounded shadow boxes);
+// origins off the grid test only those, origins with max |p_i| > pmax test everything.
+struct DSCell {
+    uint32_t obj, root;
+};
 struct alignas(16) DSGrid {
     float e1[3];
     int32_t G;  // cells per side; 0 = no grid for this light
     float e2[3];
     float pmax;
     float u0, v0, su, sv;
-    int32_t off;  // this light's G * G masks in dsg_mask
-    uint32_t always;
-    int32_t pad0, pad1;
+    int32_t off;  // this light's G * G cells in dsg_cells
+    uint32_t always, always_root;
+    int32_t pad0;
 };
 
 template <class T>
@@ -313,6 +317,7 @@ struct SceneView {
     cptr<int32_t> bin_faces;         // stored face indices (within the mesh), nearest first
     cptr<float> bin_zmin;            // per entry: a lower bound of any hit t on that face
     cptr<uint32_t> bin_objmask;      // per bin: spheres (bits 0-15) and boxes (16-31) a ray may hit
+    cptr<uint32_t> bin_rootmask;     // per bin: hierarchy roots (bit q: the q-th; later ones always)
     int32_t bins_x, bins_on, mesh_bins, pad5;
     int32_t n_objs_all, n_mats, pad6, pad7;  // object records (incl. hierarchy leaves), materials
     // Light grids (per light; shadow rays of point lights against the scene's one mesh)
@@ -323,7 +328,7 @@ struct SceneView {
     int32_t lgrid_on, pad8, pad9, pad10;
     // Shadow grids (per light; directional lights against the spheres and boxes)
     cptr<DSGrid> dsgrid;
-    cptr<uint32_t> dsg_mask;
+    cptr<DSCell> dsg_cells;
     int32_t dsg_on, pad11, pad12, pad13;
 };
 
@@ -1481,11 +1486,16 @@ RTX_HY bool hier_shadow(const SceneView& S, const HStack& hs, int r, f3 o, f3 d,
 // The shadow rays of every hierarchy root, for the lanes not yet occluded. (Out of line,
 // with hier_closest too, the kernel measured 247 VGPRs against 195 inlined: the calls cost
 // more registers than they isolate.)
+// rmask: the roots (bit q: the q-th, q < 32) the lane's ray may meet (DSGrid).
 template <bool MESH>
-RTX_HD bool hier_occluded(const SceneView& S, const HStack& hs, f3 o, f3 d, double t_max, float time, bool occ) {
-    for (int r = 0; r < S.n_nodes; r = S.nodes[r].end) {
+RTX_HD bool hier_occluded(const SceneView& S, const HStack& hs, f3 o, f3 d, double t_max, float time, bool occ,
+                          uint32_t rmask = ~0u) {
+    int q = 0;
+    for (int r = 0; r < S.n_nodes; r = S.nodes[r].end, ++q) {
         if (RTX_ALL(occ)) break;
-        if (!occ) occ = hier_shadow<MESH>(S, hs, r, o, d, t_max, time);
+        const bool live = !occ && (q >= 32 || ((rmask >> q) & 1u) != 0u);
+        if (!RTX_ANY(live)) continue;
+        if (live) occ = hier_shadow<MESH>(S, hs, r, o, d, t_max, time);
     }
     return occ;
 }
@@ -1503,8 +1513,10 @@ struct HHit {
 #ifndef RTX_HIER_FIRST
 #define RTX_HIER_FIRST 0  // nearest root first: measured slower (NovelScene1 29.1 -> 31.5 ms): off
 #endif
+// rmask: the roots (bit q: the q-th, q < 32) the wave's rays may hit (primary-ray bins).
 template <bool MESH>
-RTX_HY void hier_closest(const SceneView& S, const HStack& hs, f3 o, f3 d, float time, Hit& h, HHit& hh) {
+RTX_HY void hier_closest(const SceneView& S, const HStack& hs, f3 o, f3 d, float time, Hit& h, HHit& hh,
+                         uint32_t rmask = ~0u) {
     hs.put_ray(0, o, d);
     // The root whose hit box the wave's first ray enters first goes first: its hit then
     // caps the others' culling. Candidates compare by (t, top-level position), so the
@@ -1520,6 +1532,7 @@ RTX_HY void hier_closest(const SceneView& S, const HStack& hs, f3 o, f3 d, float
         }
     }
 #endif
+    int q = -1;  // the root's ordinal (when no root goes first)
     for (int k = first >= 0 ? -1 : 0; k < S.n_nodes;) {
         int r;
         if (k < 0) {
@@ -1530,6 +1543,8 @@ RTX_HY void hier_closest(const SceneView& S, const HStack& hs, f3 o, f3 d, float
             k = S.nodes[k].end;
             if (r == first) continue;  // visited first
         }
+        ++q;
+        if (first < 0 && q < 32 && !((rmask >> q) & 1u)) continue;  // the tile's rays miss its hit box
         const int32_t oid = S.nodes[r].oid;
         auto want = [&](double t) {
             const float t32 = (float)t;
@@ -1821,7 +1836,13 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
             }
         }
     }
-    if (X && RTX_ABLATE != 9) hier_closest<MESH>(S, hs, o, d, time, h, hh);  // hierarchies (hierarchy.py:42-78)
+    if (X && RTX_ABLATE != 9) {  // hierarchies (hierarchy.py:42-78)
+#if defined(RTX_PRIMARY_BINS) && !RTX_PRIMARY_BINS
+        hier_closest<MESH>(S, hs, o, d, time, h, hh);
+#else
+        hier_closest<MESH>(S, hs, o, d, time, h, hh, bin >= 0 ? S.bin_rootmask[wave_uniform(bin)] : ~0u);
+#endif
+    }
     return h;
 }
 
@@ -1892,20 +1913,23 @@ RTX_HD int32_t first_where(int32_t v, bool pred) {
 #endif
 }
 
-// The spheres and boxes directional light `light`'s shadow ray from p may meet (DSGrid);
-// ~0: all.
-RTX_HD uint32_t dir_shadow_mask(const SceneView& S, int light, f3 p) {
+// The spheres, boxes and hierarchy roots directional light `light`'s shadow ray from p may
+// meet (DSGrid); all bits: everything.
+RTX_HD DSCell dir_shadow_mask(const SceneView& S, int light, f3 p) {
     cref<DSGrid> g = S.dsgrid[light];
     const int32_t G = g.G;
-    if (G == 0) return ~0u;
+    if (G == 0) return DSCell{~0u, ~0u};
     const float m = fmaxf(fabsf(p.x), fmaxf(fabsf(p.y), fabsf(p.z)));
-    if (!(m <= g.pmax)) return ~0u;  // (NaN too)
+    if (!(m <= g.pmax)) return DSCell{~0u, ~0u};  // (NaN too)
     const float fx = (dot(p, mk(g.e1[0], g.e1[1], g.e1[2])) - g.u0) * g.su;
     const float fy = (dot(p, mk(g.e2[0], g.e2[1], g.e2[2])) - g.v0) * g.sv;
-    uint32_t msk = g.always;
-    if (fx >= 0.0f && fx < (float)G && fy >= 0.0f && fy < (float)G)
-        msk |= S.dsg_mask[g.off + (int32_t)fy * G + (int32_t)fx];
-    return msk;
+    DSCell c{g.always, g.always_root};
+    if (fx >= 0.0f && fx < (float)G && fy >= 0.0f && fy < (float)G) {
+        const DSCell q = S.dsg_cells[g.off + (int32_t)fy * G + (int32_t)fx];
+        c.obj |= q.obj;
+        c.root |= q.root;
+    }
+    return c;
 }
 
 #ifndef RTX_PLANE_SHADOW_RCP
@@ -1964,10 +1988,11 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
     }
     if (RTX_ALL(occ)) return true;
     // the spheres and boxes this lane's ray may meet: a directional light's shadow grid
-    uint32_t smask = ~0u;
+    DSCell sc{~0u, ~0u};
 #if !(defined(RTX_DIR_GRIDS) && !RTX_DIR_GRIDS)
-    if (light >= 0 && S.dsg_on && RTX_NSPHERE(S) + RTX_NBOX(S) > 0) smask = dir_shadow_mask(S, light, o);
+    if (light >= 0 && S.dsg_on) sc = dir_shadow_mask(S, light, o);
 #endif
+    const uint32_t smask = sc.obj;
     for (int k = 0; k < RTX_NSPHERE(S); ++k, ++oi) {  // simple_geometry.py:48-72 (shadow_epsilon 1e-3)
         if (RTX_ABLATE == 19) continue;  // cost probe: spheres never occlude
         const bool sl = ((smask >> (k & 15)) & 1u) != 0u;
@@ -2102,7 +2127,7 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
             }
         }
     }
-    if (X && RTX_ABLATE != 10) occ = hier_occluded<MESH>(S, hs, o, d, t_max, time, occ);  // hierarchy.py:80-109
+    if (X && RTX_ABLATE != 10) occ = hier_occluded<MESH>(S, hs, o, d, t_max, time, occ, sc.root);  // hierarchy.py:80-109
     return occ;
 }
 

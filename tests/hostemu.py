@@ -128,33 +128,35 @@ def occluded_light(scene, o, light, grids):
     return occ.astype(bool), cells
 
 
-def bins(scene, subimage=0, tasks=1):
+def bins(scene, subimage=0, tasks=1, roots=False):
     """The primary-ray bins rtx_camera_set builds (rtx_api.hip primary_bins): the object
     mask (uint32 [bins_y, bins_x]: spheres bits 0-15, boxes 16-31) and mesh-face count per
-    8x8 bin, or None when the camera has no bins."""
+    8x8 bin (roots=True: and the hierarchy-root mask), or None when the camera has none."""
     sd = scene.scene_desc()
     cd, tables = scene.camera_desc(subimage, tasks)
     bx, by = (cd.ncols + 7) // 8, (cd.height + 7) // 8
     mask = np.zeros(bx * by, np.uint32)
     nf = np.zeros(bx * by, np.int32)
+    rm = np.zeros(bx * by, np.uint32)
     f = lib().rtx_hostemu_bins
-    f.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
     f.restype = C.c_int64
-    n = f(C.addressof(sd), C.addressof(cd), mask.ctypes.data, nf.ctypes.data, bx * by)
+    n = f(C.addressof(sd), C.addressof(cd), mask.ctypes.data, nf.ctypes.data, rm.ctypes.data, bx * by)
     if n == 0:
         return None
     assert n == bx * by, n
-    return mask.reshape(by, bx), nf.reshape(by, bx)
+    out = (mask.reshape(by, bx), nf.reshape(by, bx))
+    return out + (rm.reshape(by, bx),) if roots else out
 
 
 def dir_shadow_mask(scene, p, light):
-    """The spheres (bits 0-15) and boxes (16-31) directional light ``light``'s shadow rays
-    from points p may meet by its shadow grid (uint32 per point, ~0: all), or None when the
-    light has no grid."""
+    """What directional light ``light``'s shadow rays from points p may meet by its shadow
+    grid (built for time 0): uint32 [n, 2] = (sphere bits 0-15 | box bits 16-31, hierarchy
+    root bits), all ones where everything is tested; None when the light has no grid."""
     sd = scene.scene_desc()
     p = np.ascontiguousarray(np.asarray(p, np.float32).reshape(-1, 3).T)
     n = p.shape[1]
-    out = np.zeros(n, np.uint32)
+    out = np.zeros((n, 2), np.uint32)
     f = lib().rtx_hostemu_dir_shadow_mask
     f.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_void_p]
     rc = f(C.addressof(sd), n, p.ctypes.data, light, out.ctypes.data)

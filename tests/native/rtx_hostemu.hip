@@ -41,10 +41,12 @@ void bind_view(const HostScene& H, SceneView& v) {
 struct Nodes {
     std::vector<DNodeHot> hot;
     std::vector<DNodeMat> mat;
+    std::vector<DBound> bounds;
     std::vector<DBox> boxes;
     void bind(const HostScene& H, SceneView& v, float tlo, float thi) {
         split_nodes(H.nodes, hot, mat);
-        boxes = split_bounds(compute_bounds(H.nodes, H.objs, H.tris, tlo, thi));
+        bounds = compute_bounds(H.nodes, H.objs, H.tris, tlo, thi);
+        boxes = split_bounds(bounds);
         v.nodes = (cptr<DNodeHot>)hot.data();
         v.nmat = (cptr<DNodeMat>)mat.data();
         bind_boxes(v, boxes.data(), H.nodes.size());
@@ -68,15 +70,19 @@ struct Grids {
     }
 };
 
-// The directional lights' shadow grids rtx_scene_create builds (RTX_DSGRID=0: none).
+// The directional lights' shadow grids rtx_camera_set builds for the motion-time range
+// [tlo, thi] (RTX_DSGRID=0: none).
 struct DirGrids {
     std::vector<DSGrid> grids;
-    std::vector<uint32_t> masks;
-    void bind(const HostScene& H, SceneView& v) {
+    std::vector<DSCell> cells;
+    void bind(const HostScene& H, SceneView& v, float tlo, float thi) {
         const char* e = getenv("RTX_DSGRID");
-        if ((e && e[0] == '0') || !dir_shadow_grids(H, grids, masks)) return;
+        if (e && e[0] == '0') return;
+        std::vector<DBound> nb;
+        if (!H.nodes.empty()) nb = compute_bounds(H.nodes, H.objs, H.tris, tlo, thi);
+        if (!dir_shadow_grids(H, nb, tlo, thi, grids, cells)) return;
         v.dsgrid = (cptr<DSGrid>)grids.data();
-        v.dsg_mask = (cptr<uint32_t>)masks.data();
+        v.dsg_cells = (cptr<DSCell>)cells.data();
         v.dsg_on = 1;
     }
 };
@@ -118,24 +124,25 @@ extern "C" int rtx_hostemu_render(const rtx_scene_desc* sd, const rtx_camera_des
     bind_view(H, k.S);
     Grids lg;
     lg.bind(H, k.S);
-    DirGrids dg;
-    dg.bind(H, k.S);
     std::vector<float> times(cd->n_times);
     for (int i = 0; i < cd->n_times; ++i) times[i] = (float)cd->times[i];
     const auto mm = std::minmax_element(times.begin(), times.end());
     Nodes nv;
     nv.bind(H, k.S, *mm.first, *mm.second);
+    DirGrids dg;
+    dg.bind(H, k.S, *mm.first, *mm.second);
     std::vector<int32_t> bstart, bfaces;
     std::vector<float> bz;
-    std::vector<uint32_t> bmask;
+    std::vector<uint32_t> bmask, brmask;
     int32_t bins_x = 0, mesh_bins = 0;
     const char* be = getenv("RTX_BINS");
-    if (!(be && be[0] == '0') && primary_bins(H, cd, bstart, bfaces, bz, bmask, bins_x, mesh_bins)) {
+    if (!(be && be[0] == '0') && primary_bins(H, cd, nv.bounds, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins)) {
         if (bfaces.empty()) { bfaces.push_back(0); bz.push_back(0.0f); }
         k.S.bin_start = (cptr<int32_t>)bstart.data();
         k.S.bin_faces = (cptr<int32_t>)bfaces.data();
         k.S.bin_zmin = (cptr<float>)bz.data();
         k.S.bin_objmask = (cptr<uint32_t>)bmask.data();
+        k.S.bin_rootmask = (cptr<uint32_t>)brmask.data();
         k.S.mesh_bins = mesh_bins;
         k.S.bins_x = bins_x;
         k.S.bins_on = 1;
@@ -186,24 +193,25 @@ extern "C" int rtx_hostemu_render_rows(const rtx_scene_desc* sd, const rtx_camer
     bind_view(H, k.S);
     Grids lg;
     lg.bind(H, k.S);
-    DirGrids dg;
-    dg.bind(H, k.S);
     std::vector<float> times(cd->n_times);
     for (int i = 0; i < cd->n_times; ++i) times[i] = (float)cd->times[i];
     const auto mm = std::minmax_element(times.begin(), times.end());
     Nodes nv;
     nv.bind(H, k.S, *mm.first, *mm.second);
+    DirGrids dg;
+    dg.bind(H, k.S, *mm.first, *mm.second);
     std::vector<int32_t> bstart, bfaces;
     std::vector<float> bz;
-    std::vector<uint32_t> bmask;
+    std::vector<uint32_t> bmask, brmask;
     int32_t bins_x = 0, mesh_bins = 0;
     const char* be = getenv("RTX_BINS");
-    if (!(be && be[0] == '0') && primary_bins(H, cd, bstart, bfaces, bz, bmask, bins_x, mesh_bins)) {
+    if (!(be && be[0] == '0') && primary_bins(H, cd, nv.bounds, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins)) {
         if (bfaces.empty()) { bfaces.push_back(0); bz.push_back(0.0f); }
         k.S.bin_start = (cptr<int32_t>)bstart.data();
         k.S.bin_faces = (cptr<int32_t>)bfaces.data();
         k.S.bin_zmin = (cptr<float>)bz.data();
         k.S.bin_objmask = (cptr<uint32_t>)bmask.data();
+        k.S.bin_rootmask = (cptr<uint32_t>)brmask.data();
         k.S.mesh_bins = mesh_bins;
         k.S.bins_x = bins_x;
         k.S.bins_on = 1;
@@ -321,7 +329,8 @@ extern "C" int rtx_hostemu_occluded_light(const rtx_scene_desc* sd, int64_t n, c
 
 // The spheres and boxes directional light `light`'s shadow rays from points ro may meet,
 // by its shadow grid (rtx_trace.h dir_shadow_mask; rtx_api.hip dir_shadow_grids): bits per
-// point, ~0 where every object is tested. Returns -1 if the light has no grid.
+// point (sphere/box bits, root bits), ~0 where everything is tested. Returns -1 if the
+// light has no grid. The grid is built for time 0.
 extern "C" int rtx_hostemu_dir_shadow_mask(const rtx_scene_desc* sd, int64_t n, const float* ro, int32_t light,
                                            uint32_t* mask) {
     HostScene H;
@@ -331,9 +340,13 @@ extern "C" int rtx_hostemu_dir_shadow_mask(const rtx_scene_desc* sd, int64_t n, 
     SceneView v{};
     bind_view(H, v);
     DirGrids dg;
-    dg.bind(H, v);
+    dg.bind(H, v, 0.0f, 0.0f);
     if (!v.dsg_on || dg.grids[light].G == 0) return -1;
-    for (int64_t i = 0; i < n; ++i) mask[i] = dir_shadow_mask(v, light, mk(ro[i], ro[n + i], ro[2 * n + i]));
+    for (int64_t i = 0; i < n; ++i) {
+        const DSCell c = dir_shadow_mask(v, light, mk(ro[i], ro[n + i], ro[2 * n + i]));
+        mask[2 * i] = c.obj;
+        mask[2 * i + 1] = c.root;
+    }
     return RTX_OK;
 }
 
@@ -445,14 +458,20 @@ extern "C" int64_t rtx_hostemu_jit_spec(const rtx_scene_desc* sd, const rtx_came
     k.S.n_leaves = (int32_t)H.leaves.size();
     Grids lg;
     lg.bind(H, k.S);
+    std::vector<float> tms(cd->n_times);
+    for (int i = 0; i < cd->n_times; ++i) tms[i] = (float)cd->times[i];
+    const auto tmm = std::minmax_element(tms.begin(), tms.end());
     DirGrids dg;
-    dg.bind(H, k.S);
+    dg.bind(H, k.S, *tmm.first, *tmm.second);
     std::vector<int32_t> bstart, bfaces;
     std::vector<float> bz;
-    std::vector<uint32_t> bmask;
+    std::vector<uint32_t> bmask, brmask;
     int32_t bins_x = 0, mesh_bins = 0;
     const char* be = getenv("RTX_BINS");
-    if (!(be && be[0] == '0') && primary_bins(H, cd, bstart, bfaces, bz, bmask, bins_x, mesh_bins)) k.S.bins_on = 1;
+    std::vector<DBound> nodeb;
+    if (!H.nodes.empty()) nodeb = compute_bounds(H.nodes, H.objs, H.tris, *tmm.first, *tmm.second);
+    if (!(be && be[0] == '0') && primary_bins(H, cd, nodeb, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins))
+        k.S.bins_on = 1;
     const int spp = k.n_dof * k.n_aa * k.n_times;
     const bool spp_mode = use_spp_mode(spp, H.has_ext);
     JitSpec sp;
@@ -544,13 +563,29 @@ extern "C" int rtx_hostemu_render_split(const rtx_scene_desc* sd, const rtx_came
     bind_view(H, k.S);
     Grids lg;
     lg.bind(H, k.S);
-    DirGrids dg;
-    dg.bind(H, k.S);
     std::vector<float> times(cd->n_times);
     for (int i = 0; i < cd->n_times; ++i) times[i] = (float)cd->times[i];
     const auto mm = std::minmax_element(times.begin(), times.end());
     Nodes nv;
     nv.bind(H, k.S, *mm.first, *mm.second);
+    DirGrids dg;
+    dg.bind(H, k.S, *mm.first, *mm.second);
+    std::vector<int32_t> bstart, bfaces;
+    std::vector<float> bz;
+    std::vector<uint32_t> bmask, brmask;
+    int32_t bins_x = 0, mesh_bins = 0;
+    const char* be = getenv("RTX_BINS");
+    if (!(be && be[0] == '0') && primary_bins(H, cd, nv.bounds, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins)) {
+        if (bfaces.empty()) { bfaces.push_back(0); bz.push_back(0.0f); }
+        k.S.bin_start = (cptr<int32_t>)bstart.data();
+        k.S.bin_faces = (cptr<int32_t>)bfaces.data();
+        k.S.bin_zmin = (cptr<float>)bz.data();
+        k.S.bin_objmask = (cptr<uint32_t>)bmask.data();
+        k.S.bin_rootmask = (cptr<uint32_t>)brmask.data();
+        k.S.mesh_bins = mesh_bins;
+        k.S.bins_x = bins_x;
+        k.S.bins_on = 1;
+    }
     std::vector<float> noise;
     const size_t nsamp = (size_t)cd->n_dof * cd->n_aa;
     if (cd->jitter == RTX_JITTER_REPLAY) noise.assign(cd->noise, cd->noise + 3 * (size_t)cd->ncols * cd->height * nsamp);
@@ -583,18 +618,24 @@ extern "C" int rtx_hostemu_render_split(const rtx_scene_desc* sd, const rtx_came
 // 8x8 tile its sphere/box mask and its number of candidate mesh faces. Returns the number
 // of bins (0: the camera has none).
 extern "C" int64_t rtx_hostemu_bins(const rtx_scene_desc* sd, const rtx_camera_desc* cd, uint32_t* mask,
-                                    int32_t* nfaces, int64_t cap) {
+                                    int32_t* nfaces, uint32_t* rmask, int64_t cap) {
     HostScene H;
     if (convert_scene(sd, H)) return -1;
     std::vector<int32_t> bstart, bfaces;
     std::vector<float> bz;
-    std::vector<uint32_t> bmask;
+    std::vector<uint32_t> bmask, brmask;
     int32_t bins_x = 0, mesh_bins = 0;
-    if (!primary_bins(H, cd, bstart, bfaces, bz, bmask, bins_x, mesh_bins)) return 0;
+    std::vector<float> tms(cd->n_times);
+    for (int i = 0; i < cd->n_times; ++i) tms[i] = (float)cd->times[i];
+    const auto tmm = std::minmax_element(tms.begin(), tms.end());
+    std::vector<DBound> nodeb;
+    if (!H.nodes.empty()) nodeb = compute_bounds(H.nodes, H.objs, H.tris, *tmm.first, *tmm.second);
+    if (!primary_bins(H, cd, nodeb, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins)) return 0;
     const int64_t n = (int64_t)bmask.size();
     for (int64_t b = 0; b < n && b < cap; ++b) {
         mask[b] = bmask[b];
         nfaces[b] = mesh_bins && b + 1 < (int64_t)bstart.size() ? bstart[b + 1] - bstart[b] : 0;
+        if (rmask) rmask[b] = brmask[b];
     }
     return n;
 }

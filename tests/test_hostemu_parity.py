@@ -488,10 +488,11 @@ def _lens_ray_scene(seed, pinhole=False):
     return d
 
 
-def _lens_ray_misses(d, mask):
+def _lens_ray_misses(d, mask, rmask=None):
     """Primary sample rays of scene d's lens camera (the DOF origin's focal direction from
     the jittered AA origin, scene.py:54-65, set up in fp32 like the device) whose closest
-    hit is a sphere or box missing from their tile's mask: (misses, rays that hit one)."""
+    hit is a sphere or box (rmask given: or a hierarchy root) missing from their tile's
+    mask: (misses, rays that hit one)."""
     from common import product_scene_dict
     sc = product_scene_dict(d)
     cd, t = sc.camera_desc()
@@ -521,12 +522,15 @@ def _lens_ray_misses(d, mask):
     prow = (H - 1 - np.broadcast_to(jj[:, :, None, None], (W, H, nd, na))).ravel()
     misses = tested = 0
     for i, k in enumerate(kinds):
-        if k not in ("sphere", "box"):
+        if k in ("sphere", "box"):
+            m, bt = mask, (0 if k == "sphere" else 16) + sum(1 for q in kinds[:i] if q == k)
+        elif k == "node" and rmask is not None:
+            m, bt = rmask, sum(1 for q in kinds[:i] if q == "node")
+        else:
             continue
-        bt = (0 if k == "sphere" else 16) + sum(1 for q in kinds[:i] if q == k)
         sel = hit == i
         tested += int(sel.sum())
-        misses += int((((mask[prow[sel] >> 3, pc[sel] >> 3] >> bt) & 1) == 0).sum())
+        misses += int((((m[prow[sel] >> 3, pc[sel] >> 3] >> np.uint32(bt)) & 1) == 0).sum())
     return misses, tested
 
 
@@ -542,6 +546,26 @@ def test_lens_bins_hold_every_sample_ray(seed):
         assert d["DOF"]["aperture"] > 0.05 * d["DOF"]["focal_length"], d["DOF"]
         return
     misses, tested = _lens_ray_misses(d, b[0])
+    assert misses == 0, (misses, tested)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_root_bins_hold_every_sample_ray(seed):
+    """Primary-ray bins of hierarchy roots (their hit boxes) and of moving objects (swept
+    over the frame's times), ray by ray: every primary sample ray of a random CSG scene --
+    pinhole or lens camera, AA jitter -- whose closest hit is a root, sphere or box finds
+    it in its tile's masks."""
+    from common import product_scene_dict
+    from scenegen import random_hier_scene
+    d = random_hier_scene(seed, res=(64, 48))
+    d.pop("motion", None)  # rays at time 0
+    d["objects"] = [o for o in d["objects"] if "ref" not in o]  # (objects map to scene positions)
+    if seed % 2:
+        d["DOF"] = {"aperture": 0.15, "focal_length": 5.0, "samples": 3}
+        d["AA"] = {"jitter": True, "samples": 2}
+    b = hostemu.bins(product_scene_dict(d), roots=True)
+    assert b is not None
+    misses, tested = _lens_ray_misses(d, b[0], b[2])
     assert misses == 0, (misses, tested)
 
 
@@ -590,18 +614,13 @@ def _shadow_probe_points(d, rng, n_obj=400):
     return np.concatenate(pts).astype(np.float32)
 
 
-@pytest.mark.parametrize("seed", range(16))
-def test_hostemu_dir_shadow_grids_hold_every_ray(seed):
-    """Directional shadow grids, ray by ray: wherever a sphere or box alone occludes a
-    directional light's shadow ray (the device's own test, objects one at a time), the
-    grid's mask for the ray's origin lists it; moving objects are listed everywhere."""
+def _check_dir_shadow_grid(d, p, what):
+    """Wherever one sphere, box or hierarchy root of scene d alone occludes a directional
+    light's shadow ray from a point of p (the device's own test, at time 0), the light's
+    grid lists it for that point. Returns the number of occluded (ray, object) pairs."""
     import copy
     from common import product_scene_dict
-    from scenegen import shadow_scene
-    d = shadow_scene(seed)
     sc = product_scene_dict(d)
-    rng = np.random.RandomState(seed)
-    p = _shadow_probe_points(d, rng)
     sd = sc.scene_desc()
     kinds = [o["type"] for o in d["objects"]]
     checked = 0
@@ -612,20 +631,47 @@ def test_hostemu_dir_shadow_grids_hold_every_ray(seed):
         assert mask is not None
         dvec = -np.asarray(sd.lights[li].vector[:3], np.float32)  # the light's negvec, as the device casts it
         for i, o in enumerate(d["objects"]):
-            if o["type"] not in ("sphere", "box"):
+            if o["type"] in ("sphere", "box"):
+                word, bt = 0, (0 if o["type"] == "sphere" else 16) + sum(1 for q in kinds[:i] if q == o["type"])
+            elif o["type"] == "node":
+                word, bt = 1, sum(1 for q in kinds[:i] if q == "node")
+            else:
                 continue
-            bt = (0 if o["type"] == "sphere" else 16) + sum(1 for q in kinds[:i] if q == o["type"])
-            has = ((mask >> np.uint32(bt)) & 1).astype(bool)
-            if "speed" in o:
-                assert has.all(), (seed, li, i)
-                continue
+            has = ((mask[:, word] >> np.uint32(bt)) & 1).astype(bool)
             one = copy.deepcopy(d)
             one["objects"] = [copy.deepcopy(o)]
             one.pop("motion", None)
             occ = hostemu.occluded(product_scene_dict(one), p, np.broadcast_to(dvec, p.shape), np.inf, 0.0)
-            assert not (occ & ~has).any(), (seed, li, i, int((occ & ~has).sum()), int(occ.sum()))
+            assert not (occ & ~has).any(), (what, li, i, int((occ & ~has).sum()), int(occ.sum()))
             checked += int(occ.sum())
-    assert checked > 0
+    return checked
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_hostemu_dir_shadow_grids_hold_every_ray(seed):
+    """Directional shadow grids, ray by ray, on spheres and boxes (static and moving)."""
+    from scenegen import shadow_scene
+    d = shadow_scene(seed)
+    p = _shadow_probe_points(d, np.random.RandomState(seed))
+    assert _check_dir_shadow_grid(d, p, "seed %d" % seed) > 0
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_hostemu_dir_shadow_grids_hold_every_ray_hierarchies(seed):
+    """Directional shadow grids, ray by ray, on hierarchy roots (their shadow boxes):
+    random CSG trees under diagonal, vertical and random directional lights."""
+    from scenegen import random_hier_scene
+    d = random_hier_scene(seed)
+    d["objects"] = [o for o in d["objects"] if "ref" not in o]  # (a copy needs its source in the scene)
+    d["lights"] = [{"name": "d%d" % k, "type": "directional", "direction": v, "colour": [1.0, 1.0, 1.0], "power": 0.5}
+                   for k, v in enumerate([[1.0, -1.0, -1.0], [0.0, -1.0, 0.0], [-0.3, 0.2, 0.9]])]
+    rng = np.random.RandomState(seed)
+    near = rng.uniform(-3.5, 3.5, (6000, 3))
+    p = [near, rng.uniform(-12, 12, (2000, 3))]
+    for l in d["lights"]:
+        u = -np.asarray(l["direction"]) / np.linalg.norm(l["direction"])
+        p.append(near - u * rng.uniform(0.001, 8.0, (len(near), 1)))
+    assert _check_dir_shadow_grid(d, np.concatenate(p).astype(np.float32), "hier seed %d" % seed) > 0
 
 
 def test_hostemu_dir_shadow_grids_skip_most_rays():
@@ -637,7 +683,7 @@ def test_hostemu_dir_shadow_grids_skip_most_rays():
         p = np.c_[rng.uniform(-6, 6, (4000, 1)), np.zeros((4000, 1)), rng.uniform(-8, 3, (4000, 1))].astype(np.float32)
         m = hostemu.dir_shadow_mask(sc, p, 0)
         assert m is not None
-        assert (m == 0).mean() > 0.6, (name, float((m == 0).mean()))
+        assert (m[:, 0] == 0).mean() > 0.6, (name, float((m[:, 0] == 0).mean()))
 
 
 @pytest.mark.parametrize("seed", range(12))
