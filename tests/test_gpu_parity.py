@@ -570,6 +570,7 @@ def test_dir_shadow_grids_equal_walk(seed, monkeypatch):
     object (RTX_DSGRID=0) == oracle, 160x120 frames."""
     from common import oracle_render_dict, product_scene_dict
     from scenegen import shadow_scene
+    monkeypatch.setenv("RTX_DSGRID_MIN", "1")  # a grid for every scene, however few its spheres
     d = shadow_scene(seed, res=(160, 120))
     a = product_scene_dict(d).render_device().clone()
     monkeypatch.setenv("RTX_DSGRID", "0")
@@ -584,7 +585,9 @@ def test_dir_shadow_grids_equal_walk(seed, monkeypatch):
                                             ("MirrorRefraction", (1920, 1080), {})])
 def test_dir_shadow_grids_full_frames(name, res, edits, monkeypatch):
     """The BASELINE configs with directional lights, with their shadow grids and without:
-    the same frames, bit for bit."""
+    the same frames, bit for bit (MirrorRefraction's four spheres get a grid only when
+    RTX_DSGRID_MIN allows it)."""
+    monkeypatch.setenv("RTX_DSGRID_MIN", "1")
     a = product_scene(name, res, **edits).render_device().clone()
     monkeypatch.setenv("RTX_DSGRID", "0")
     b = product_scene(name, res, **edits).render_device().clone()

@@ -648,8 +648,10 @@ def _check_dir_shadow_grid(d, p, what):
 
 
 @pytest.mark.parametrize("seed", range(16))
-def test_hostemu_dir_shadow_grids_hold_every_ray(seed):
-    """Directional shadow grids, ray by ray, on spheres and boxes (static and moving)."""
+def test_hostemu_dir_shadow_grids_hold_every_ray(seed, monkeypatch):
+    """Directional shadow grids, ray by ray, on spheres and boxes (static and moving; a
+    grid for every scene, however few its spheres)."""
+    monkeypatch.setenv("RTX_DSGRID_MIN", "1")
     from scenegen import shadow_scene
     d = shadow_scene(seed)
     p = _shadow_probe_points(d, np.random.RandomState(seed))
@@ -657,10 +659,11 @@ def test_hostemu_dir_shadow_grids_hold_every_ray(seed):
 
 
 @pytest.mark.parametrize("seed", range(12))
-def test_hostemu_dir_shadow_grids_hold_every_ray_hierarchies(seed):
+def test_hostemu_dir_shadow_grids_hold_every_ray_hierarchies(seed, monkeypatch):
     """Directional shadow grids, ray by ray, on hierarchy roots (their shadow boxes):
     random CSG trees under diagonal, vertical and random directional lights."""
     from scenegen import random_hier_scene
+    monkeypatch.setenv("RTX_DSGRID_MIN", "1")
     d = random_hier_scene(seed)
     d["objects"] = [o for o in d["objects"] if "ref" not in o]  # (a copy needs its source in the scene)
     d["lights"] = [{"name": "d%d" % k, "type": "directional", "direction": v, "colour": [1.0, 1.0, 1.0], "power": 0.5}
@@ -674,14 +677,16 @@ def test_hostemu_dir_shadow_grids_hold_every_ray_hierarchies(seed):
     assert _check_dir_shadow_grid(d, np.concatenate(p).astype(np.float32), "hier seed %d" % seed) > 0
 
 
-def test_hostemu_dir_shadow_grids_skip_most_rays():
-    """The grids are tight enough to pay: on DepthOfField and MirrorRefraction most
-    floor points' shadow rays test no sphere or box."""
+def test_hostemu_dir_shadow_grids_skip_most_rays(monkeypatch):
+    """The grids are tight enough to pay: on DepthOfField (and on MirrorRefraction, whose
+    four spheres alone get no grid unless RTX_DSGRID_MIN allows it) most floor points'
+    shadow rays test no sphere or box."""
+    rng = np.random.RandomState(1)
+    p = np.c_[rng.uniform(-6, 6, (4000, 1)), np.zeros((4000, 1)), rng.uniform(-8, 3, (4000, 1))].astype(np.float32)
+    assert hostemu.dir_shadow_mask(product_scene("MirrorRefraction", (8, 8)), p, 0) is None
+    monkeypatch.setenv("RTX_DSGRID_MIN", "1")
     for name in ("DepthOfField", "MirrorRefraction"):
-        sc = product_scene(name, (8, 8))
-        rng = np.random.RandomState(1)
-        p = np.c_[rng.uniform(-6, 6, (4000, 1)), np.zeros((4000, 1)), rng.uniform(-8, 3, (4000, 1))].astype(np.float32)
-        m = hostemu.dir_shadow_mask(sc, p, 0)
+        m = hostemu.dir_shadow_mask(product_scene(name, (8, 8)), p, 0)
         assert m is not None
         assert (m[:, 0] == 0).mean() > 0.6, (name, float((m[:, 0] == 0).mean()))
 
@@ -691,6 +696,7 @@ def test_hostemu_dir_shadow_grids_equal_walk(seed, monkeypatch):
     """Frames with the directional shadow grids == without (RTX_DSGRID=0) == the oracle."""
     from common import oracle_render_dict, product_scene_dict
     from scenegen import shadow_scene
+    monkeypatch.setenv("RTX_DSGRID_MIN", "1")
     d = shadow_scene(seed)
     img, cnt = hostemu.render(product_scene_dict(d))
     monkeypatch.setenv("RTX_DSGRID", "0")
