@@ -105,6 +105,39 @@ def shadow_scene(seed, res=(40, 30)):
     return sc
 
 
+def many_roots_scene(seed, res=(48, 32), n_roots=40, n_spheres=20):
+    """More hierarchy roots than the 32 bits of a bin or shadow-grid cell, and more spheres
+    than the 16 a mask holds: the ones beyond are tested by every ray. A lens camera with
+    AA jitter, a directional and a point light."""
+    rng = np.random.RandomState(9000 + seed)
+    r = lambda lo, hi, n=None: np.round(rng.uniform(lo, hi, n), 3).tolist()  # noqa: E731
+    mats = [{"name": "m%d" % i, "ID": i, "diffuse": r(0, 1, 3), "specular": r(0, 1, 3), "hardness": 16}
+            for i in range(3)]
+    objs = [{"name": "ground", "type": "plane", "normal": [0.0, 1.0, 0.0], "position": [0.0, -1.0, 0.0],
+             "materials": [0, 1]}]
+    for k in range(n_roots):
+        kids = [{"name": "c%d_%d" % (k, j), "type": "sphere", "radius": float(r(0.1, 0.35)),
+                 "position": r(-0.3, 0.3, 3)} for j in range(2)]
+        if rng.rand() < 0.3:
+            kids.append({"name": "cb%d" % k, "type": "box", "size": r(0.2, 0.5, 3), "position": r(-0.2, 0.2, 3)})
+        n = {"name": "n%d" % k, "type": "node", "hierarchy_type": str(rng.choice(["union", "intersection"])),
+             "position": r(-5, 5, 3), "materials": [int(rng.randint(3))], "children": kids}
+        if rng.rand() < 0.2:
+            n["speed"] = r(-0.3, 0.3, 3)
+        objs.append(n)
+    for k in range(n_spheres):
+        objs.append({"name": "s%d" % k, "type": "sphere", "radius": float(r(0.1, 0.5)), "position": r(-5, 5, 3),
+                     "materials": [int(rng.randint(3))]})
+    order = rng.permutation(len(objs))
+    return {"resolution": list(res), "AA": {"jitter": True, "samples": 2}, "ambient": [0.1, 0.1, 0.1],
+            "DOF": {"aperture": 0.1, "focal_length": 8.0, "samples": 2},
+            "camera": {"position": [0.0, 4.0, 12.0], "lookAt": [0.0, 0.0, 0.0], "up": [0.0, 1.0, 0.0], "fov": 60.0},
+            "materials": mats, "objects": [objs[i] for i in order],
+            "lights": [{"name": "d", "type": "directional", "direction": [1.0, -1.0, -0.5], "colour": [1.0, 1.0, 1.0],
+                        "power": 0.7},
+                       {"name": "p", "type": "point", "position": [3.0, 6.0, 4.0], "colour": [1.0, 1.0, 1.0], "power": 0.5}]}
+
+
 def tie_scene(res=(40, 30)):
     """Coincident geometry: the first object in scene order must win closest-hit ties."""
     return {"resolution": list(res), "ambient": [0.1, 0.1, 0.1],

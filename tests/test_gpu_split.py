@@ -84,3 +84,23 @@ def test_split_equals_one_kernel_full_novel_scene1(monkeypatch):
     torch.cuda.synchronize()
     assert one.startswith("k_render_ext") and sc.last_kernel.startswith("k_split_"), (one, sc.last_kernel)
     assert torch.equal(a, b), float((a != b).float().mean())
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_split_many_roots_bins_and_grids(seed, split, monkeypatch):
+    """40 hierarchy roots and 20 flat spheres (beyond the 32 root bits and 16 sphere bits
+    of the bins and shadow-grid cells), lens camera with Philox jitter: the split passes
+    with bins and grids == without == the oracle."""
+    from scenegen import many_roots_scene
+    from oracle import philox as PH
+    d = many_roots_scene(seed, res=(96, 64))
+    sc = product_scene_dict(d)
+    a = sc.render_device().clone()
+    assert sc.last_kernel.startswith("k_split_"), sc.last_kernel
+    monkeypatch.setenv("RTX_BINS", "0")
+    monkeypatch.setenv("RTX_DSGRID", "0")
+    b = product_scene_dict(d).render_device().clone()
+    assert torch.equal(a, b)
+    img = np.ascontiguousarray(np.transpose(a.cpu().numpy()[::-1], (1, 0, 2))).astype(np.float64)
+    noise = PH.jitter_noise(sc.seed, 0, 96, 64, sc.vc.dof_samples, sc.samples)
+    assert_parity(img, oracle_render_dict(d, noise=noise), "many roots seed %d" % seed)

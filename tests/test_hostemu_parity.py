@@ -569,6 +569,25 @@ def test_root_bins_hold_every_sample_ray(seed):
     assert misses == 0, (misses, tested)
 
 
+@pytest.mark.parametrize("seed", range(2))
+def test_hostemu_many_roots_bins_and_grids(seed, monkeypatch):
+    """40 hierarchy roots and 20 flat spheres -- beyond the 32 root bits and 16 sphere bits
+    of the bins and shadow-grid cells: bins and grids on == both off == the oracle (with
+    the restated Philox stream), one-kernel and split forms."""
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import many_roots_scene
+    d = many_roots_scene(seed)
+    sc = product_scene_dict(d)
+    assert hostemu.bins(sc, roots=True) is not None
+    img, _ = hostemu.render(sc)
+    split, _ = hostemu.render_split(sc)
+    monkeypatch.setenv("RTX_BINS", "0")
+    monkeypatch.setenv("RTX_DSGRID", "0")
+    walk, _ = hostemu.render(product_scene_dict(d))
+    assert np.array_equal(img, walk) and np.array_equal(split, walk)
+    assert_parity(img, oracle_render_dict(d, noise=_lens_noise(sc)), "many roots seed %d" % seed)
+
+
 def test_lens_ray_check_is_sensitive():
     """The ray check above fails the pinhole bins (no lens growth) of the same scenes:
     lens rays do leave the pinhole footprint, so the growth is what holds them."""
