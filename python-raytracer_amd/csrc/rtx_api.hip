@@ -2346,9 +2346,13 @@ int tile_schedule(rtx_scene* s, hipStream_t st) {
 
 // Records per chunk ($RTX_SPLIT_RECORDS, default 2^26 = 4 GiB of 64-B records): a chunk
 // takes as many whole pixels as fit when every sample fills every chain level.
+// Records per chunk of the split passes (64 B each; a chunk reserves every sample's
+// deepest chain). 2^28 (16 GiB of the 288 GB) measured faster than 2^26 and 2^27 --
+// fewer, longer launches: NovelScene1 16.97 -> 16.12 ms, NovelScene2 76.7 -> 70.5 ms
+// (profiles/r04/split_records/); $RTX_SPLIT_RECORDS lowers it.
 int64_t split_records() {
     const char* e = getenv("RTX_SPLIT_RECORDS");
-    const long long v = (e && *e) ? atoll(e) : (1ll << 26);
+    const long long v = (e && *e) ? atoll(e) : (1ll << 28);
     return std::min<long long>(std::max<long long>(v, 1024), 1ll << 30);
 }
 
