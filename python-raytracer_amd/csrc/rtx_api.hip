@@ -766,6 +766,19 @@ int convert_camera(const rtx_camera_desc* c, KParams& k) {
     return RTX_OK;
 }
 
+// An upper bound of |o| for every camera ray origin (AA/DOF origins plus jitter); +inf if
+// a table is not finite.
+double camera_origin_bound(const rtx_camera_desc* c) {
+    double m = 0.0;
+    const int64_t n = (int64_t)c->n_dof * c->n_aa;
+    for (int64_t i = 0; i < n; ++i) {
+        const float* p = c->aa_origins + 3 * i;
+        m = std::max(m, std::sqrt((double)p[0] * p[0] + (double)p[1] * p[1] + (double)p[2] * p[2]));
+    }
+    if (c->jitter != RTX_JITTER_OFF) m += std::fabs(c->jitter_scale) * (1.0 + 1e-5);
+    return std::isfinite(m) ? m * (1.0 + 1e-6) : INFINITY;
+}
+
 // $RTX_LENS_BINS=0: lens cameras get no primary-ray bins (experiment, A/B)
 bool lens_bins_disabled() {
     const char* e = getenv("RTX_LENS_BINS");
@@ -1236,7 +1249,17 @@ bool light_grids(const HostScene& H, std::vector<DLGrid>& grids, std::vector<int
 // side) for origins with max |p_i| <= pmax (5/4 of the objects' extent + 1). Objects
 // beyond the 16th of a kind, and roots with unbounded shadow boxes, are `always` tested;
 // roots with empty ones never. nb: the nodes' bounds for [tlo, thi] (hierarchy scenes).
-bool dir_shadow_grids(const HostScene& H, const std::vector<DBound>& nb, double tlo, double thi,
+//
+// Self tests. A camera ray's closest hit on a static box B sits at P = fl32(o + d t32),
+// within delta <= 2^-23 (|P| + |o|) + 2^-24 |P| (the roundings of t32, d t32 and the sum)
+// of the exact ray point at the reference's entry t, which lies on B's boundary. A shadow
+// ray P + t D can then enter B only at t <= delta / |D_a| for an axis a with P outside B's
+// slab (inside B every slab entry is <= 0), so B occludes it only if delta / min |D_a|
+// (over D_a != 0) exceeds 1e-4. self_boxes marks the boxes where 2^-21 (|P|max + |o|max)
+// -- twice the bound -- stays below 1e-4 min |D_a| / 2: their own shadow test cannot pass
+// for such a hit point and is skipped. omax bounds |o| of the camera's sample origins
+// (camera_origin_bound).
+bool dir_shadow_grids(const HostScene& H, const std::vector<DBound>& nb, double tlo, double thi, double omax,
                       std::vector<DSGrid>& grids, std::vector<DSCell>& cells) {
     grids.assign(H.lights.size(), DSGrid{});
     cells.clear();
@@ -1394,6 +1417,23 @@ bool dir_shadow_grids(const HostScene& H, const std::vector<DBound>& nb, double 
         g.off = (int32_t)cells.size();
         g.always = always;
         g.always_root = always_root;
+        double dmin = INFINITY;
+        for (int q = 0; q < 3; ++q)
+            if (d[q] != 0.0) dmin = std::min(dmin, std::fabs(d[q]));
+        const char* es = getenv("RTX_SELF_SKIP");  // experiment: 0 = every box tests itself
+        if (H.n_box <= 16 && std::isfinite(omax) && !(es && es[0] == '0')) {
+            for (int32_t k = 0; k < H.n_box; ++k) {
+                const DObj& ob = H.objs[H.n_plane + H.n_sphere + k];
+                if (ob.has_speed) continue;
+                double pm = 0.0;
+                for (int q = 0; q < 3; ++q) {
+                    const double m = std::max(std::fabs((double)ob.a[q]), std::fabs((double)ob.b[q]));
+                    pm += m * m;
+                }
+                const double delta = 0x1p-21 * (std::sqrt(pm) + omax);
+                if (2.0 * delta < 1e-4 * dmin) g.self_boxes |= 1u << (16 + k);
+            }
+        }
         cells.resize(cells.size() + (size_t)G * G, DSCell{0u, 0u});
         auto cell = [&](double u, double o0, double s) {  // as the device maps it, +-1 below
             return (int32_t)std::floor((u - o0) * s);
@@ -2120,7 +2160,8 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
         std::vector<DSGrid> grids;
         std::vector<DSCell> cells;
         const char* e = getenv("RTX_DSGRID");
-        if (!(e && e[0] == '0') && dir_shadow_grids(s->h_bins, nbounds, *mm.first, *mm.second, grids, cells)) {
+        if (!(e && e[0] == '0') &&
+            dir_shadow_grids(s->h_bins, nbounds, *mm.first, *mm.second, camera_origin_bound(c), grids, cells)) {
             if ((rc = upload(&s->d_dsgrid, grids)) || (rc = upload(&s->d_dsg_cells, cells))) return rc;
             k.S.dsgrid = (cptr<DSGrid>)s->d_dsgrid;
             k.S.dsg_cells = (cptr<DSCell>)s->d_dsg_cells;

@@ -282,7 +282,9 @@ struct alignas(16) DSGrid {
     float u0, v0, su, sv;
     int32_t off;  // this light's G * G cells in dsg_cells
     uint32_t always, always_root;
-    int32_t pad0;
+    // boxes (bits 16-31) whose own shadow test a camera ray's hit point on them may skip:
+    // it cannot pass (rtx_api.hip dir_shadow_grids)
+    uint32_t self_boxes;
 };
 
 template <class T>
@@ -1940,7 +1942,7 @@ RTX_HD DSCell dir_shadow_mask(const SceneView& S, int light, f3 p) {
 // light grid, if any, may stand in for the mesh's BVH walk).
 template <bool MESH, bool X, bool COUNT>
 RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, Tally& tl, const HStack& hs,
-                     const OriginTerms* ot = nullptr, int light = -1) {
+                     const OriginTerms* ot = nullptr, int light = -1, int32_t self_obj = -1) {
     const float tmax32 = (float)t_max;
     // the floats around t_max (both tmax32 for the shader's 1.0 and inf)
     const float tmax_dn = (double)tmax32 > t_max ? nextafterf(tmax32, -INFINITY) : tmax32;
@@ -1989,8 +1991,12 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
     if (RTX_ALL(occ)) return true;
     // the spheres and boxes this lane's ray may meet: a directional light's shadow grid
     DSCell sc{~0u, ~0u};
+    uint32_t self_boxes = 0u;  // (self_obj: the flat object a camera ray hit at o, or -1)
 #if !(defined(RTX_DIR_GRIDS) && !RTX_DIR_GRIDS)
-    if (light >= 0 && S.dsg_on) sc = dir_shadow_mask(S, light, o);
+    if (light >= 0 && S.dsg_on) {
+        sc = dir_shadow_mask(S, light, o);
+        self_boxes = S.dsgrid[light].self_boxes;
+    }
 #endif
     const uint32_t smask = sc.obj;
     for (int k = 0; k < RTX_NSPHERE(S); ++k, ++oi) {  // simple_geometry.py:48-72 (shadow_epsilon 1e-3)
@@ -2039,7 +2045,7 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
     }
     for (int k = 0; k < RTX_NBOX(S); ++k, ++oi) {  // simple_geometry.py:251-294
         if (RTX_ABLATE == 20) continue;  // cost probe: boxes never occlude
-        const bool sl = ((smask >> (16 + (k & 15))) & 1u) != 0u;
+        const bool sl = ((smask >> (16 + (k & 15))) & 1u) != 0u && !(oi == self_obj && k < 16 && ((self_boxes >> (16 + k)) & 1u));
         if (!RTX_ANY(sl && !occ)) continue;
         const DObj ob = S.objs[oi];
         const f3 mn = moved(ob, ob.a, time), mx = moved(ob, ob.b, time);
@@ -2240,7 +2246,7 @@ RTX_HD double spec_pow(double x, const DMat& m, int pow_bits) {
 // shadow ray is occluded, as a separate pass found it; no shadow ray is traced here.
 template <bool MESH, bool X, bool COUNT>
 RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const DMat& m, f3 diffuse, float time,
-                           Tally& tl, const HStack& hs, int64_t occ_mask = -1) {
+                           Tally& tl, const HStack& hs, int64_t occ_mask = -1, int32_t self_obj = -1) {
     f3 colour = mk(0.0f, 0.0f, 0.0f);
     tally_inc<COUNT>(tl, &Tally::shade);
     OriginTerms ot;
@@ -2269,7 +2275,7 @@ RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const 
         tally_inc<COUNT>(tl, &Tally::shadow);
         if (occ_mask >= 0) {
             if ((occ_mask >> li) & 1) continue;
-        } else if (RTX_ABLATE != 1 && occluded<MESH, X, COUNT>(S, pos, sdir, t_max, time, tl, hs, otp, li)) {
+        } else if (RTX_ABLATE != 1 && occluded<MESH, X, COUNT>(S, pos, sdir, t_max, time, tl, hs, otp, li, self_obj)) {
             continue;
         }
         if (RTX_ABLATE == 3) { colour = add(colour, mul(ld3(L.cp), diffuse)); continue; }
@@ -2375,7 +2381,9 @@ RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const 
         if ((RTX_ABLATE == 2 || RTX_ABLATE == 7) && !chain) { tail = ld3(m.diffuse); break; }
         // scene.py:143-146: Plane/AABB hits shade with get_diffuse(position)
         const f3 diffuse = (X && sf.gobj >= 0) ? get_diffuse(S, S.objs[sf.gobj], sf.position, time) : ld3(m.diffuse);
-        const f3 L = regular_lighting<MESH, X, COUNT>(S, d, sf.position, n, m, diffuse, time, tl, hs);
+        // a camera ray's hit (level 0) tells occluded which flat object it lies on
+        const f3 L = regular_lighting<MESH, X, COUNT>(S, d, sf.position, n, m, diffuse, time, tl, hs, -1,
+                                                      level == 0 ? h.obj : -1);
         if (!SEC || !chain) {
             tail = clamp01(L);
             break;

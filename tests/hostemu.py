@@ -166,6 +166,18 @@ def dir_shadow_mask(scene, p, light):
     return out
 
 
+def dsgrid_self(scene, light, subimage=0, tasks=1):
+    """The boxes (bits 16-31) whose own shadow test toward directional light ``light`` a
+    camera ray's hit on them skips (DSGrid.self_boxes), or None without a grid."""
+    sd = scene.scene_desc()
+    cd, tables = scene.camera_desc(subimage, tasks)
+    f = lib().rtx_hostemu_dsgrid_self
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
+    f.restype = C.c_int64
+    r = f(C.addressof(sd), C.addressof(cd), light)
+    return None if r < 0 else int(r)
+
+
 def philox(ctr, key):
     """The device's Philox4x32-10 of one counter (4 uint32) and key (k0, k1)."""
     c = np.ascontiguousarray(np.asarray(ctr, np.uint32))

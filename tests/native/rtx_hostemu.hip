@@ -75,12 +75,12 @@ struct Grids {
 struct DirGrids {
     std::vector<DSGrid> grids;
     std::vector<DSCell> cells;
-    void bind(const HostScene& H, SceneView& v, float tlo, float thi) {
+    void bind(const HostScene& H, SceneView& v, float tlo, float thi, double omax = INFINITY) {
         const char* e = getenv("RTX_DSGRID");
         if (e && e[0] == '0') return;
         std::vector<DBound> nb;
         if (!H.nodes.empty()) nb = compute_bounds(H.nodes, H.objs, H.tris, tlo, thi);
-        if (!dir_shadow_grids(H, nb, tlo, thi, grids, cells)) return;
+        if (!dir_shadow_grids(H, nb, tlo, thi, omax, grids, cells)) return;
         v.dsgrid = (cptr<DSGrid>)grids.data();
         v.dsg_cells = (cptr<DSCell>)cells.data();
         v.dsg_on = 1;
@@ -130,7 +130,7 @@ extern "C" int rtx_hostemu_render(const rtx_scene_desc* sd, const rtx_camera_des
     Nodes nv;
     nv.bind(H, k.S, *mm.first, *mm.second);
     DirGrids dg;
-    dg.bind(H, k.S, *mm.first, *mm.second);
+    dg.bind(H, k.S, *mm.first, *mm.second, camera_origin_bound(cd));
     std::vector<int32_t> bstart, bfaces;
     std::vector<float> bz;
     std::vector<uint32_t> bmask, brmask;
@@ -199,7 +199,7 @@ extern "C" int rtx_hostemu_render_rows(const rtx_scene_desc* sd, const rtx_camer
     Nodes nv;
     nv.bind(H, k.S, *mm.first, *mm.second);
     DirGrids dg;
-    dg.bind(H, k.S, *mm.first, *mm.second);
+    dg.bind(H, k.S, *mm.first, *mm.second, camera_origin_bound(cd));
     std::vector<int32_t> bstart, bfaces;
     std::vector<float> bz;
     std::vector<uint32_t> bmask, brmask;
@@ -350,6 +350,22 @@ extern "C" int rtx_hostemu_dir_shadow_mask(const rtx_scene_desc* sd, int64_t n, 
     return RTX_OK;
 }
 
+// The boxes (bits 16-31) whose own shadow test a camera ray's hit on them skips, for
+// directional light `light` and this camera (DSGrid::self_boxes); -1: no grid.
+extern "C" int64_t rtx_hostemu_dsgrid_self(const rtx_scene_desc* sd, const rtx_camera_desc* cd, int32_t light) {
+    HostScene H;
+    if (convert_scene(sd, H)) return -1;
+    std::vector<float> tms(cd->n_times);
+    for (int i = 0; i < cd->n_times; ++i) tms[i] = (float)cd->times[i];
+    const auto tmm = std::minmax_element(tms.begin(), tms.end());
+    SceneView v{};
+    bind_view(H, v);
+    DirGrids dg;
+    dg.bind(H, v, *tmm.first, *tmm.second, camera_origin_bound(cd));
+    if (!v.dsg_on || light < 0 || light >= (int32_t)dg.grids.size() || dg.grids[light].G == 0) return -1;
+    return (int64_t)dg.grids[light].self_boxes;
+}
+
 // Light grid statistics (tests and tuning): per light G, list entries, the longest list
 // and the non-empty cells; zeros for a light without a grid.
 extern "C" int rtx_hostemu_lgrid_stats(const rtx_scene_desc* sd, int64_t* out) {
@@ -462,7 +478,7 @@ extern "C" int64_t rtx_hostemu_jit_spec(const rtx_scene_desc* sd, const rtx_came
     for (int i = 0; i < cd->n_times; ++i) tms[i] = (float)cd->times[i];
     const auto tmm = std::minmax_element(tms.begin(), tms.end());
     DirGrids dg;
-    dg.bind(H, k.S, *tmm.first, *tmm.second);
+    dg.bind(H, k.S, *tmm.first, *tmm.second, camera_origin_bound(cd));
     std::vector<int32_t> bstart, bfaces;
     std::vector<float> bz;
     std::vector<uint32_t> bmask, brmask;
@@ -569,7 +585,7 @@ extern "C" int rtx_hostemu_render_split(const rtx_scene_desc* sd, const rtx_came
     Nodes nv;
     nv.bind(H, k.S, *mm.first, *mm.second);
     DirGrids dg;
-    dg.bind(H, k.S, *mm.first, *mm.second);
+    dg.bind(H, k.S, *mm.first, *mm.second, camera_origin_bound(cd));
     std::vector<int32_t> bstart, bfaces;
     std::vector<float> bz;
     std::vector<uint32_t> bmask, brmask;

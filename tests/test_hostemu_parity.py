@@ -696,6 +696,100 @@ def test_hostemu_dir_shadow_grids_hold_every_ray_hierarchies(seed, monkeypatch):
     assert _check_dir_shadow_grid(d, np.concatenate(p).astype(np.float32), "hier seed %d" % seed) > 0
 
 
+@pytest.mark.parametrize("seed", list(range(8)) + ["dof"])
+def test_hostemu_box_self_shadow_never_passes(seed):
+    """The skipped self tests (DSGrid.self_boxes): rays from the camera's sample origins
+    aimed at random points of each marked box -- faces, edges, corners, grazing -- hit it
+    at fp32 points from which that box alone never occludes the light's shadow ray (the
+    device's own test); the marks hold."""
+    import copy
+    from common import product_scene_dict
+    from rtx.io import bundled_scene_dict
+    from scenegen import shadow_scene
+    if seed == "dof":
+        d = bundled_scene_dict("DepthOfField", resolution=(64, 48))
+        d["AA"] = {"jitter": True, "samples": 2}
+    else:
+        d = shadow_scene(seed)
+    sc = product_scene_dict(d)
+    sd = sc.scene_desc()
+    cd, t = sc.camera_desc()
+    rng = np.random.RandomState(11)
+    aa = np.asarray(t["aa"], np.float64).reshape(-1, 3)
+    boxes = [i for i, o in enumerate(d["objects"]) if o["type"] == "box"]
+    marked = 0
+    for li, l in enumerate(d["lights"]):
+        if l["type"] != "directional":
+            continue
+        bits = hostemu.dsgrid_self(sc, li)
+        if not bits:
+            continue
+        dvec = -np.asarray(sd.lights[li].vector[:3], np.float32)
+        for k, i in enumerate(boxes):
+            if not (bits >> (16 + k)) & 1:
+                continue
+            o = d["objects"][i]
+            if "min" in o:
+                mn, mx = np.minimum(o["min"], o["max"]), np.maximum(o["min"], o["max"])
+            else:
+                mn = np.asarray(o["position"]) - np.asarray(o["size"]) / 2
+                mx = np.asarray(o["position"]) + np.asarray(o["size"]) / 2
+            n = 6000
+            tgt = rng.uniform(mn, mx, (n, 3))
+            ax = rng.randint(3, size=n)
+            tgt[np.arange(n), ax] = np.where(rng.rand(n) < 0.5, mn[ax], mx[ax])  # on a face
+            edge = rng.rand(n) < 0.3
+            ax2 = (ax + 1) % 3
+            tgt[edge, ax2[edge]] = np.where(rng.rand(edge.sum()) < 0.5, mn[ax2[edge]], mx[ax2[edge]])
+            org = aa[rng.randint(len(aa), size=n)] + rng.normal(size=(n, 3)) * 0.3 * float(t["jscale"])
+            dr = tgt - org
+            dr /= np.linalg.norm(dr, axis=1, keepdims=True)
+            hit = hostemu.intersect(sc, org.astype(np.float32), dr.astype(np.float32))
+            on = hit["obj"] == i
+            one = copy.deepcopy(d)
+            one["objects"] = [copy.deepcopy(o)]
+            occ = hostemu.occluded(product_scene_dict(one), hit["position"][on], np.broadcast_to(dvec, (int(on.sum()), 3)),
+                                   np.inf, 0.0)
+            assert not occ.any(), (seed, li, k, int(on.sum()), int(occ.sum()))
+            marked += int(on.sum())  # (a box inside another object takes no hits)
+    assert marked > 1000 or seed not in ("dof", 1)
+
+
+def test_hostemu_box_self_shadow_grazing_light_not_marked():
+    """Under a grazing light (direction y = 1e-5) a box's own shadow test does pass for
+    some camera hits on its top face (fp32 points just above it): such boxes must not be
+    marked, and are not."""
+    import copy
+    from common import product_scene_dict
+    from scenegen import shadow_scene
+    d = shadow_scene(1)
+    d["lights"] = [{"name": "g", "type": "directional", "direction": [1.0, 1e-5, 0.3], "colour": [1.0, 1.0, 1.0],
+                    "power": 0.7}]
+    sc = product_scene_dict(d)
+    assert hostemu.dsgrid_self(sc, 0) == 0
+    cd, t = sc.camera_desc()
+    aa = np.asarray(t["aa"], np.float64).reshape(-1, 3)
+    rng = np.random.RandomState(1)
+    dvec = -np.asarray(sc.scene_desc().lights[0].vector[:3], np.float32)
+    self_occ = 0
+    for i, o in enumerate(d["objects"]):
+        if o["type"] != "box" or "speed" in o:
+            continue
+        mn = np.minimum(o["min"], o["max"]) if "min" in o else np.asarray(o["position"]) - np.asarray(o["size"]) / 2
+        mx = np.maximum(o["min"], o["max"]) if "min" in o else np.asarray(o["position"]) + np.asarray(o["size"]) / 2
+        tgt = rng.uniform(mn, mx, (20000, 3))
+        tgt[:, 1] = mx[1]
+        org = aa[rng.randint(len(aa), size=20000)]
+        dr = (tgt - org) / np.linalg.norm(tgt - org, axis=1, keepdims=True)
+        hit = hostemu.intersect(sc, org.astype(np.float32), dr.astype(np.float32))
+        on = hit["obj"] == i
+        one = copy.deepcopy(d)
+        one["objects"] = [copy.deepcopy(o)]
+        self_occ += int(hostemu.occluded(product_scene_dict(one), hit["position"][on],
+                                         np.broadcast_to(dvec, (int(on.sum()), 3)), np.inf, 0.0).sum())
+    assert self_occ > 0
+
+
 def test_hostemu_dir_shadow_grids_skip_most_rays(monkeypatch):
     """The grids are tight enough to pay: on DepthOfField (and on MirrorRefraction, whose
     four spheres alone get no grid unless RTX_DSGRID_MIN allows it) most floor points'
