@@ -779,6 +779,58 @@ double camera_origin_bound(const rtx_camera_desc* c) {
     return std::isfinite(m) ? m * (1.0 + 1e-6) : INFINITY;
 }
 
+// Self tests of planes (SceneView::plane_self). A camera ray (origin o, |o| <= omax) hits
+// static plane k (point p0, normal n) at P = fl32(o + d t32), t32 = fl32(num0 / den0) of
+// fp32 dot products. With num0 = num + A, den0 = den + B (their roundings),
+//   t32 den - num = A + e (num + A) - t32 B  (exactly; e: the quotient's rounding),
+// and |t32 B| <= 2^-22 |n|_1 |P - o|: so P's offset from the plane, (P - p0).n, stays
+// within 2^-20 |n|_1 (|p0|_1 + |o|_1 + |P|_1) however grazing the ray, and the shadow
+// test's own num' = fl32((p0 - P).n) within 2^-19 |n|_1 (...) =: b0 + b1 m (m = max |P_i|,
+// |P|_1 <= 3m, |o|_1 <= 3 omax). The test needs 1e-4 < num' / denom' to pass; denom' =
+// fl32(D.n) is at least c0 - c1 m (directional D: |D.n| less its rounding; point light
+// L: |(L - p0).n| less P's offset and the roundings of L - P and the dot). So for
+// m < (0.5e-4 c0 - b0) / (b1 + 0.5e-4 c1) the plane cannot occlude its own hit point
+// (|num' / denom'| < 0.5e-4). Returns [light][plane < 4] limits (-1: none).
+std::vector<float> plane_self_limits(const HostScene& H, double omax) {
+    std::vector<float> lim(4 * H.lights.size(), -1.0f);
+    if (!std::isfinite(omax)) return lim;
+    for (size_t li = 0; li < H.lights.size(); ++li) {
+        const DLight& Lt = H.lights[li];
+        for (int32_t k = 0; k < std::min(H.n_plane, 4); ++k) {
+            const DObj& ob = H.objs[k];
+            if (ob.has_speed) continue;
+            double n1 = 0.0, p01 = 0.0, h = 0.0, dabs = 0.0, l1 = 0.0;
+            for (int a = 0; a < 3; ++a) {
+                n1 += std::fabs((double)ob.b[a]);
+                p01 += std::fabs((double)ob.a[a]);
+            }
+            const double b0 = 0x1p-19 * n1 * (p01 + 3.0 * omax), b1 = 0x1p-19 * n1 * 3.0;
+            double c0, c1;
+            if (Lt.type == LIGHT_DIRECTIONAL) {
+                for (int a = 0; a < 3; ++a) {
+                    h += (double)Lt.negvec[a] * ob.b[a];
+                    dabs += std::fabs((double)Lt.negvec[a] * ob.b[a]);
+                }
+                c0 = std::fabs(h) - 0x1p-21 * dabs;
+                c1 = 0.0;
+            } else {
+                for (int a = 0; a < 3; ++a) {
+                    h += ((double)Lt.vec[a] - ob.a[a]) * ob.b[a];
+                    l1 += std::fabs((double)Lt.vec[a]);
+                }
+                c0 = std::fabs(h) * (1.0 - 1e-12) - b0 - 0x1p-21 * n1 * l1;
+                c1 = b1 + 0x1p-21 * n1 * 3.0;
+            }
+            const double m = (0.5e-4 * c0 - b0) / (b1 + 0.5e-4 * c1);
+            if (!(m > 0.0) || !std::isfinite(m)) continue;
+            float f = (float)(m * (1.0 - 1e-6));
+            if ((double)f > m) f = std::nextafter(f, 0.0f);
+            lim[4 * li + k] = f;
+        }
+    }
+    return lim;
+}
+
 // $RTX_LENS_BINS=0: lens cameras get no primary-ray bins (experiment, A/B)
 bool lens_bins_disabled() {
     const char* e = getenv("RTX_LENS_BINS");
@@ -1910,6 +1962,7 @@ struct rtx_scene {
     void* d_lgrid = nullptr;        // light grids (per scene: lights and mesh are static)
     void* d_dsgrid = nullptr;       // directional lights' shadow grids (per camera)
     void* d_dsg_cells = nullptr;
+    void* d_plane_self = nullptr;   // self tests of planes (per camera)
     void* d_lg_start = nullptr;
     void* d_lg_faces = nullptr;
     void* d_lg_d2 = nullptr;
@@ -1985,7 +2038,8 @@ void free_camera(rtx_scene* s) {
     s->d_bounds_cam = nullptr;
     (void)hipFree(s->d_dsgrid);
     (void)hipFree(s->d_dsg_cells);
-    s->d_dsgrid = s->d_dsg_cells = nullptr;
+    (void)hipFree(s->d_plane_self);
+    s->d_dsgrid = s->d_dsg_cells = s->d_plane_self = nullptr;
     (void)hipFree(s->d_kp);
     (void)hipFree(s->d_tile_perm);
     (void)hipFree(s->d_tile_time);
@@ -2155,6 +2209,13 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
         nbounds = compute_bounds(s->h_nodes, s->h_objs, s->h_tris, *mm.first, *mm.second);
         if ((rc = upload(&s->d_bounds_cam, split_bounds(nbounds)))) return rc;
         bind_boxes(k.S, (const DBox*)s->d_bounds_cam, s->h_nodes.size());
+    }
+    {  // self tests of planes (RTX_SELF_SKIP=0: none)
+        const char* es = getenv("RTX_SELF_SKIP");
+        if (!(es && es[0] == '0') && s->view.n_plane > 0 && !s->h_bins.lights.empty()) {
+            if ((rc = upload(&s->d_plane_self, plane_self_limits(s->h_bins, camera_origin_bound(c))))) return rc;
+            k.S.plane_self = (cptr<float>)s->d_plane_self;
+        }
     }
     {  // shadow grids of directional lights (RTX_DSGRID=0: every ray tests every object)
         std::vector<DSGrid> grids;

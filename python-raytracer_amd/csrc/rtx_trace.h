@@ -332,6 +332,10 @@ struct SceneView {
     cptr<DSGrid> dsgrid;
     cptr<DSCell> dsg_cells;
     int32_t dsg_on, pad11, pad12, pad13;
+    // Self tests of planes (per camera; rtx_api.hip plane_self_limits): [light][plane < 4]
+    // the largest max |p_i| of a camera ray's hit point p on that plane whose own shadow
+    // test toward the light cannot pass (-1: none); null: no skips
+    cptr<float> plane_self;
 };
 
 // Mesh records read by the hot BVH walks (closest_hit / occluded). Scene-specialized
@@ -1950,8 +1954,17 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
     const float tmax_lim = nextafterf(tmax_dn, -INFINITY);  // a float strictly below t_max
     bool occ = false;
     int oi = 0;
+    // self tests of planes (SceneView::plane_self) for a lane that hit plane self_obj
+    cptr<float> pself = nullptr;
+    float pm = INFINITY;
+    if (light >= 0 && S.plane_self != nullptr && RTX_NPLANE(S) > 0) {  // (wave-uniform)
+        pself = S.plane_self + 4 * light;
+        pm = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
+    }
     for (int k = 0; k < RTX_NPLANE(S); ++k, ++oi) {  // simple_geometry.py:122-131
         if (RTX_ABLATE == 21) continue;  // cost probe: planes never occlude
+        // a camera hit on this plane, close enough to the origin: its own test cannot pass
+        if (pself != nullptr && k < 4 && RTX_ALL(occ || (oi == self_obj && pm <= pself[k]))) continue;
         const DObj ob = S.objs[oi];
         const f3 n = ld3(ob.b);
         const float denom = dot(d, n);

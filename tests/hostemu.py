@@ -178,6 +178,18 @@ def dsgrid_self(scene, light, subimage=0, tasks=1):
     return None if r < 0 else int(r)
 
 
+def plane_self(scene):
+    """The planes' self-test limits for this camera (rtx_api.hip plane_self_limits):
+    float32 [n_lights, 4], -1 where a plane's own shadow test is always run."""
+    sd = scene.scene_desc()
+    cd, tables = scene.camera_desc()
+    out = np.zeros((sd.n_lights, 4), np.float32)
+    f = lib().rtx_hostemu_plane_self
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    _chk(f(C.addressof(sd), C.addressof(cd), out.ctypes.data))
+    return out
+
+
 def philox(ctr, key):
     """The device's Philox4x32-10 of one counter (4 uint32) and key (k0, k1)."""
     c = np.ascontiguousarray(np.asarray(ctr, np.uint32))

@@ -75,7 +75,13 @@ struct Grids {
 struct DirGrids {
     std::vector<DSGrid> grids;
     std::vector<DSCell> cells;
+    std::vector<float> pself;
     void bind(const HostScene& H, SceneView& v, float tlo, float thi, double omax = INFINITY) {
+        const char* es = getenv("RTX_SELF_SKIP");  // the planes' self tests, as rtx_camera_set
+        if (!(es && es[0] == '0') && H.n_plane > 0 && !H.lights.empty()) {
+            pself = plane_self_limits(H, omax);
+            v.plane_self = (cptr<float>)pself.data();
+        }
         const char* e = getenv("RTX_DSGRID");
         if (e && e[0] == '0') return;
         std::vector<DBound> nb;
@@ -364,6 +370,16 @@ extern "C" int64_t rtx_hostemu_dsgrid_self(const rtx_scene_desc* sd, const rtx_c
     dg.bind(H, v, *tmm.first, *tmm.second, camera_origin_bound(cd));
     if (!v.dsg_on || light < 0 || light >= (int32_t)dg.grids.size() || dg.grids[light].G == 0) return -1;
     return (int64_t)dg.grids[light].self_boxes;
+}
+
+// The planes' self-test limits rtx_camera_set builds for this camera (plane_self_limits):
+// out[light * 4 + plane], -1 where none.
+extern "C" int rtx_hostemu_plane_self(const rtx_scene_desc* sd, const rtx_camera_desc* cd, float* out) {
+    HostScene H;
+    if (int rc = convert_scene(sd, H)) return rc;
+    const std::vector<float> lim = plane_self_limits(H, camera_origin_bound(cd));
+    std::copy(lim.begin(), lim.end(), out);
+    return RTX_OK;
 }
 
 // Light grid statistics (tests and tuning): per light G, list entries, the longest list

@@ -790,6 +790,81 @@ def test_hostemu_box_self_shadow_grazing_light_not_marked():
     assert self_occ > 0
 
 
+@pytest.mark.parametrize("case", ["TwoSpheresPlane", "DepthOfField", "MirrorRefraction", "rand0", "rand1", "rand2",
+                                  "rand3", "shadow0", "shadow1", "lowlight"])
+def test_hostemu_plane_self_shadow_never_passes(case):
+    """The skipped self tests of planes (SceneView::plane_self): camera rays from the
+    sample origins hit each plane near and far, head-on and grazing; wherever the hit
+    point's max |p_i| is within the light's limit, the plane alone never occludes the
+    point's shadow ray toward that light (the device's own test, d and t_max as
+    regular_lighting casts them). 'lowlight' puts a point light 3e-4 above the ground
+    (above the test's 1e-4 floor on |denom|): no limit there, and self-occluded points do
+    exist."""
+    import copy
+    from common import product_scene_dict
+    from rtx.io import bundled_scene_dict
+    from scenegen import random_scene, shadow_scene
+    if case.startswith("rand"):
+        d = random_scene(int(case[4:]))
+    elif case.startswith("shadow"):
+        d = shadow_scene(int(case[6:]))
+    elif case == "lowlight":
+        d = random_scene(0)
+        d["lights"] = [{"name": "low", "type": "point", "position": [1.0, -1.0 + 3e-4, 0.5],
+                        "colour": [1.0, 1.0, 1.0], "power": 1.0}]
+        d["objects"] = [o for o in d["objects"] if o["type"] == "plane"][:1]
+        d["objects"][0]["position"] = [0.0, -1.0, 0.0]
+        d["objects"][0]["normal"] = [0.0, 1.0, 0.0]
+    else:
+        d = bundled_scene_dict(case, resolution=(64, 48))
+    sc = product_scene_dict(d)
+    sd = sc.scene_desc()
+    lim = hostemu.plane_self(sc)
+    cd, t = sc.camera_desc()
+    aa = np.asarray(t["aa"], np.float64).reshape(-1, 3)
+    rng = np.random.RandomState(3)
+    planes = [i for i, o in enumerate(d["objects"]) if o["type"] == "plane"]
+    tested = self_occ = 0
+    for k, i in enumerate(planes[:4]):
+        o = d["objects"][i]
+        if "speed" in o:
+            continue
+        p0, nrm = np.asarray(o["position"], np.float64), np.asarray(o["normal"], np.float64)
+        u = np.cross(nrm, [0.3, 0.5, 0.7])
+        u /= np.linalg.norm(u)
+        v = np.cross(nrm / np.linalg.norm(nrm), u)
+        n = 20000
+        rad = np.exp(rng.uniform(np.log(0.01), np.log(400.0), n))  # near and far (grazing)
+        ang = rng.uniform(0, 2 * np.pi, n)
+        tgt = p0 + (np.cos(ang) * rad)[:, None] * u + (np.sin(ang) * rad)[:, None] * v
+        org = aa[rng.randint(len(aa), size=n)]
+        dr = (tgt - org) / np.linalg.norm(tgt - org, axis=1, keepdims=True)
+        hit = hostemu.intersect(sc, org.astype(np.float32), dr.astype(np.float32))
+        on = hit["obj"] == i
+        P = hit["position"][on]
+        m = np.abs(P).max(axis=1)
+        one = copy.deepcopy(d)
+        one["objects"] = [copy.deepcopy(o)]
+        one.pop("motion", None)
+        s1 = product_scene_dict(one)
+        for li, l in enumerate(d["lights"]):
+            if l["type"] == "directional":
+                D = np.broadcast_to(-np.asarray(sd.lights[li].vector[:3], np.float32), P.shape)
+                tmax = np.inf
+            else:
+                D = (np.asarray(sd.lights[li].vector[:3], np.float32) - P).astype(np.float32)
+                tmax = 1.0
+            occ = hostemu.occluded(s1, P, D, tmax, 0.0)
+            within = m <= lim[li, k]
+            assert not (occ & within).any(), (case, k, li, float(lim[li, k]), int((occ & within).sum()))
+            tested += int(within.sum())
+            self_occ += int(occ.sum())
+    if case == "lowlight":
+        assert (lim < 0).all() and self_occ > 0, (lim, self_occ)
+    elif case in ("TwoSpheresPlane", "DepthOfField", "MirrorRefraction"):
+        assert tested > 1000, tested  # (random scenes may have no limit: lights near a plane)
+
+
 def test_hostemu_dir_shadow_grids_skip_most_rays(monkeypatch):
     """The grids are tight enough to pay: on DepthOfField (and on MirrorRefraction, whose
     four spheres alone get no grid unless RTX_DSGRID_MIN allows it) most floor points'
