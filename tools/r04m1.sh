@@ -3,4 +3,4 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-TAG=r04m STEPS="tests smoke pmc" CONFIGS="tsp1080 mr1080 tm1080 dof4k ns1 ns2 blob1080" bash tools/session.sh
+TAG=${TAG:-r04m} STEPS="tests smoke pmc" CONFIGS="tsp1080 mr1080 tm1080 dof4k ns1 ns2 blob1080" bash tools/session.sh
