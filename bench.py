@@ -47,6 +47,8 @@ CONFIGS = {
     "blob1080": ("blob", (1920, 1080), None,
                  "81,920-face smooth mesh 1920x1080 1spp (bunny-sized stand-in; reference bunny.obj is absent)"),
 }
+# The render-bound config beside the metric's at N > 1.
+SCALING_CONFIG = "dof4k"
 # CPU-baseline sub-sampling for the configs whose full frame takes minutes on one core:
 # the first of N column strips (np.array_split(arange(W), N)[0]) per repeat.
 CPU_STRIPS = {"tm1080": 16, "dof4k": 16, "ns1": 32, "ns2": 128, "blob1080": 64}
@@ -298,26 +300,16 @@ def timed(fn, steps, use_dist, sync=cuda_sync, device="cuda"):
     return max_over_ranks(t1 - t0, use_dist, device)
 
 
-def measure_sharded(sc, rank, world, steps, warmup, use_dist, device, sync=cuda_sync, stream=None,
-                    render_rows=None, render_block=None, render_block_k=None, graph=True):
-    """The N > 1 measurements (bench.py's multi-GPU leg; at N = 1 with --pipeline a
-    rehearsal). Renderers default to the HIP kernels on this rank's GPU; the CPU tests
-    inject the host emulation (tests/test_bench_multirank.py).
-
-    - value: ONE frame sharded over the ranks, frame by frame. Every step renders this
-      rank's interleaved 8-row groups of the frame straight to uint8 (fused
-      rtx_render_groups_rgb8, one launch per frame) and gathers them to rank 0 (one RCCL
-      gather), awaited before the next frame starts; rank 0 puts the rows in image order.
-      No batching and no overlap across frames: the latency of one frame, the reference's
-      one-frame-per-run strip render + glue (render.nu:10-15, provided/glue.py:17-27).
-    - throughput: the frame stream of one static scene state (rtx.distributed.FrameExchange:
-      frame k to rank k mod N, N frames per batched launch and per all_to_all, overlapped).
-    - gather_to_rank0: the same stream with every frame gathered to rank 0 (FramePipeline).
-    Returns a dict (times are the max over ranks) and, on rank 0, the last frame of the
-    value loop ([H, W, 3] uint8)."""
-    from rtx.distributed import FrameExchange, FrameGather, FramePipeline
+def sharded_frame(sc, rank, world, steps, warmup, use_dist, device, sync=cuda_sync, stream=None, render_rows=None):
+    """ONE frame sharded over the ranks, frame by frame (the N > 1 value): every step renders
+    this rank's interleaved 8-row groups of the frame straight to uint8 (fused
+    rtx_render_groups_rgb8, one launch per frame) and gathers them to rank 0 (one RCCL
+    gather), awaited before the next frame starts; rank 0 puts the rows in image order. No
+    batching and no overlap across frames: the latency of one frame, the reference's
+    one-frame-per-run strip render + glue (render.nu:10-15, provided/glue.py:17-27).
+    Returns (seconds for `steps` frames, max over ranks; rank 0's last frame [H, W, 3])."""
+    from rtx.distributed import FrameGather
     H, W = sc.vc.height, sc.vc.width
-    spp = sc.samples_per_pixel
     single = FrameGather(H, W, 3, world, rank, torch.uint8, device, interleave=True, dst=0)
     if render_rows is None:
         def render_rows(out):
@@ -335,7 +327,38 @@ def measure_sharded(sc, rank, world, steps, warmup, use_dist, device, sync=cuda_
     for _ in range(warmup):
         one_frame()
     sync()
-    frame_s = timed(one_frame, steps, use_dist, sync, device)
+    return timed(one_frame, steps, use_dist, sync, device), last[0]
+
+
+def sharded_config_field(cfg, sc, rank, world, steps, warmup, use_dist, device, sync=cuda_sync, stream=None,
+                         render_rows=None):
+    """The scaling config's sharded frame beside the metric's (DESIGN.md section 7:
+    DepthOfField 4K is render-bound at every N, TwoSpheresPlane 1080p is link-bound at
+    N = 2): the same one-frame-per-step loop as the value, on `sc`."""
+    s, _ = sharded_frame(sc, rank, world, steps, warmup, use_dist, device, sync, stream, render_rows)
+    W, H = sc.vc.width, sc.vc.height
+    return {"config": cfg, "workload": CONFIGS[cfg][3], "steps": steps, "frame_ms": round(s * 1e3 / steps, 5),
+            "Mrays_s": round(W * H * sc.samples_per_pixel * steps / s / 1e6, 3),
+            "note": "one frame per step sharded over the N ranks (uint8 rows) and gathered to rank 0, awaited: "
+                    "the value's loop on the render-bound scaling config"}
+
+
+def measure_sharded(sc, rank, world, steps, warmup, use_dist, device, sync=cuda_sync, stream=None,
+                    render_rows=None, render_block=None, render_block_k=None, graph=True):
+    """The N > 1 measurements (bench.py's multi-GPU leg; at N = 1 with --pipeline a
+    rehearsal). Renderers default to the HIP kernels on this rank's GPU; the CPU tests
+    inject the host emulation (tests/test_bench_multirank.py).
+
+    - value: ONE frame sharded over the ranks, frame by frame (sharded_frame).
+    - throughput: the frame stream of one static scene state (rtx.distributed.FrameExchange:
+      frame k to rank k mod N, N frames per batched launch and per all_to_all, overlapped).
+    - gather_to_rank0: the same stream with every frame gathered to rank 0 (FramePipeline).
+    Returns a dict (times are the max over ranks) and, on rank 0, the last frame of the
+    value loop ([H, W, 3] uint8)."""
+    from rtx.distributed import FrameExchange, FramePipeline
+    H, W = sc.vc.height, sc.vc.width
+    spp = sc.samples_per_pixel
+    frame_s, last_frame = sharded_frame(sc, rank, world, steps, warmup, use_dist, device, sync, stream, render_rows)
 
     def run_frames(loop, n):
         if use_dist:
@@ -384,7 +407,17 @@ def measure_sharded(sc, rank, world, steps, warmup, use_dist, device, sync=cuda_
         "headline": "value = ONE frame sharded over the N ranks (uint8 rows, fused) and gathered to rank 0, "
                     "frame by frame, awaited: no batching or overlap across frames",
     }
-    return out, last[0]
+    return out, last_frame
+
+
+def rgb8_field(render_u8, steps, timer, W, H, spp, kernel):
+    """The N = 1 frame into uint8 (main.py's PNG bytes from the fused kernel,
+    rtx_render_rgb8): the output every N > 1 rank renders, so the 1 -> N ratio can be taken
+    on the same bytes. timer(fn, n) -> ms per call (HIP events on the launch stream)."""
+    ms = timer(render_u8, steps)
+    return {"frame_ms": round(ms, 5), "Mrays_s": round(W * H * spp / ms / 1e3, 3), "kernel": kernel(),
+            "note": "the same frame rendered straight to uint8 (rtx_render_rgb8, 3 B/pixel), as each rank does "
+                    "at N > 1; HIP events over the same number of launches"}
 
 
 def roofline(bytes_alg, kern_ms, rows_frac, pmc_path):
@@ -501,6 +534,14 @@ def main():
         wall_s = timed(full_frame, a.steps, use_dist)
         kern_ms = kernel_ms(full_frame, a.steps, stream)  # the render kernel alone, same launches
         kernel = sc.last_kernel
+        fb8 = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
+
+        def frame_u8():
+            sc.render_device(out=fb8, stream=stream)
+        frame_u8()  # (its first call may compile the uint8 variant of the specialized kernel)
+        torch.cuda.synchronize()
+        extra["rgb8"] = rgb8_field(frame_u8, a.steps, lambda fn, n: kernel_ms(fn, n, stream), W, H, spp,
+                                   lambda: sc.last_kernel)
         rows_frac = 1.0
         scaling, parallelism = "strong", "single GPU"
     else:
@@ -542,6 +583,10 @@ def main():
         extra["weak_scaling"] = {"Mrays_s": round(world * W * H * spp * a.steps / weak_s / 1e6, 3),
                                  "ms_per_step": round(weak_s * 1e3 / a.steps, 5),
                                  "note": "frame-parallel: each rank renders its own whole frame, no collective"}
+        if a.config != SCALING_CONFIG:  # the render-bound scaling config's sharded frame beside it
+            sc2 = make_scene(SCALING_CONFIG)  # (its warm-up frames compile its kernel)
+            extra["scaling_config"] = sharded_config_field(SCALING_CONFIG, sc2, rank, world, min(a.steps, 10), 2,
+                                                           use_dist, dev, stream=stream)
         scaling, parallelism = "strong", "rows x %d ranks + one RCCL gather to rank 0 per frame" % world
     ms_per_step = wall_s * 1e3 / a.steps
     value = W * H * spp * a.steps / wall_s / 1e6

@@ -2004,16 +2004,35 @@ struct rtx_scene {
     // fp32 staging of the rgb8 entry points when no scene-specialized kernel is available
     float* d_scratch = nullptr;
     size_t scratch_floats = 0;
-    // the split hierarchy passes' shade-point records (rtx_split.h) and their counter
     // the measured tile schedule (tile_schedule): dispatch order and wave durations of a
     // whole frame's tiles; state 0 none, 1 measure the next whole frame, 2 sort, 3 ordered,
     // 4 measured and left in row-major order
     void* d_tile_perm = nullptr;
     void* d_tile_time = nullptr;
     int tile_sched = 0;
-    ShadePt* d_split = nullptr;
-    unsigned int* d_split_count = nullptr;
+    hipEvent_t tile_event = nullptr;  // recorded after the measuring launch
+    // the split hierarchy passes (rtx_split.h, render_split): the record arrays of one
+    // chunk (kept while the scene lives, reused by every frame), the per-chunk append
+    // counters of a frame, the per-block redo flags (all zero between renders), and what the
+    // pool sizing learned: deeper records per sample (split_ratio), read back without a
+    // stall from the last frame's counters (split_pending: h_split_count is in flight)
+    uint32_t* d_split = nullptr;
     int64_t split_cap = 0;
+    unsigned int* d_split_count = nullptr;
+    int64_t split_nchunk_cap = 0;
+    uint32_t* d_split_redo = nullptr;  // per chunk block: list entry, then flag (2 words)
+    int64_t split_redo_cap = 0;
+    double split_ratio = -1.0;
+    unsigned int* h_split_count = nullptr;  // pinned
+    std::vector<std::pair<int64_t, int64_t>> split_chunks;  // (samples, records) of the read-back frame's chunks
+    bool split_pending = false;
+    hipEvent_t split_read = nullptr;     // the readback's completion
+    hipEvent_t split_done = nullptr;     // the last split render's completion (cross-stream order)
+    hipStream_t split_stream = nullptr;  // its stream
+    bool split_used = false;
+    // buffers a captured graph may still reference: freed only with the scene
+    std::vector<void*> split_retired;
+    bool split_captured = false;
 };
 
 namespace {
@@ -2058,8 +2077,15 @@ void free_camera(rtx_scene* s) {
 void free_scene(rtx_scene* s) {
     free_camera(s);
     (void)hipFree(s->d_scratch);
+    if (s->split_done) (void)hipEventSynchronize(s->split_done);
     (void)hipFree(s->d_split);
     (void)hipFree(s->d_split_count);
+    (void)hipFree(s->d_split_redo);
+    for (void* p : s->split_retired) (void)hipFree(p);
+    if (s->split_read) { (void)hipEventSynchronize(s->split_read); (void)hipEventDestroy(s->split_read); }
+    if (s->split_done) (void)hipEventDestroy(s->split_done);
+    (void)hipHostFree(s->h_split_count);
+    if (s->tile_event) (void)hipEventDestroy(s->tile_event);
     for (void* p : {s->d_objs, s->d_tris, s->d_trins, s->d_fboxes, s->d_mats, s->d_lights, s->d_leaves, s->d_tri_orig, s->d_nodes, s->d_nmat,
                     s->d_texels, s->d_lut, s->d_bounds_abi, s->d_lgrid, s->d_lg_start, s->d_lg_faces, s->d_lg_d2})
         (void)hipFree(p);
@@ -2397,6 +2423,11 @@ int rtx_render_groups_rgb8(rtx_scene* s, int32_t phase, int32_t stride, uint8_t*
 }
 
 namespace {
+bool stream_capturing(hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
 int launch_to_rgb8(const float* fb, uint8_t* out, int64_t n, hipStream_t st) {
     if ((reinterpret_cast<uintptr_t>(fb) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 3) == 0)
         hipLaunchKernelGGL(k_to_rgb8, dim3((unsigned)((n / 4 + 256) / 256)), dim3(256), 0, st, fb, out, n);
@@ -2426,10 +2457,10 @@ bool split_enabled() {
 // nothing). The order changes when tiles run, not what they compute.
 int tile_schedule(rtx_scene* s, hipStream_t st) {
     if (s->tile_sched != 2) return RTX_OK;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return RTX_OK;
+    if (stream_capturing(st)) return RTX_OK;
     const int32_t n = s->kp.tile_n;
     std::vector<uint32_t> t((size_t)n);
+    RTX_HIP(hipEventSynchronize(s->tile_event));  // the measuring launch (maybe on another stream)
     RTX_HIP(hipMemcpyAsync(t.data(), s->d_tile_time, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, st));
     RTX_HIP(hipStreamSynchronize(st));
     double sum = 0.0;
@@ -2449,38 +2480,120 @@ int tile_schedule(rtx_scene* s, hipStream_t st) {
     return RTX_OK;
 }
 
-// Records per chunk ($RTX_SPLIT_RECORDS, default 2^26 = 4 GiB of 64-B records): a chunk
-// takes as many whole pixels as fit when every sample fills every chain level.
-// Records per chunk of the split passes (64 B each; a chunk reserves every sample's
-// deepest chain). 2^28 (16 GiB of the 288 GB) measured faster than 2^26 and 2^27 --
-// fewer, longer launches: NovelScene1 16.97 -> 16.12 ms, NovelScene2 76.7 -> 70.5 ms
-// (profiles/r04/split_records/); $RTX_SPLIT_RECORDS lowers it.
-int64_t split_records() {
-    const char* e = getenv("RTX_SPLIT_RECORDS");
-    const long long v = (e && *e) ? atoll(e) : (1ll << 28);
-    return std::min<long long>(std::max<long long>(v, 1024), 1ll << 30);
+// Record bytes of one chunk of the split passes ($RTX_SPLIT_BYTES, default 2 GiB; 40 B per
+// record): NovelScene1 (67 M samples, ~1.8 records each) renders in 3 chunks.
+int64_t split_budget() {
+    const char* e = getenv("RTX_SPLIT_BYTES");
+    const long long v = (e && *e) ? atoll(e) : (2ll << 30);
+    return std::max<long long>(v, 4096);
+}
+// $RTX_SPLIT_RATIO: a fixed deeper-record pool per sample instead of the learned one (the
+// tests force the redo path with a tiny pool).
+double split_fixed_ratio() {
+    const char* e = getenv("RTX_SPLIT_RATIO");
+    return (e && *e) ? std::max(0.0, atof(e)) : -1.0;
 }
 
-int render_split(rtx_scene* s, Launch L, const KParams* kp, size_t hbytes, hipStream_t st, int sel, int32_t nframes) {
+// The deeper-record pool learns from the counters of an earlier frame once they have
+// arrived on the host (never waits): at least 1/8 more than the fullest chunk needed.
+void split_learn(rtx_scene* s, int levels) {
+    if (!s->split_pending || hipEventQuery(s->split_read) != hipSuccess) return;
+    s->split_pending = false;
+    double need = 0.0;
+    for (size_t c = 0; c < s->split_chunks.size(); ++c)
+        if (s->split_chunks[c].first > 0)
+            need = std::max(need, (double)s->h_split_count[c] / (double)s->split_chunks[c].first);
+    const double want = std::min<double>(levels - 1, need * 1.125 + 1.0 / 64);
+    if (want > s->split_ratio) s->split_ratio = want;
+}
+
+// Frees a split buffer, or keeps it for the scene's life when a captured graph may use it.
+void split_release(rtx_scene* s, void* p) {
+    if (!p) return;
+    if (s->split_captured) s->split_retired.push_back(p);
+    else (void)hipFree(p);
+}
+
+constexpr int64_t kRedoBlocks = 2048;  // grid of the split passes' redo launch
+
+int render_split(rtx_scene* s, Launch L, const KParams* kp, size_t hbytes, hipStream_t st, int sel, int32_t nframes,
+                 bool cnt) {
     constexpr int B = kBlock<true>;
     const int spp = s->kp.n_dof * s->kp.n_aa * s->kp.n_times;
     const int64_t npix = (int64_t)L.nrows * s->kp.ncols;
     if (npix <= 0 || nframes <= 0) return RTX_OK;
     const int levels = s->has_secondary ? kMaxDepth : 1;
     const int ppb = spp_pixels_per_block(spp, B);
-    int64_t chunk = std::max<int64_t>(1, split_records() / ((int64_t)spp * levels));
-    if (chunk < npix) chunk = std::max<int64_t>(ppb, chunk / ppb * ppb);
-    chunk = std::min(chunk, npix);
-    const int64_t cap = chunk * spp * levels;
-    if (cap >= (1ll << 31)) return fail(RTX_ERR_INVALID, "rtx_render: split chunk too large");
-    if (s->split_cap < cap) {
-        (void)hipFree(s->d_split);
+    const bool capturing = stream_capturing(st);
+    const double fixed = split_fixed_ratio();
+    if (s->split_ratio < 0.0) s->split_ratio = levels > 1 ? 1.0 : 0.0;
+    if (!capturing) split_learn(s, levels);
+    // counting renders reserve every level (a redone block would count its rays twice)
+    const double ratio = levels == 1 ? 0.0 : cnt ? (double)(levels - 1) : fixed >= 0.0 ? fixed : s->split_ratio;
+    // the records of one chunk: within the budget and 3/4 of the device's free memory, the
+    // budget halved when an allocation fails anyway
+    int64_t budget = split_budget();
+    {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess)
+            budget = std::min<int64_t>(budget, (int64_t)((fr + (size_t)s->split_cap * kSpBytes) / 4 * 3));
+    }
+    SplitPlan pl;
+    for (;;) {
+        pl = split_plan(npix, spp, ppb, ratio, budget);
+        if (pl.cap >= (1ll << 31) && pl.chunk > ppb) { budget /= 2; continue; }  // (record indices are int32)
+        if (pl.cap >= (1ll << 31)) return fail(RTX_ERR_INVALID, "rtx_render: split chunk too large");
+        if (s->split_cap >= pl.cap) break;
+        if (capturing)
+            return fail(RTX_ERR_STATE, "rtx_render: render a hierarchy/texture scene once before capturing it "
+                                       "(its record buffer is allocated on first use)");
+        split_release(s, s->d_split);
         s->d_split = nullptr;
         s->split_cap = 0;
-        RTX_HIP(hipMalloc((void**)&s->d_split, (size_t)cap * sizeof(ShadePt)));
-        if (!s->d_split_count) RTX_HIP(hipMalloc((void**)&s->d_split_count, sizeof(unsigned int)));
-        s->split_cap = cap;
+        const hipError_t e = hipMalloc((void**)&s->d_split, (size_t)pl.cap * kSpBytes);
+        if (e == hipSuccess) {
+            s->split_cap = pl.cap;
+            break;
+        }
+        s->d_split = nullptr;
+        (void)hipGetLastError();
+        if (e != hipErrorOutOfMemory || pl.chunk <= ppb)
+            return fail(RTX_ERR_HIP, std::string("rtx_render: split records: ") + hipGetErrorString(e));
+        budget = std::min(budget, pl.cap * kSpBytes) / 2;
     }
+    const int64_t chunk = pl.chunk, cap = s->split_cap;
+    const int64_t nchunk = (npix + chunk - 1) / chunk;
+    const int64_t nblk = (chunk + ppb - 1) / ppb;
+    if (s->split_nchunk_cap < nchunk || s->split_redo_cap < nblk) {
+        if (capturing) return fail(RTX_ERR_STATE, "rtx_render: render a hierarchy/texture scene once before capturing it");
+        if (s->split_pending) {
+            (void)hipEventSynchronize(s->split_read);
+            s->split_pending = false;
+        }
+    }
+    if (s->split_nchunk_cap < nchunk) {
+        split_release(s, s->d_split_count);
+        (void)hipHostFree(s->h_split_count);
+        s->d_split_count = nullptr;
+        s->h_split_count = nullptr;
+        s->split_nchunk_cap = 0;
+        RTX_HIP(hipMalloc((void**)&s->d_split_count, 2 * sizeof(unsigned int) * nchunk));
+        RTX_HIP(hipHostMalloc((void**)&s->h_split_count, 2 * sizeof(unsigned int) * nchunk));
+        s->split_nchunk_cap = nchunk;
+    }
+    if (s->split_redo_cap < nblk) {  // flags all zero between renders: the redo launch clears what it lists
+        split_release(s, s->d_split_redo);
+        s->d_split_redo = nullptr;
+        s->split_redo_cap = 0;
+        RTX_HIP(hipMalloc((void**)&s->d_split_redo, 2 * sizeof(uint32_t) * nblk));
+        RTX_HIP(hipMemsetAsync(s->d_split_redo, 0, 2 * sizeof(uint32_t) * nblk, st));
+        s->split_redo_cap = nblk;
+    }
+    if (!s->split_read) RTX_HIP(hipEventCreateWithFlags(&s->split_read, hipEventDisableTiming));
+    if (!s->split_done) RTX_HIP(hipEventCreateWithFlags(&s->split_done, hipEventDisableTiming));
+    // one scene's renders share these buffers: a render on another stream waits for the last one
+    if (!capturing && s->split_used && s->split_stream != st)
+        RTX_HIP(hipStreamWaitEvent(st, s->split_done, 0));
     auto launch = [&](int pass, const RenderLaunch& r, const Launch& Lc, const SplitBuf& sb) {
         return s->has_mesh ? launch_split_m1(sel, pass, r, Lc, sb) : launch_split_m0(sel, pass, r, Lc, sb);
     };
@@ -2489,17 +2602,45 @@ int render_split(rtx_scene* s, Launch L, const KParams* kp, size_t hbytes, hipSt
         Launch Lc = L;
         Lc.fb = reinterpret_cast<float*>(base + f * L.fstride);
         Lc.fstride = 0;
-        for (int64_t p0 = 0; p0 < npix; p0 += chunk) {
+        Lc.redo = RedoList{nullptr, nullptr, nullptr};
+        RTX_HIP(hipMemsetAsync(s->d_split_count, 0, 2 * sizeof(unsigned int) * nchunk, st));
+        int64_t c = 0;
+        for (int64_t p0 = 0; p0 < npix; p0 += chunk, ++c) {
             const int64_t np = std::min(chunk, npix - p0), nq = np * spp;
             Lc.pix0 = (int32_t)p0;
-            const SplitBuf sb{s->d_split, s->d_split_count, nq, cap};
-            RTX_HIP(hipMemsetAsync(s->d_split_count, 0, sizeof(unsigned int), st));
+            uint32_t* const redo_n = s->d_split_count + nchunk + c;
+            uint32_t* const redo_list = s->d_split_redo;
+            uint32_t* const redo_flag = s->d_split_redo + s->split_redo_cap;
+            const SplitBuf sb{s->d_split, s->d_split_count + c, redo_n, redo_list, redo_flag, nq, cap};
             RenderLaunch r{kp, (unsigned)((nq + B - 1) / B), 1u, hbytes * B, st, true};
             RTX_HIP(launch(0, r, Lc, sb));
             RTX_HIP(launch(1, r, Lc, sb));
             r.nblocks = (unsigned)((np + ppb - 1) / ppb);
             RTX_HIP(launch(2, r, Lc, sb));
+            // the blocks whose chains found the pool full, again in the one-kernel form: a
+            // small grid strides over the list (a few microseconds when it is empty)
+            if (levels > 1) {
+                Launch Lf = Lc;
+                Lf.redo = RedoList{redo_n, redo_list, redo_flag};
+                r.nblocks = (unsigned)std::min<int64_t>((np + ppb - 1) / ppb, kRedoBlocks);
+                RTX_HIP(s->has_mesh ? launch_render_ext_m1(sel, r, Lf) : launch_render_ext_m0(sel, r, Lf));
+            }
         }
+    }
+    if (!capturing) {
+        if (levels > 1 && !cnt && fixed < 0.0 && !s->split_pending) {  // what this frame's chains used
+            RTX_HIP(hipMemcpyAsync(s->h_split_count, s->d_split_count, sizeof(unsigned int) * nchunk,
+                                   hipMemcpyDeviceToHost, st));
+            RTX_HIP(hipEventRecord(s->split_read, st));
+            s->split_chunks.clear();
+            for (int64_t p0 = 0; p0 < npix; p0 += chunk) s->split_chunks.emplace_back(std::min(chunk, npix - p0) * spp, cap);
+            s->split_pending = true;
+        }
+        RTX_HIP(hipEventRecord(s->split_done, st));
+        s->split_stream = st;
+        s->split_used = true;
+    } else {
+        s->split_captured = true;
     }
     return RTX_OK;
 }
@@ -2536,6 +2677,7 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
         L.pix0 = 0;
         L.tperm = 0;
         L.tlog = 0;
+        L.redo = RedoList{nullptr, nullptr, nullptr};
     }
     rtx_scene::Resolved& rs = s->resolved[(out8 ? 8 : 0) | (cnt ? 4 : 0) | (jit ? 2 : 0) | (spp_mode ? 1 : 0)];
     if (!rs.done) {
@@ -2548,11 +2690,14 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
         // whole-frame launches follow the measured tile schedule
         const bool whole = s->tile_sched != 0 && !spp_mode && L.row0 == 0 && L.nrows == s->kp.height &&
                            L.gstride == 0;
-        if (whole) {
+        // (a captured launch neither measures nor sorts: its replays run later, and the
+        // schedule's state machine follows eager frames only)
+        const bool capturing = whole && stream_capturing(st);
+        if (whole && !capturing) {
             if (int rc = tile_schedule(s, st)) return rc;
             L.tlog = s->tile_sched == 1;
-            L.tperm = s->tile_sched == 3;
         }
+        if (whole) L.tperm = s->tile_sched == 3;
         if (!spp_mode && persist_waves() > 0) {  // experiment: grid = resident wave slots
             int cus = 0;
             if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) == hipSuccess && cus > 0) {
@@ -2562,7 +2707,11 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
         }
         RTX_HIP(hipModuleLaunchKernel(rs.fn, (unsigned)nblocks, (unsigned)nframes, 1, blk, 1, 1,
                                       s->has_ext ? (unsigned)(hbytes * blk) : 0u, st, args, nullptr));
-        if (L.tlog) s->tile_sched = 2;  // measured: sorted before the next whole frame
+        if (L.tlog) {  // measured: sorted before the next whole frame
+            if (!s->tile_event) RTX_HIP(hipEventCreateWithFlags(&s->tile_event, hipEventDisableTiming));
+            RTX_HIP(hipEventRecord(s->tile_event, st));
+            s->tile_sched = 2;
+        }
         s->last_kernel = L.tperm ? rs.name + "+tiles" : rs.name;
         return RTX_OK;
     }
@@ -2596,11 +2745,12 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
              s->has_secondary ? 1 : 0, s->has_ext ? 1 : 0, cnt ? 1 : 0, jit ? 1 : 0,
              (spp_mode && s->has_ext) ? "_spp" : "");
     s->last_kernel = gname;
-    if (s->has_ext && split_enabled() && s->view.n_lights <= 32) {
+    if (s->has_ext && split_enabled() && s->view.n_lights <= 32 && s->view.n_mats <= kSpMaxMats &&
+        s->kp.n_times <= kSpMaxTimes) {
         snprintf(gname, sizeof(gname), "k_split_%d%d%d%d", s->has_mesh ? 1 : 0, s->has_secondary ? 1 : 0, cnt ? 1 : 0,
                  jit ? 1 : 0);
         s->last_kernel = gname;
-        return render_split(s, L, kp, hbytes, st, sel & 11, nframes);
+        return render_split(s, L, kp, hbytes, st, sel & 11, nframes, cnt);
     }
     if (s->has_ext) {  // precompiled in rtx_kern_ext_m{0,1}.hip
         const RenderLaunch rl{kp, (unsigned)nblocks, (unsigned)nframes, hbytes * kBlock<true>, st, spp_mode};

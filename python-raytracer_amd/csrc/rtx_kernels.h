@@ -289,6 +289,14 @@ RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, 
     put_channel(fb, 3 * p + 2, colour.z);
 }
 
+// Blocks of a split chunk to render again in the one-kernel form (rtx_split.h): n == nullptr
+// for every other launch. A listed block's flag is set; the launch that renders it clears it.
+struct RedoList {
+    const uint32_t* n;       // blocks listed
+    const uint32_t* blocks;  // their indices
+    uint32_t* flags;         // per block of the chunk
+};
+
 // The per-frame parameters live in device memory (uploaded by rtx_camera_set) and are
 // read with scalar loads; only the per-call output block is passed by value.
 struct Launch {
@@ -304,6 +312,9 @@ struct Launch {
     int32_t pix0;   // split hierarchy passes (rtx_split.h): the chunk's first pixel of the block
     int32_t tperm;  // RTX_TILE_SCHED kernels: 1 = dispatch a whole frame's tiles by P.tile_perm
     int32_t tlog;   // RTX_TILE_SCHED kernels: 1 = record each wave's duration in P.tile_time
+    // render_body_spp as the split passes' fallback (rtx_split.h): render only the listed
+    // blocks (chains that found the record pool full), pixels from pix0 on
+    RedoList redo;
 };
 
 // This block's framebuffer (frame blockIdx.y of a batched launch; the only frame otherwise).
@@ -554,7 +565,8 @@ __host__ __device__ inline int spp_pixels_per_block(int spp, int block) { return
 // (dof, aa, time; scene.py:57-70) starting from +0 -- the same fp32 sums as
 // render_pixel -- and writes the mean. Samples s map to (kd, ka, kt) with kt fastest.
 template <bool MESH, bool SEC, bool X, bool COUNT, bool JIT>
-__device__ __forceinline__ void render_body_spp(const KParams* __restrict__ Pp, const Launch L) {
+__device__ __forceinline__ void render_block_spp(const KParams* __restrict__ Pp, const Launch& L, int64_t blk, Tally& tl,
+                                                 bool& any_active) {
     constexpr int B = kBlock<X>;
     const KParams& P = *Pp;
     const int32_t ncols = P.ncols;
@@ -563,17 +575,15 @@ __device__ __forceinline__ void render_body_spp(const KParams* __restrict__ Pp, 
     const int PPB = spp_pixels_per_block(S, B);
     const int rounds = (PPB * S + B - 1) / B;
     const float rS = 1.0f / (float)S, rT = 1.0f / (float)nt, rA = 1.0f / (float)na;
-    Tally tl = {};
     __shared__ float frames[SEC ? kFrameLds * kFrameWords * B : 1];
     __shared__ float sbuf[3 * B];
     extern __shared__ float hstack[];  // X: [level][9][thread] (dynamic size)
     const FrameStack fs{frames + threadIdx.x, B};
     const HStack hs{hstack + threadIdx.x, B};
     const int64_t npix = (int64_t)L.nrows * ncols;
-    const int64_t pix0 = (int64_t)blockIdx.x * PPB;
+    const int64_t pix0 = L.pix0 + blk * PPB;
     const int tid = threadIdx.x;
     float acc = 0.0f;  // rounds > 1 (one pixel per block): lane ch < 3 sums channel ch
-    bool any_active = false;
     for (int rd = 0; rd < rounds; ++rd) {
         const int flat = rd * B + tid;  // the block's sample index
         int s;
@@ -612,9 +622,24 @@ __device__ __forceinline__ void render_body_spp(const KParams* __restrict__ Pp, 
             const float* src = sbuf + tid * B;
             for (int k = 0; k < hi; ++k) acc += src[k];
         }
-        if (rounds > 1) __syncthreads();  // sbuf is reused by the next round
+        __syncthreads();  // sbuf is reused by the next round (or block)
     }
     if (rounds > 1 && tid < 3 && pix0 < npix) put_channel(frame_fb(L), 3 * pix0 + tid, sample_mean(P, acc));
+}
+
+template <bool MESH, bool SEC, bool X, bool COUNT, bool JIT>
+__device__ __forceinline__ void render_body_spp(const KParams* __restrict__ Pp, const Launch L) {
+    Tally tl = {};
+    bool any_active = false;
+    // one block, or (the split passes' redo list) the grid strides over the listed blocks;
+    // one call site either way
+    const bool listed = L.redo.n != nullptr;
+    const uint32_t nb = listed ? *L.redo.n : 1u;
+    for (uint32_t i = listed ? blockIdx.x : 0u; i < nb; i += listed ? gridDim.x : 1u) {
+        const uint32_t b = listed ? L.redo.blocks[i] : blockIdx.x;
+        render_block_spp<MESH, SEC, X, COUNT, JIT>(Pp, L, (int64_t)b, tl, any_active);
+        if (listed && threadIdx.x == 0) L.redo.flags[b] = 0u;
+    }
     flush_tally<COUNT>(tl, L.counters, any_active);
 }
 

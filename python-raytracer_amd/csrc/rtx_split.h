@@ -11,16 +11,30 @@
 //               of its chain and the pixel's ordered sum (as render_body_spp).
 // Each pass is a kernel of its own with its own (smaller) register allocation. The
 // arithmetic is the one-kernel form's, operation for operation, so the frame is
-// bit-identical (tests/test_gpu_parity.py runs the hierarchy scenes both ways).
-// A frame is processed in chunks of whole pixels, so the records fit a fixed buffer
-// (rtx_api.hip render_split).
+// bit-identical (tests/test_gpu_split.py runs the hierarchy scenes both ways).
+//
+// Records (round 5): structure of arrays, 4-byte words, so every pass reads only what it
+// needs and a wave's accesses are coalesced (level-0 records sit at the sample's index;
+// deeper ones are appended in wave order):
+//   pass B reads  pos (12 B) + meta (4 B)                       and writes occ (4 B);
+//   pass C reads  pos, meta, normal (12 B), gobj, next, occ     (40 B).
+// The ray direction that hit a record is not stored: C recomputes it walking down the
+// chain (the camera ray, then reflect / refract of the parent's stored normal, the same
+// fp32 operations as A), so a record is 40 B instead of 64 B.
+// The deeper records come from a pool sized by use (rtx_api.hip render_split learns the
+// frame's chain depth), not by the worst case of ten levels per sample. A hit that finds
+// the pool full marks its pixel block in `redo`, and the block is rendered again by the
+// one-kernel form after pass C (render_body_spp with L.redo): the same bytes, so an
+// undersized pool costs time, never a wrong pixel.
 #pragma once
 
 #include "rtx_kernels.h"
 
 // Occupancy requests (waves per SIMD) of the trace and shadow passes.
+// (trace: 4 keeps it at <= 128 VGPRs without spills, as in round 4; the SoA record stores
+// had taken it to 129 VGPRs, 3 waves/SIMD)
 #ifndef RTX_LB_SPLIT_A
-#define RTX_LB_SPLIT_A 1
+#define RTX_LB_SPLIT_A 4
 #endif
 #ifndef RTX_LB_SPLIT_B
 #define RTX_LB_SPLIT_B 1
@@ -28,33 +42,33 @@
 
 namespace rtx {
 
-// One hit of a sample's chain (64 B, written by A, its mask by B, read by C).
-struct alignas(16) ShadePt {
-    float pos[3];
-    float time;
-    float n[3];     // the normal the lighting uses (negated inside a refractive object)
-    int32_t mat;
-    float d[3];     // the ray direction that hit (the specular half vector)
-    int32_t gobj;   // DObj whose get_diffuse shades the hit, or -1
-    int32_t next;   // the record of the child's hit, or -1 (black child / none)
-    uint32_t flags; // kSpHit | kSpChain
-    uint32_t occ;   // B: bit li = light li's shadow ray is occluded
-    int32_t prev;   // the parent's record (the hit whose reflect/refract ray this is), or -1
-};
+// The record arrays of a chunk, each `cap` words.
+enum SpArray : int { kSpPx, kSpPy, kSpPz, kSpMeta, kSpNx, kSpNy, kSpNz, kSpGobj, kSpNext, kSpOcc, kSpArrays };
+constexpr int64_t kSpBytes = 4 * kSpArrays;  // bytes per record
+// meta: 0 = no hit (black); else kSpHit | kSpChain (a mirror / refractive hit whose child
+// ray was cast) | the motion-time index << 2 | the material << kSpMatShift.
 constexpr uint32_t kSpHit = 1u, kSpChain = 2u;
+constexpr int kSpTimeBits = 10, kSpMatShift = 2 + kSpTimeBits;
+// (the split path serves scenes within these: rtx_api.hip render_launch)
+constexpr int64_t kSpMaxTimes = 1 << kSpTimeBits, kSpMaxMats = 1 << 16;
 
-// The chunk's record buffer: level-0 records at [0, nsamp) (one per sample, in sample
-// order), the chain's deeper hits appended at nsamp + (*count)++.
 struct SplitBuf {
-    ShadePt* rec;
-    unsigned int* count;  // appended records (reset before A)
-    int64_t nsamp;        // samples of the chunk
-    int64_t cap;          // records the buffer holds
+    uint32_t* w;          // kSpArrays arrays of cap words
+    unsigned int* count;  // deeper records appended in this chunk (zero before A)
+    uint32_t* redo_n;     // shade blocks listed for the redo launch (zero before A)
+    uint32_t* redo_list;  // their indices
+    uint32_t* redo_flag;  // per shade block of the chunk: listed (cleared by the redo launch)
+    int64_t nsamp;        // samples of the chunk (= its level-0 records)
+    int64_t cap;          // records the arrays hold
+    RTX_HD uint32_t* u(int a) const { return w + a * cap; }
+    RTX_HD float* f(int a) const { return reinterpret_cast<float*>(w + a * cap); }
+    RTX_HD int32_t* i(int a) const { return reinterpret_cast<int32_t*>(w + a * cap); }
 };
 
 // Sample q of the chunk (q = pixel * spp + s, the reference's dof -> aa -> time order with
 // time fastest, as render_body_spp): pixel and sample indices.
 struct SampleIx {
+    int32_t qp;  // the chunk's pixel
     int32_t rr, cc, j, kd, ka, kt;
 };
 RTX_HD SampleIx sample_ix(const KParams& P, const Launch& L, int64_t q, int S, int nt, int na) {
@@ -62,6 +76,7 @@ RTX_HD SampleIx sample_ix(const KParams& P, const Launch& L, int64_t q, int S, i
     const uint32_t qp = (uint32_t)q / (uint32_t)S;  // (chunks hold < 2^31 samples)
     const int s = (int)((uint32_t)q - qp * (uint32_t)S);
     const int64_t p = L.pix0 + (int64_t)qp;
+    x.qp = (int32_t)qp;
     x.rr = (int32_t)(p / P.ncols);
     x.cc = (int32_t)(p - (int64_t)x.rr * P.ncols);
     x.j = P.height - 1 - image_row(L, x.rr);
@@ -72,9 +87,24 @@ RTX_HD SampleIx sample_ix(const KParams& P, const Launch& L, int64_t q, int S, i
     return x;
 }
 
+// Lists shade block b for the redo launch (once).
+RTX_HD void list_redo(const SplitBuf& sb, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (atomicExch(&sb.redo_flag[b], 1u) == 0u) sb.redo_list[atomicAdd(sb.redo_n, 1u)] = b;
+#else
+    if (__atomic_exchange_n(&sb.redo_flag[b], 1u, __ATOMIC_RELAXED) == 0u)
+        sb.redo_list[__atomic_fetch_add(sb.redo_n, 1u, __ATOMIC_RELAXED)] = b;
+#endif
+}
+
+// The camera ray's direction of a sample (scene.py:58).
+RTX_HD f3 sample_dir(const KParams& P, const SampleIx& x) {
+    return normalize(sub(pixel_focal(P, x.cc, x.j), ld3(P.dof_o + 3 * x.kd)));
+}
+
 // Pass A for sample q: the chain of closest hits (cast_ray's loop without the lighting).
 // alloc(hit) returns the appended record of a deeper hit (every lane of the wave calls it
-// at the same level; lanes without a hit get -1).
+// at the same level; lanes without a hit get -1, lanes whose hit finds the pool full -2).
 template <bool MESH, bool SEC, bool COUNT, bool JIT, class Alloc>
 RTX_HD void trace_sample(const KParams& P, const Launch& L, const SplitBuf& sb, int64_t q, Tally& tl,
                          const HStack& hs, Alloc& alloc) {
@@ -82,8 +112,7 @@ RTX_HD void trace_sample(const KParams& P, const Launch& L, const SplitBuf& sb, 
     const int nt = RTX_NTIMES(P), na = RTX_NAA(P);
     const int Sn = RTX_NDOF(P) * na * nt;
     const SampleIx x = sample_ix(P, L, q, Sn, nt, na);
-    const f3 focal = pixel_focal(P, x.cc, x.j);
-    f3 d = normalize(sub(focal, ld3(P.dof_o + 3 * x.kd)));  // scene.py:58
+    f3 d = sample_dir(P, x);
     f3 o = sample_origin<JIT>(P, x.cc, x.j, x.kd, x.ka);
     const float time = P.times[x.kt];
     // the primary-ray bin of the wave's pixels when they share one (rtx_api.hip primary_bins)
@@ -104,13 +133,17 @@ RTX_HD void trace_sample(const KParams& P, const Launch& L, const SplitBuf& sb, 
         const bool hit = h.obj != -1;
         if (level > 0) {  // a deeper hit is appended and linked from its parent
             slot = alloc(hit);
-            if (slot >= 0) sb.rec[parent].next = (int32_t)slot;
+            if (slot >= 0) {
+                sb.i(kSpNext)[parent] = (int32_t)slot;
+            } else if (hit) {  // the pool is full: the one-kernel form renders the block again
+                list_redo(sb, (uint32_t)x.qp / (uint32_t)spp_pixels_per_block(Sn, kBlock<true>));
+                return;
+            }
         }
         if (!hit) {
-            if (level == 0) sb.rec[q].flags = 0u;  // miss -> black
+            if (level == 0) sb.u(kSpMeta)[q] = 0u;  // miss -> black
             return;
         }
-        if (slot < 0) return;  // (cannot happen: the chunk's buffer holds every level)
         const Surface sf = resolve_hit<MESH, true>(S, h, hh, o, d, time);
         const DMat m = RTX_MAT(S, sf.mat);
         f3 n = sf.normal;
@@ -130,18 +163,15 @@ RTX_HD void trace_sample(const KParams& P, const Launch& L, const SplitBuf& sb, 
             next_d = rdir;
             chain = true;
         }
-        ShadePt r;
-        r.pos[0] = sf.position.x; r.pos[1] = sf.position.y; r.pos[2] = sf.position.z;
-        r.time = time;
-        r.n[0] = n.x; r.n[1] = n.y; r.n[2] = n.z;
-        r.mat = sf.mat;
-        r.d[0] = d.x; r.d[1] = d.y; r.d[2] = d.z;
-        r.gobj = sf.gobj;
-        r.next = -1;
-        r.flags = kSpHit | (chain ? kSpChain : 0u);
-        r.occ = 0u;
-        r.prev = (int32_t)parent;
-        sb.rec[slot] = r;
+        sb.f(kSpPx)[slot] = sf.position.x;
+        sb.f(kSpPy)[slot] = sf.position.y;
+        sb.f(kSpPz)[slot] = sf.position.z;
+        sb.u(kSpMeta)[slot] = kSpHit | (chain ? kSpChain : 0u) | ((uint32_t)x.kt << 2) | ((uint32_t)sf.mat << kSpMatShift);
+        sb.f(kSpNx)[slot] = n.x;
+        sb.f(kSpNy)[slot] = n.y;
+        sb.f(kSpNz)[slot] = n.z;
+        sb.i(kSpGobj)[slot] = sf.gobj;
+        sb.i(kSpNext)[slot] = -1;
         if (!SEC || !chain || tir) return;
         in_shape = m.type == MAT_REFRACTIVE ? !in_shape : false;
         o = next_o;
@@ -150,11 +180,10 @@ RTX_HD void trace_sample(const KParams& P, const Launch& L, const SplitBuf& sb, 
     }
 }
 
-// Pass B for one record: its shadow rays (regular_lighting's per-light rays, scene.py:
-// 148-164) -> occlusion mask.
+// Pass B for one shading point: its shadow rays (regular_lighting's per-light rays,
+// scene.py:148-164) -> occlusion mask.
 template <bool MESH, bool COUNT>
-RTX_HD uint32_t shadow_record(const SceneView& S, const ShadePt& R, Tally& tl, const HStack& hs) {
-    const f3 pos = mk(R.pos[0], R.pos[1], R.pos[2]);
+RTX_HD uint32_t shadow_mask(const SceneView& S, f3 pos, float time, Tally& tl, const HStack& hs) {
     tally_inc<COUNT>(tl, &Tally::shade);
     uint32_t occm = 0u;
     for (int li = 0; li < RTX_NLIGHTS(S); ++li) {
@@ -169,43 +198,90 @@ RTX_HD uint32_t shadow_record(const SceneView& S, const ShadePt& R, Tally& tl, c
             t_max = INFINITY;
         }
         tally_inc<COUNT>(tl, &Tally::shadow);
-        if (occluded<MESH, true, COUNT>(S, pos, sdir, t_max, R.time, tl, hs, nullptr, li)) occm |= 1u << li;
+        if (occluded<MESH, true, COUNT>(S, pos, sdir, t_max, time, tl, hs, nullptr, li)) occm |= 1u << li;
     }
     return occm;
 }
 
-// The lighting of one record (scene.py:140-187 with its occlusion mask; no ray traced).
-template <bool MESH>
-RTX_HD f3 record_lighting(const SceneView& S, const ShadePt& R, const DMat& m) {
+// Pass C for the sample q (whose level-0 record is q): cast_ray's value (scene.py:97-116)
+// from its chain of records. Walking down the `next` links it recomputes each record's
+// incoming ray direction and lights the record (regular_lighting with the record's
+// occlusion mask; no ray traced); the lighting and material of every level that blends
+// with a child go to a frame stack (LDS on the device), the deepest level's stays in
+// registers; then it blends bottom-up -- the unwinding order.
+// The stack: per frame three floats and a 16-bit material index (the split path serves
+// scenes with at most 2^16 materials), [frame][word][lane] so lanes hit distinct banks.
+struct ShadeStack {
+    float* f;     // [kMaxDepth - 1][3][stride]
+    uint16_t* m;  // [kMaxDepth - 1][stride]
+    int stride;
+    RTX_HD void put(int k, f3 L, int32_t mat) const {
+        float* p = f + 3 * k * stride;
+        p[0] = L.x;
+        p[stride] = L.y;
+        p[2 * stride] = L.z;
+        m[k * stride] = (uint16_t)mat;
+    }
+    RTX_HD f3 get(int k, int32_t& mat) const {
+        const float* p = f + 3 * k * stride;
+        mat = m[k * stride];
+        return f3{p[0], p[stride], p[2 * stride]};
+    }
+};
+constexpr int kShadeFrames = kMaxDepth - 1;  // the deepest level never blends with a child
+
+template <bool MESH, bool SEC>
+RTX_HD f3 shade_sample(const KParams& P, const Launch& L, const SplitBuf& sb, int64_t q, const ShadeStack& fs) {
+    const SceneView& S = P.S;
+    uint32_t meta = sb.u(kSpMeta)[q];
+    if (!(meta & kSpHit)) return mk(0.0f, 0.0f, 0.0f);  // miss -> black
+    const int nt = RTX_NTIMES(P), na = RTX_NAA(P);
+    const int Sn = RTX_NDOF(P) * na * nt;
+    const SampleIx x = sample_ix(P, L, q, Sn, nt, na);
+    const float time = P.times[x.kt];
+    f3 d = sample_dir(P, x);
+    int nfr = 0;  // frames on the stack (levels whose colour blends with a child's)
+    bool in_shape = false;
+    int64_t r = q;
     Tally tl = {};
     const HStack hs{nullptr, 1};
-    const f3 pos = mk(R.pos[0], R.pos[1], R.pos[2]);
-    const f3 diffuse = R.gobj >= 0 ? get_diffuse(S, S.objs[R.gobj], pos, R.time) : ld3(m.diffuse);
-    return regular_lighting<MESH, true, false>(S, mk(R.d[0], R.d[1], R.d[2]), pos, mk(R.n[0], R.n[1], R.n[2]), m,
-                                               diffuse, R.time, tl, hs, (int64_t)R.occ);
-}
-
-// Pass C for the sample whose level-0 record is r: cast_ray's value (scene.py:97-116)
-// from its chain of records. The chain is walked to its deepest record by the `next`
-// links, then back up by the `prev` links, lighting each record on the way up and
-// blending it into the child's colour -- the unwinding order, with no frame stack.
-template <bool MESH, bool SEC>
-RTX_HD f3 shade_sample(const SceneView& S, const SplitBuf& sb, int64_t r) {
-    if (!(sb.rec[r].flags & kSpHit)) return mk(0.0f, 0.0f, 0.0f);  // miss -> black
-    if (SEC)
-        for (int32_t nx = sb.rec[r].next; nx >= 0; nx = sb.rec[r].next) r = nx;
-    // from the deepest record up: a diffuse hit ends the chain with its own clamped
-    // colour; a mirror / refractive one blends its lighting with its child's colour (black
-    // when the child ray was not traced or missed: TIR, the depth limit)
     f3 tail = mk(0.0f, 0.0f, 0.0f);
-    bool deepest = true;
-    for (int64_t p = r; p >= 0;) {
-        const ShadePt R = sb.rec[p];
-        const DMat m = RTX_MAT(S, R.mat);
-        const f3 L = record_lighting<MESH>(S, R, m);
-        tail = (deepest && !(R.flags & kSpChain)) ? clamp01(L) : clamp01(add(scale(L, m.tint), scale(tail, m.omt)));
-        deepest = false;
-        p = SEC ? R.prev : -1;
+    for (int k = 0; k < (SEC ? kMaxDepth : 1); ++k) {
+        const int32_t mi = (int32_t)(meta >> kSpMatShift);
+        const DMat m = RTX_MAT(S, mi);
+        const f3 pos = mk(sb.f(kSpPx)[r], sb.f(kSpPy)[r], sb.f(kSpPz)[r]);
+        const f3 n = mk(sb.f(kSpNx)[r], sb.f(kSpNy)[r], sb.f(kSpNz)[r]);
+        const int32_t gobj = sb.i(kSpGobj)[r];
+        const f3 diffuse = gobj >= 0 ? get_diffuse(S, S.objs[gobj], pos, time) : ld3(m.diffuse);
+        const f3 lit = regular_lighting<MESH, true, false>(S, d, pos, n, m, diffuse, time, tl, hs, (int64_t)sb.u(kSpOcc)[r]);
+        if (!SEC || !(meta & kSpChain)) {  // a diffuse hit ends the chain with its clamped colour
+            tail = clamp01(lit);
+            break;
+        }
+        const int32_t nx = sb.i(kSpNext)[r];
+        if (nx < 0) {  // the child ray missed, or total internal reflection: black child
+            tail = clamp01(add(scale(lit, m.tint), scale(tail, m.omt)));
+            break;
+        }
+        fs.put(nfr++, lit, mi);
+        // the child's ray, as trace_sample cast it (the stored normal is already negated
+        // inside a refractive object)
+        if (m.type == MAT_MIRROR) {
+            d = reflect(d, n);
+            in_shape = false;
+        } else {
+            d = refract(d, n, in_shape ? m.eta_in : m.eta_out);
+            in_shape = !in_shape;
+        }
+        r = nx;
+        meta = sb.u(kSpMeta)[r];
+    }
+    // from the deepest blending level up: colour = clamp(L * tint + child * (1 - tint))
+    for (int k = nfr - 1; k >= 0; --k) {
+        int32_t mi;
+        const f3 lit = fs.get(k, mi);
+        const DMat m = RTX_MAT(S, mi);
+        tail = clamp01(add(scale(lit, m.tint), scale(tail, m.omt)));
     }
     return tail;
 }
@@ -234,7 +310,7 @@ __device__ __forceinline__ void split_trace(const KParams* __restrict__ Pp, cons
             const int64_t slot = sb.nsamp + base +
                                  (int64_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
-            return slot < sb.cap ? slot : -1;
+            return slot < sb.cap ? slot : -2;
 #else
             (void)hit;
             return -1;
@@ -246,7 +322,7 @@ __device__ __forceinline__ void split_trace(const KParams* __restrict__ Pp, cons
 }
 
 // Pass B: records in index order (level 0 in sample order, then the appended deeper
-// hits), grid-stride over the chunk's count.
+// hits), grid-stride over the chunk's records.
 template <bool MESH, bool COUNT>
 __device__ __forceinline__ void split_shadow(const KParams* __restrict__ Pp, const Launch L, SplitBuf sb) {
     constexpr int B = kBlock<true>;
@@ -254,14 +330,19 @@ __device__ __forceinline__ void split_shadow(const KParams* __restrict__ Pp, con
     const HStack hs{hstack + threadIdx.x, B};
     Tally tl = {};
     const SceneView S = Pp->S;
-    const int64_t n = sb.nsamp + (int64_t)*sb.count;
+    const int64_t n = min(sb.nsamp + (int64_t)*sb.count, sb.cap);  // (appends past cap were refused)
     bool any = false;
     for (int64_t r = (int64_t)blockIdx.x * B + threadIdx.x; r - (int64_t)threadIdx.x < n;
          r += (int64_t)gridDim.x * B) {
-        const bool hit = r < n && (sb.rec[r].flags & kSpHit);
+        const uint32_t meta = r < n ? sb.u(kSpMeta)[r] : 0u;
+        const bool hit = (meta & kSpHit) != 0u;
         if (!RTX_ANY(hit)) continue;
         any = true;
-        if (hit) sb.rec[r].occ = shadow_record<MESH, COUNT>(S, sb.rec[r], tl, hs);
+        if (hit) {
+            const f3 pos = mk(sb.f(kSpPx)[r], sb.f(kSpPy)[r], sb.f(kSpPz)[r]);
+            const float time = Pp->times[(meta >> 2) & (kSpMaxTimes - 1)];
+            sb.u(kSpOcc)[r] = shadow_mask<MESH, COUNT>(S, pos, time, tl, hs);
+        }
     }
     flush_tally<COUNT>(tl, L.counters, any);
 }
@@ -276,7 +357,14 @@ __device__ __forceinline__ void split_shade(const KParams* __restrict__ Pp, cons
     const int PPB = spp_pixels_per_block(Sn, B);
     const int rounds = (PPB * Sn + B - 1) / B;
     const float rS = 1.0f / (float)Sn;  // (a block's samples < 2^22: udiv_small)
-    __shared__ float sbuf[3 * B];
+    // LDS: the frame stacks (SEC: 9 x 14 B per lane, 8,064 B per one-wave block, so 20
+    // blocks share a CU's 160 KB: 5 waves/SIMD) and, aliased onto them, the colours of the
+    // block's samples, written after every lane's stack is dead (one wave per block)
+    constexpr int kStackWords = SEC ? kShadeFrames * 3 * B + kShadeFrames * B / 2 : 0;
+    __shared__ float lds[kStackWords > 3 * B ? kStackWords : 3 * B];
+    float* const sbuf = lds;
+    static_assert(!SEC || B == 64, "the aliased colour buffer needs one wave per block");
+    const ShadeStack fs{lds + threadIdx.x, reinterpret_cast<uint16_t*>(lds + kShadeFrames * 3 * B) + threadIdx.x, B};
     const int64_t npix = sb.nsamp / Sn;  // the chunk's pixels
     const int64_t pix0 = (int64_t)blockIdx.x * PPB;
     const int tid = threadIdx.x;
@@ -287,7 +375,7 @@ __device__ __forceinline__ void split_shade(const KParams* __restrict__ Pp, cons
         const int lp = udiv_small(flat, Sn, rS, s);
         const int64_t p = pix0 + lp;
         f3 c = mk(0.0f, 0.0f, 0.0f);
-        if (lp < PPB && p < npix) c = shade_sample<MESH, SEC>(P.S, sb, p * Sn + s);
+        if (lp < PPB && p < npix) c = shade_sample<MESH, SEC>(P, L, sb, p * Sn + s, fs);
         sbuf[tid] = c.x;
         sbuf[B + tid] = c.y;
         sbuf[2 * B + tid] = c.z;
@@ -312,6 +400,24 @@ __device__ __forceinline__ void split_shade(const KParams* __restrict__ Pp, cons
     if (rounds > 1 && tid < 3 && pix0 < npix) put_channel(frame_fb(L), 3 * (L.pix0 + pix0) + tid, sample_mean(P, acc));
 }
 
+// Chunking of a frame (host; rtx_api.hip render_split and the host emulation share it):
+// a chunk is whole shade blocks of pixels; its record arrays hold one level-0 record per
+// sample plus `ratio` deeper records per sample, within `budget` bytes.
+struct SplitPlan {
+    int64_t chunk;  // pixels per chunk (a multiple of the shade block unless it is the whole frame)
+    int64_t cap;    // records per chunk
+};
+#if !defined(__HIPCC_RTC__)
+inline SplitPlan split_plan(int64_t npix, int spp, int ppb, double ratio, int64_t budget) {
+    const double per_pix = (double)spp * (1.0 + ratio) * (double)kSpBytes;
+    int64_t chunk = std::max<int64_t>(1, (int64_t)((double)budget / per_pix));
+    if (chunk < npix) chunk = std::max<int64_t>(ppb, chunk / ppb * ppb);
+    chunk = std::min(chunk, npix);
+    const int64_t nsamp = chunk * spp;
+    return SplitPlan{chunk, nsamp + (int64_t)std::ceil((double)nsamp * ratio)};
+}
+#endif
+
 #if !defined(__HIPCC_RTC__)
 template <bool MESH, bool SEC, bool COUNT, bool JIT>
 __global__ __launch_bounds__(kBlock<true>, RTX_LB_SPLIT_A) void k_split_trace(const KParams* __restrict__ Pp,
@@ -323,8 +429,9 @@ __global__ __launch_bounds__(kBlock<true>, RTX_LB_SPLIT_B) void k_split_shadow(c
                                                                                const Launch L, SplitBuf sb) {
     split_shadow<MESH, COUNT>(Pp, L, sb);
 }
+// (shade: 5 waves/SIMD, which its LDS stacks allow, needs <= 96 VGPRs)
 template <bool MESH, bool SEC>
-__global__ __launch_bounds__(kBlock<true>) void k_split_shade(const KParams* __restrict__ Pp, const Launch L,
+__global__ __launch_bounds__(kBlock<true>, 5) void k_split_shade(const KParams* __restrict__ Pp, const Launch L,
                                                               SplitBuf sb) {
     split_shade<MESH, SEC>(Pp, L, sb);
 }

@@ -59,19 +59,25 @@ def render(scene, subimage=0, tasks=1, threads=8):
     return img, cnt
 
 
-def render_split(scene, subimage=0, tasks=1, threads=8, chunk_records=1 << 26):
+def render_split(scene, subimage=0, tasks=1, threads=8, budget=1 << 31, ratio=9.0, with_redone=False):
     """The hierarchy/texture scenes' three split passes (csrc/rtx_split.h) on the host,
-    chunked like render_split of librtx.so; same layout as render()."""
+    chunked like render_split of librtx.so (`budget` record bytes per chunk, `ratio` deeper
+    records per sample; the default reserves every level, so no block is redone and the
+    tallies are the passes' own); same layout as render(). with_redone: also the number of
+    blocks rendered again because their chains found the pool full."""
     sd = scene.scene_desc()
     cd, tables = scene.camera_desc(subimage, tasks)
     H = scene.vc.height
     fb = np.zeros((H, cd.ncols, 3), np.float32)
     cnt = np.zeros(16, np.uint64)
+    redone = C.c_int64(0)
     f = lib().rtx_hostemu_render_split
-    f.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_int, C.c_int64]
-    _chk(f(C.addressof(sd), C.addressof(cd), 0, H, fb.ctypes.data, cnt.ctypes.data, threads, chunk_records))
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_int, C.c_int64,
+                  C.c_double, C.c_void_p]
+    _chk(f(C.addressof(sd), C.addressof(cd), 0, H, fb.ctypes.data, cnt.ctypes.data, threads, budget, ratio,
+           C.addressof(redone)))
     img = np.ascontiguousarray(np.transpose(fb[::-1], (1, 0, 2))).astype(np.float64)
-    return img, cnt
+    return (img, cnt, redone.value) if with_redone else (img, cnt)
 
 
 def render_rows(scene, rows, threads=8):

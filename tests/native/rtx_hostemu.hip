@@ -521,25 +521,29 @@ extern "C" int64_t rtx_hostemu_jit_spec(const rtx_scene_desc* sd, const rtx_came
     return (int64_t)s.size();
 }
 
-// The split hierarchy passes (rtx_split.h trace_sample / shadow_record / shade_sample) on
-// the host, chunked like rtx_api.hip render_split (chunk_records: records per chunk), over
-// image rows [row0, row0 + nrows). Deeper records are appended by concurrent threads, so
-// their order varies from run to run; the frame must not.
+// The split hierarchy passes (rtx_split.h trace_sample / shadow_mask / shade_sample) on
+// the host, chunked like rtx_api.hip render_split (split_plan with `budget` bytes and
+// `ratio` deeper records per sample), over image rows [row0, row0 + nrows). Deeper records
+// are appended by concurrent threads, so their order varies from run to run; the frame
+// must not. Blocks whose chains found the pool full are rendered again per pixel
+// (render_pixel: the one-kernel form's sums), as the device's redo launch does.
 template <bool MESH, bool SEC, bool JIT>
-static void split_frame(const KParams& k, const Launch& L0, int64_t npix, int spp, int64_t chunk_records, float* fb,
-                        uint64_t* tot, int threads) {
-    const int levels = SEC ? kMaxDepth : 1;
-    int64_t chunk = std::max<int64_t>(1, chunk_records / ((int64_t)spp * levels));
-    chunk = std::min(chunk, npix);
-    const int64_t cap = chunk * spp * levels;
-    std::vector<ShadePt> rec((size_t)cap);
+static void split_frame(const KParams& k, const Launch& L0, int64_t npix, int spp, int64_t budget, double ratio,
+                        float* fb, uint64_t* tot, int threads, int64_t* redone) {
+    const int ppb = spp_pixels_per_block(spp, kBlock<true>);
+    const SplitPlan pl = split_plan(npix, spp, ppb, SEC ? ratio : 0.0, budget);
+    const int64_t chunk = pl.chunk, cap = pl.cap;
+    std::vector<uint32_t> words((size_t)(cap * kSpArrays));
+    std::vector<uint32_t> redo_list((size_t)((chunk + ppb - 1) / ppb)), redo_flag(redo_list.size(), 0u);
     unsigned int count = 0;
+    uint32_t redo_n = 0;
     for (int64_t p0 = 0; p0 < npix; p0 += chunk) {
         const int64_t np = std::min(chunk, npix - p0), nq = np * spp;
         Launch L = L0;
         L.pix0 = (int32_t)p0;
         count = 0;
-        const SplitBuf sb{rec.data(), &count, nq, cap};
+        redo_n = 0;
+        const SplitBuf sb{words.data(), &count, &redo_n, redo_list.data(), redo_flag.data(), nq, cap};
 #pragma omp parallel num_threads(threads > 0 ? threads : 1)
         {
             uint64_t loc[RTX_COUNTERS] = {};
@@ -551,26 +555,31 @@ static void split_frame(const KParams& k, const Launch& L0, int64_t npix, int sp
                 auto alloc = [&](bool hit) -> int64_t {
                     if (!hit) return -1;
                     const int64_t slot = sb.nsamp + (int64_t)__atomic_fetch_add(sb.count, 1u, __ATOMIC_RELAXED);
-                    return slot < sb.cap ? slot : -1;
+                    return slot < sb.cap ? slot : -2;
                 };
                 trace_sample<MESH, SEC, true, JIT>(k, L, sb, q, tl, hs, alloc);
                 for (int c = 0; c < kMaxDepth; ++c) loc[c] += tl.cast[c];
                 loc[RTX_CNT_TRI] += tl.tri;
             }
-            const int64_t n = sb.nsamp + (int64_t)__atomic_load_n(sb.count, __ATOMIC_RELAXED);
+            const int64_t n = std::min(sb.cap, sb.nsamp + (int64_t)__atomic_load_n(sb.count, __ATOMIC_RELAXED));
 #pragma omp for schedule(dynamic, 64)
             for (int64_t r = 0; r < n; ++r) {
-                if (!(rec[r].flags & kSpHit)) continue;
+                const uint32_t meta = sb.u(kSpMeta)[r];
+                if (!(meta & kSpHit)) continue;
                 Tally tl = {};
-                rec[r].occ = shadow_record<MESH, true>(k.S, rec[r], tl, hs);
+                const f3 pos = mk(sb.f(kSpPx)[r], sb.f(kSpPy)[r], sb.f(kSpPz)[r]);
+                sb.u(kSpOcc)[r] = shadow_mask<MESH, true>(k.S, pos, k.times[(meta >> 2) & (kSpMaxTimes - 1)], tl, hs);
                 loc[RTX_CNT_SHADOW] += tl.shadow;
                 loc[RTX_CNT_SHADE] += tl.shade;
                 loc[RTX_CNT_TRI] += tl.tri;
             }
+            float fst[kShadeFrames * 3];
+            uint16_t fsm[kShadeFrames];
+            const ShadeStack fsc{fst, fsm, 1};
 #pragma omp for schedule(dynamic, 16)
             for (int64_t p = 0; p < np; ++p) {
                 f3 colour = mk(0.0f, 0.0f, 0.0f);
-                for (int s = 0; s < spp; ++s) colour = add(colour, shade_sample<MESH, SEC>(k.S, sb, p * spp + s));
+                for (int s = 0; s < spp; ++s) colour = add(colour, shade_sample<MESH, SEC>(k, L, sb, p * spp + s, fsc));
                 const int64_t o = 3 * (p0 + p);
                 fb[o] = sample_mean(k, colour.x);
                 fb[o + 1] = sample_mean(k, colour.y);
@@ -579,12 +588,28 @@ static void split_frame(const KParams& k, const Launch& L0, int64_t npix, int sp
 #pragma omp critical
             for (int c = 0; c < RTX_COUNTERS; ++c) tot[c] += loc[c];
         }
+        // the redo blocks (their tallies are not counted: the device's counting renders
+        // reserve every level, so they never redo)
+        for (uint32_t i = 0; i < redo_n; ++i) {
+            const int64_t b = redo_list[i];
+            redo_flag[(size_t)b] = 0u;
+            ++*redone;
+            float fst[kMaxDepth * kFrameWords];
+            const FrameStack fs{fst, 1};
+            float hst[kMaxHLevels * 9];
+            const HStack hs{hst, 1};
+            for (int64_t p = p0 + b * ppb; p < std::min(p0 + (b + 1) * ppb, p0 + np); ++p) {
+                Tally tl = {};
+                const int32_t rr = (int32_t)(p / k.ncols), cc = (int32_t)(p - (int64_t)rr * k.ncols);
+                render_pixel<MESH, SEC, true, false, JIT>(k, fb, image_row(L, rr) - rr, rr, cc, tl, fs, hs, -1);
+            }
+        }
     }
 }
 
 extern "C" int rtx_hostemu_render_split(const rtx_scene_desc* sd, const rtx_camera_desc* cd, int32_t row0,
                                         int32_t nrows, float* fb, uint64_t* counters, int threads,
-                                        int64_t chunk_records) {
+                                        int64_t budget, double ratio, int64_t* redone) {
     HostScene H;
     int rc = convert_scene(sd, H);
     if (rc) return rc;
@@ -632,14 +657,14 @@ extern "C" int rtx_hostemu_render_split(const rtx_scene_desc* sd, const rtx_came
     const bool jit = k.jitter != RTX_JITTER_OFF;
     const int sel = (H.has_mesh ? 4 : 0) | (H.has_secondary ? 2 : 0) | (jit ? 1 : 0);
     switch (sel) {
-        case 0: split_frame<false, false, false>(k, L, npix, spp, chunk_records, fb, tot, threads); break;
-        case 1: split_frame<false, false, true>(k, L, npix, spp, chunk_records, fb, tot, threads); break;
-        case 2: split_frame<false, true, false>(k, L, npix, spp, chunk_records, fb, tot, threads); break;
-        case 3: split_frame<false, true, true>(k, L, npix, spp, chunk_records, fb, tot, threads); break;
-        case 4: split_frame<true, false, false>(k, L, npix, spp, chunk_records, fb, tot, threads); break;
-        case 5: split_frame<true, false, true>(k, L, npix, spp, chunk_records, fb, tot, threads); break;
-        case 6: split_frame<true, true, false>(k, L, npix, spp, chunk_records, fb, tot, threads); break;
-        case 7: split_frame<true, true, true>(k, L, npix, spp, chunk_records, fb, tot, threads); break;
+        case 0: split_frame<false, false, false>(k, L, npix, spp, budget, ratio, fb, tot, threads, redone); break;
+        case 1: split_frame<false, false, true>(k, L, npix, spp, budget, ratio, fb, tot, threads, redone); break;
+        case 2: split_frame<false, true, false>(k, L, npix, spp, budget, ratio, fb, tot, threads, redone); break;
+        case 3: split_frame<false, true, true>(k, L, npix, spp, budget, ratio, fb, tot, threads, redone); break;
+        case 4: split_frame<true, false, false>(k, L, npix, spp, budget, ratio, fb, tot, threads, redone); break;
+        case 5: split_frame<true, false, true>(k, L, npix, spp, budget, ratio, fb, tot, threads, redone); break;
+        case 6: split_frame<true, true, false>(k, L, npix, spp, budget, ratio, fb, tot, threads, redone); break;
+        case 7: split_frame<true, true, true>(k, L, npix, spp, budget, ratio, fb, tot, threads, redone); break;
     }
     if (counters)
         for (int q = 0; q < RTX_COUNTERS; ++q) counters[q] = tot[q];

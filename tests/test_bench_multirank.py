@@ -58,6 +58,9 @@ def _worker(rank, world, port, res, steps, out_q):
     mg, frame = bench.measure_sharded(sc, rank, world, steps, 2, True, torch.device("cpu"), sync=lambda: None,
                                       render_rows=render_rows, render_block=render_block,
                                       render_block_k=render_block_k, graph=False)
+    # the scaling config's sharded frame beside the value (here the same scene stands in)
+    mg["scaling_config"] = bench.sharded_config_field("dof4k", sc, rank, world, 2, 1, True, torch.device("cpu"),
+                                                      sync=lambda: None, render_rows=render_rows)
     out_q.put((rank, mg, None if frame is None else frame.clone().numpy(), calls[0]))
     dist.barrier()
     dist.destroy_process_group()
@@ -90,6 +93,41 @@ def test_bench_sharded_frame_loop(world, res):
     W, H = res
     assert mg0["throughput"]["Mrays_s"] > 0 and mg0["gather_to_rank0"]["Mrays_s"] > 0
     assert mg0["rows_per_rank"] == [min(len(r) for r in _parts(H, world)), max(len(r) for r in _parts(H, world))]
+    # the fields the 1 -> N comparison needs: the scaling config's sharded frame at N > 1 ...
+    sc_f = mg0["scaling_config"]
+    assert sc_f["config"] == "dof4k" and sc_f["frame_ms"] > 0 and sc_f["Mrays_s"] > 0
+    for r in range(1, world):
+        assert got[r][0]["scaling_config"]["frame_ms"] == sc_f["frame_ms"]  # max over ranks
+
+
+def test_bench_n1_line_has_rgb8_frame():
+    """... and at N = 1 the uint8 frame (the bytes every N > 1 rank renders) beside the
+    fp32 one: bench.rgb8_field with the host emulation's uint8 frame and a wall timer."""
+    import sys
+    import time
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), "python-raytracer_amd"), here):
+        sys.path.insert(0, p)
+    import bench
+    import hostemu
+    from common import product_scene, oracle_render
+    from oracle import oracle as O
+    from rtx.distributed import to_rgb8
+    res = (24, 16)
+    sc = product_scene("TwoSpheresPlane", res)
+    out = {}
+
+    def frame_u8():
+        out["f"] = to_rgb8(torch.from_numpy(hostemu.render_rows(sc, np.arange(res[1]), threads=2)))
+
+    def timer(fn, n):
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        return (time.perf_counter() - t0) * 1e3 / n
+    f = bench.rgb8_field(frame_u8, 2, timer, res[0], res[1], 1, lambda: "hostemu")
+    assert f["frame_ms"] > 0 and f["Mrays_s"] > 0 and f["kernel"] == "hostemu"
+    assert np.array_equal(out["f"].numpy(), O.to_png_array(oracle_render("TwoSpheresPlane", res)))
 
 
 def _parts(H, world):

@@ -53,8 +53,8 @@ def test_split_tallies_match_oracle(split):
 
 
 def test_split_small_chunks_and_row_groups(split, monkeypatch):
-    """Many chunks (RTX_SPLIT_RECORDS small) and interleaved 8-row groups: the same frame."""
-    monkeypatch.setenv("RTX_SPLIT_RECORDS", "4000")
+    """Many chunks (RTX_SPLIT_BYTES small) and interleaved 8-row groups: the same frame."""
+    monkeypatch.setenv("RTX_SPLIT_BYTES", str(4000 * 40))
     name, res, edits = "NovelScene1", (80, 40), {"AA": {"jitter": False, "samples": 2}}
     sc = product_scene(name, res, **edits)
     ref = oracle_render(name, res, **edits)
@@ -104,3 +104,79 @@ def test_split_many_roots_bins_and_grids(seed, split, monkeypatch):
     img = np.ascontiguousarray(np.transpose(a.cpu().numpy()[::-1], (1, 0, 2))).astype(np.float64)
     noise = PH.jitter_noise(sc.seed, 0, 96, 64, sc.vc.dof_samples, sc.samples)
     assert_parity(img, oracle_render_dict(d, noise=noise), "many roots seed %d" % seed)
+
+
+@pytest.mark.parametrize("ratio,budget", [("0", None), ("0.02", str(3000 * 40)), ("0.3", None)])
+def test_split_pool_overflow_redo(ratio, budget, split, monkeypatch):
+    """A deeper-record pool smaller than the chains need: hits that find it full mark their
+    blocks, and the one-kernel form renders those again after pass C (render_body_spp with
+    L.redo) -- the frame is the oracle's, bit for bit, on frames with many mirrors."""
+    from scenegen import random_hier_scene
+    monkeypatch.setenv("RTX_SPLIT_RATIO", ratio)
+    if budget:
+        monkeypatch.setenv("RTX_SPLIT_BYTES", budget)
+    for seed in (3, 5):
+        d = random_hier_scene(seed, res=(40, 30))
+        d["materials"] = [dict(m, type="mirror", tint=m.get("tint", 0.3)) if i % 2 == 0 else m
+                          for i, m in enumerate(d["materials"])]
+        sc = product_scene_dict(d)
+        img = sc.render()
+        assert sc.last_kernel.startswith("k_split_"), sc.last_kernel
+        assert_parity(img, oracle_render_dict(d), "pool overflow %s seed %d" % (ratio, seed))
+
+
+def test_split_pool_learns_and_frames_repeat(split):
+    """The learned pool (no fixed ratio): the first frame may redo blocks, later frames size
+    the pool from the first's counters; every frame is the same bytes."""
+    name, res, edits = "NovelScene1", (160, 80), {"AA": {"jitter": False, "samples": 2}}
+    sc = product_scene(name, res, **edits)
+    frames = []
+    for _ in range(4):
+        frames.append(sc.render_device().clone())
+        torch.cuda.synchronize()
+    for f in frames[1:]:
+        assert torch.equal(f, frames[0])
+    img = np.ascontiguousarray(np.transpose(frames[0].cpu().numpy()[::-1], (1, 0, 2))).astype(np.float64)
+    assert_parity(img, oracle_render(name, res, **edits), name)
+
+
+def test_split_renders_on_two_streams(split):
+    """Renders of one hierarchy scene on two streams share its record buffers: the library
+    orders them (each waits for the other's last split render), so both frames are right."""
+    name, res, edits = "NovelScene2", (96, 48), {"AA": {"jitter": False, "samples": 2}}
+    sc = product_scene(name, res, **edits)
+    ref = sc.render_device().clone()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    for k in range(6):
+        st = s1 if k % 2 == 0 else s2
+        o = torch.empty_like(ref)
+        sc.render_device(out=o, stream=st)
+        outs.append(o)
+    torch.cuda.synchronize()
+    for o in outs:
+        assert torch.equal(o, ref)
+
+
+def test_split_capture_needs_a_first_render(split):
+    """Graph capture of a hierarchy scene whose record buffer does not exist yet is refused
+    (the library does not allocate inside a capture); after one eager render the capture
+    works and its replays give the eager frame."""
+    from rtx._native import RtxError
+    name, res, edits = "NovelScene1", (64, 32), {"AA": {"jitter": False, "samples": 2}}
+    sc = product_scene(name, res, **edits)
+    sc._set_camera(0, 1)
+    out = torch.empty((res[1], res[0], 3), dtype=torch.float32, device="cuda")
+    st = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with pytest.raises(RtxError):
+        with torch.cuda.graph(g, stream=st):
+            sc.render_device(out=out, stream=st)
+    ref = sc.render_device().clone()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        sc.render_device(out=out, stream=st)
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)

@@ -924,18 +924,32 @@ SPLIT_CASES = [("NovelScene1", (64, 32), {"AA": {"jitter": False, "samples": 2}}
                ("NovelScene2", (48, 24), {"AA": {"jitter": False, "samples": 1}})]
 
 
-@pytest.mark.parametrize("chunk", [1 << 26, 2000])
+@pytest.mark.parametrize("budget", [1 << 31, 2000 * 40])
 @pytest.mark.parametrize("name,res,edits", SPLIT_CASES)
-def test_hostemu_split_passes_bit_exact(name, res, edits, chunk):
+def test_hostemu_split_passes_bit_exact(name, res, edits, budget):
     """The hierarchy scenes' three split passes (csrc/rtx_split.h: chains of closest hits,
     then shadow rays per record, then lighting + unwinding + the ordered mean), host build,
     one chunk or many: bit-identical to the oracle, with its ray tallies."""
     sc = product_scene(name, res, **edits)
-    img, cnt = hostemu.render_split(sc, chunk_records=chunk)
+    img, cnt = hostemu.render_split(sc, budget=budget)
     ref, tl = oracle_render(name, res, tallies=True, **edits)
     assert_parity(img, ref, name)
     assert list(cnt[:10]) == tl[:10]
     assert cnt[10] == tl[11] and cnt[11] == tl[12]
+
+
+@pytest.mark.parametrize("ratio,budget", [(0.0, 1 << 31), (0.02, 3000 * 40), (0.3, 1 << 31)])
+def test_hostemu_split_pool_overflow_redo(ratio, budget):
+    """A deeper-record pool smaller than the chains need (rtx_split.h): the hits that find
+    it full mark their blocks, which are rendered again in the one-kernel form -- the frame
+    is still the oracle's, bit for bit, and blocks were in fact redone."""
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import random_hier_scene
+    d = random_hier_scene(3, res=(40, 30))
+    d["materials"] = [dict(m, type="mirror", tint=m.get("tint", 0.3)) if i % 2 == 0 else m for i, m in enumerate(d["materials"])]
+    img, _, redone = hostemu.render_split(product_scene_dict(d), budget=budget, ratio=ratio, with_redone=True)
+    assert_parity(img, oracle_render_dict(d), "pool overflow %g" % ratio)
+    assert redone > 0
 
 
 @pytest.mark.parametrize("seed", range(12))
@@ -945,7 +959,7 @@ def test_hostemu_split_random_hierarchy_scenes(seed):
     from common import oracle_render_dict, product_scene_dict
     from scenegen import random_hier_scene
     d = random_hier_scene(seed, mesh=(seed % 4 == 0))
-    img, cnt = hostemu.render_split(product_scene_dict(d), chunk_records=3000)
+    img, cnt = hostemu.render_split(product_scene_dict(d), budget=3000 * 40)
     ref, tl = oracle_render_dict(d, tallies=True)
     assert_parity(img, ref, "seed %d" % seed)
     assert list(cnt[:10]) == tl[:10] and cnt[10] == tl[11]

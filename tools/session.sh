@@ -10,6 +10,8 @@
 # bench     the default bench line (N = 1, with CPU baselines unless CPU=0)
 # configs   bench.py --config C for C in CONFIGS (CPU=1 adds the CPU legs to each line)
 # ab        tools/ab_jitflags.sh: VARIANTS="name=jit flags;..." over CONFIGS
+# abl       tools/ab_lib.sh: LIBS="name=_abl/librtx_x.so;name2=default" over CONFIGS (ROUNDS times,
+#           interleaved)
 # pmc       rocprofv3 counter passes (FETCH_SIZE, WRITE_SIZE, instruction mix) per CONFIGS
 #           -> $OUT/pmc_<config>.json
 # rocprof   rocprofv3 --kernel-trace --stats of the default bench
@@ -51,6 +53,11 @@ for s in ${STEPS:-tests smoke bench rocprof}; do
     ab)
       CONFIGS="$CFGS" bash tools/ab_jitflags.sh > "$OUT/ab.log" 2>&1 || { tail "$OUT/ab.log"; exit 1; }
       cat "$OUT/ab.log"; mkdir -p "$OUT/ab"; cp gpurun_out/abj/*.json "$OUT/ab/" ;;
+    abl)
+      for r in $(seq 1 ${ROUNDS:-2}); do
+        VARIANTS="$LIBS" CONFIGS="$CFGS" STEPS=${BSTEPS:-10} bash tools/ab_lib.sh > "$OUT/abl_$r.log" 2>&1 || { tail "$OUT/abl_$r.log"; exit 1; }
+        cat "$OUT/abl_$r.log"; mkdir -p "$OUT/abl_$r"; cp gpurun_out/abl/*.json "$OUT/abl_$r/"
+      done ;;
     pmc)
       for c in $CFGS; do
         CFG=$c TAG="${OUT#gpurun_out/}/pmc_$c" bash tools/pmc_session.sh > "$OUT/pmc_$c.log" 2>&1 || { tail "$OUT/pmc_$c.log"; exit 1; }
