@@ -1311,7 +1311,7 @@ bool light_grids(const HostScene& H, std::vector<DLGrid>& grids, std::vector<int
 // -- twice the bound -- stays below 1e-4 min |D_a| / 2: their own shadow test cannot pass
 // for such a hit point and is skipped. omax bounds |o| of the camera's sample origins
 // (camera_origin_bound).
-bool dir_shadow_grids(const HostScene& H, const std::vector<DBound>& nb, double tlo, double thi, double omax,
+bool dir_shadow_grids(const HostScene& H, const std::vector<DBound>& nb, double tlo, double thi,
                       std::vector<DSGrid>& grids, std::vector<DSCell>& cells) {
     grids.assign(H.lights.size(), DSGrid{});
     cells.clear();
@@ -1469,23 +1469,6 @@ bool dir_shadow_grids(const HostScene& H, const std::vector<DBound>& nb, double 
         g.off = (int32_t)cells.size();
         g.always = always;
         g.always_root = always_root;
-        double dmin = INFINITY;
-        for (int q = 0; q < 3; ++q)
-            if (d[q] != 0.0) dmin = std::min(dmin, std::fabs(d[q]));
-        const char* es = getenv("RTX_SELF_SKIP");  // experiment: 0 = every box tests itself
-        if (H.n_box <= 16 && std::isfinite(omax) && !(es && es[0] == '0')) {
-            for (int32_t k = 0; k < H.n_box; ++k) {
-                const DObj& ob = H.objs[H.n_plane + H.n_sphere + k];
-                if (ob.has_speed) continue;
-                double pm = 0.0;
-                for (int q = 0; q < 3; ++q) {
-                    const double m = std::max(std::fabs((double)ob.a[q]), std::fabs((double)ob.b[q]));
-                    pm += m * m;
-                }
-                const double delta = 0x1p-21 * (std::sqrt(pm) + omax);
-                if (2.0 * delta < 1e-4 * dmin) g.self_boxes |= 1u << (16 + k);
-            }
-        }
         cells.resize(cells.size() + (size_t)G * G, DSCell{0u, 0u});
         auto cell = [&](double u, double o0, double s) {  // as the device maps it, +-1 below
             return (int32_t)std::floor((u - o0) * s);
@@ -1505,6 +1488,33 @@ bool dir_shadow_grids(const HostScene& H, const std::vector<DBound>& nb, double 
         any = true;
     }
     return any;
+}
+
+// The self-test marks of the grids (DSGrid.self_boxes, see above): per camera, as they
+// depend on omax (camera_origin_bound); the grids and their cells depend on the frame's
+// time range only.
+void dir_self_boxes(const HostScene& H, std::vector<DSGrid>& grids, double omax) {
+    const char* es = getenv("RTX_SELF_SKIP");  // 0 = every box tests itself
+    for (size_t li = 0; li < grids.size() && li < H.lights.size(); ++li) {
+        DSGrid& g = grids[li];
+        g.self_boxes = 0u;
+        if (g.G == 0 || H.n_box > 16 || !std::isfinite(omax) || (es && es[0] == '0')) continue;
+        const DLight& Lt = H.lights[li];
+        double dmin = INFINITY;
+        for (int q = 0; q < 3; ++q)
+            if (Lt.negvec[q] != 0.0f) dmin = std::min(dmin, std::fabs((double)Lt.negvec[q]));
+        for (int32_t k = 0; k < H.n_box; ++k) {
+            const DObj& ob = H.objs[H.n_plane + H.n_sphere + k];
+            if (ob.has_speed) continue;
+            double pm = 0.0;
+            for (int q = 0; q < 3; ++q) {
+                const double m = std::max(std::fabs((double)ob.a[q]), std::fabs((double)ob.b[q]));
+                pm += m * m;
+            }
+            const double delta = 0x1p-21 * (std::sqrt(pm) + omax);
+            if (2.0 * delta < 1e-4 * dmin) g.self_boxes |= 1u << (16 + k);
+        }
+    }
 }
 
 }  // namespace
@@ -1955,18 +1965,10 @@ struct rtx_scene {
     std::vector<DTri> h_tris;
     std::vector<DBox> h_bounds_abi;
     HostScene h_bins;   // objs/tris and type counts, for the camera's primary-ray face bins
-    int32_t* d_bin_start = nullptr;
-    int32_t* d_bin_faces = nullptr;
-    float* d_bin_zmin = nullptr;
-    uint32_t* d_bin_mask = nullptr;
     void* d_lgrid = nullptr;        // light grids (per scene: lights and mesh are static)
-    void* d_dsgrid = nullptr;       // directional lights' shadow grids (per camera)
-    void* d_dsg_cells = nullptr;
-    void* d_plane_self = nullptr;   // self tests of planes (per camera)
     void* d_lg_start = nullptr;
     void* d_lg_faces = nullptr;
     void* d_lg_d2 = nullptr;
-    void* d_bounds_cam = nullptr;   // for the camera's motion times
     void* d_bounds_abi = nullptr;   // for the time of the last rtx_intersect / rtx_occluded
     void* d_nodes = nullptr;
     void* d_nmat = nullptr;
@@ -1980,16 +1982,23 @@ struct rtx_scene {
     void* d_lights = nullptr;
     void* d_leaves = nullptr;
     void* d_tri_orig = nullptr;
-    // camera
+    // camera: every per-camera table (pixel tables, sample origins, motion times, replayed
+    // noise, hierarchy bounds, self-test limits, shadow-grid headers, primary-ray bins, tile
+    // schedule, and the KParams block) in ONE device buffer, uploaded with one copy and
+    // reused by later cameras while it is large enough (rtx_camera_set)
     bool cam_set = false;
     KParams kp{};
-    float* d_xs = nullptr;
-    float* d_ys = nullptr;
-    float* d_dof = nullptr;
-    float* d_aa = nullptr;
-    float* d_times = nullptr;
-    float* d_noise = nullptr;
-    KParams* d_kp = nullptr;
+    char* d_cam = nullptr;
+    size_t cam_cap = 0;
+    KParams* d_kp = nullptr;  // (inside d_cam)
+    // per frame time range [tlo, thi] (not per camera): the hierarchy bounds and the
+    // directional lights' shadow-grid headers and cells (the cells in their own buffer)
+    bool tr_valid = false;
+    float tr_lo = 0.0f, tr_hi = 0.0f;
+    std::vector<DBound> tr_bounds;
+    std::vector<DSGrid> tr_grids;
+    bool tr_grids_on = false, tr_dsg_off = false;
+    void* d_dsg_cells = nullptr;
     // the kernel resolved for each (counters, jitter, sample-parallel) variant of the
     // current camera: looked up (and compiled) once per camera, not per frame; nullptr
     // after a lookup means the generic kernel
@@ -2045,28 +2054,10 @@ int upload(void** dptr, const std::vector<T>& v) {
     return RTX_OK;
 }
 
+// Forgets the camera (its kernels are specialized on its sample counts); the device
+// buffers stay for the next camera (free_scene frees them).
 void free_camera(rtx_scene* s) {
-    for (float* p : {s->d_xs, s->d_ys, s->d_dof, s->d_aa, s->d_times, s->d_noise}) (void)hipFree(p);
-    for (int32_t* p : {s->d_bin_start, s->d_bin_faces}) (void)hipFree(p);
-    (void)hipFree(s->d_bin_zmin);
-    (void)hipFree(s->d_bin_mask);
-    s->d_bin_start = s->d_bin_faces = nullptr;
-    s->d_bin_zmin = nullptr;
-    s->d_bin_mask = nullptr;
-    (void)hipFree(s->d_bounds_cam);
-    s->d_bounds_cam = nullptr;
-    (void)hipFree(s->d_dsgrid);
-    (void)hipFree(s->d_dsg_cells);
-    (void)hipFree(s->d_plane_self);
-    s->d_dsgrid = s->d_dsg_cells = s->d_plane_self = nullptr;
-    (void)hipFree(s->d_kp);
-    (void)hipFree(s->d_tile_perm);
-    (void)hipFree(s->d_tile_time);
-    s->d_tile_perm = nullptr;
-    s->d_tile_time = nullptr;
     s->tile_sched = 0;
-    s->d_xs = s->d_ys = s->d_dof = s->d_aa = s->d_times = s->d_noise = nullptr;
-    s->d_kp = nullptr;
     s->cam_set = false;
     for (auto& r : s->resolved) {  // specialized on the camera's sample counts
         jit_release(r.key);
@@ -2076,6 +2067,8 @@ void free_camera(rtx_scene* s) {
 
 void free_scene(rtx_scene* s) {
     free_camera(s);
+    (void)hipFree(s->d_cam);
+    (void)hipFree(s->d_dsg_cells);
     (void)hipFree(s->d_scratch);
     if (s->split_done) (void)hipEventSynchronize(s->split_done);
     (void)hipFree(s->d_split);
@@ -2091,6 +2084,22 @@ void free_scene(rtx_scene* s) {
         (void)hipFree(p);
     delete s;
 }
+
+}  // namespace
+
+namespace {
+// Host staging of the camera tables: 256-byte aligned segments of one buffer.
+struct CamStage {
+    std::vector<char> b;
+    size_t put(const void* p, size_t n) {
+        const size_t off = (b.size() + 255) & ~(size_t)255;
+        b.resize(off + std::max<size_t>(n, 4));
+        if (n) memcpy(b.data() + off, p, n);
+        return off;
+    }
+    template <class T>
+    size_t put(const std::vector<T>& v) { return put(v.data(), sizeof(T) * v.size()); }
+};
 
 }  // namespace
 
@@ -2217,81 +2226,118 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     const size_t nsamp = (size_t)c->n_dof * c->n_aa;
     std::vector<float> times(c->n_times);
     for (int i = 0; i < c->n_times; ++i) times[i] = (float)c->times[i];  // current_time * speed casts to fp32
-    auto up = [&](float** d, const float* h, size_t n) -> int {
-        RTX_HIP(hipMalloc((void**)d, sizeof(float) * n));
-        RTX_HIP(hipMemcpy(*d, h, sizeof(float) * n, hipMemcpyHostToDevice));
-        return RTX_OK;
-    };
-    if ((rc = up(&s->d_xs, c->xs, c->ncols)) || (rc = up(&s->d_ys, c->ys, c->height)) ||
-        (rc = up(&s->d_dof, c->dof_origins, 3 * (size_t)c->n_dof)) || (rc = up(&s->d_aa, c->aa_origins, 3 * nsamp)) ||
-        (rc = up(&s->d_times, times.data(), times.size())))
-        return rc;
-    if (c->jitter == RTX_JITTER_REPLAY && (rc = up(&s->d_noise, c->noise, 3 * (size_t)c->ncols * c->height * nsamp)))
-        return rc;
-    k.S = s->view;
     const auto mm = std::minmax_element(times.begin(), times.end());
-    std::vector<DBound> nbounds;
-    if (!s->h_nodes.empty()) {  // hierarchy bounds over the frame's motion-time range
-        nbounds = compute_bounds(s->h_nodes, s->h_objs, s->h_tris, *mm.first, *mm.second);
-        if ((rc = upload(&s->d_bounds_cam, split_bounds(nbounds)))) return rc;
-        bind_boxes(k.S, (const DBox*)s->d_bounds_cam, s->h_nodes.size());
-    }
-    {  // self tests of planes (RTX_SELF_SKIP=0: none). Scenes with secondary rays get none:
-        // MirrorRefraction measured 1.4 % slower with them (most of its shadow rays leave
-        // deeper levels, which pay the check and never skip), TSP 3 % and TM 2 % faster
-        // (profiles/r04/plane_self/)
-        const char* es = getenv("RTX_SELF_SKIP");
-        if (!(es && es[0] == '0') && s->view.n_plane > 0 && !s->h_bins.lights.empty() && !s->has_secondary) {
-            if ((rc = upload(&s->d_plane_self, plane_self_limits(s->h_bins, camera_origin_bound(c))))) return rc;
-            k.S.plane_self = (cptr<float>)s->d_plane_self;
-        }
-    }
-    {  // shadow grids of directional lights (RTX_DSGRID=0: every ray tests every object)
-        std::vector<DSGrid> grids;
+    const double omax = camera_origin_bound(c);
+    k.S = s->view;
+    // what depends on the frame's time range only: computed again when it changes
+    const char* edsg = getenv("RTX_DSGRID");  // 0: every shadow ray tests every object
+    const bool dsg_off = edsg && edsg[0] == '0';
+    if (!s->tr_valid || s->tr_lo != *mm.first || s->tr_hi != *mm.second || s->tr_dsg_off != dsg_off) {
+        s->tr_bounds.clear();
+        if (!s->h_nodes.empty())  // hierarchy bounds over the frame's motion-time range
+            s->tr_bounds = compute_bounds(s->h_nodes, s->h_objs, s->h_tris, *mm.first, *mm.second);
         std::vector<DSCell> cells;
-        const char* e = getenv("RTX_DSGRID");
-        if (!(e && e[0] == '0') &&
-            dir_shadow_grids(s->h_bins, nbounds, *mm.first, *mm.second, camera_origin_bound(c), grids, cells)) {
-            if ((rc = upload(&s->d_dsgrid, grids)) || (rc = upload(&s->d_dsg_cells, cells))) return rc;
-            k.S.dsgrid = (cptr<DSGrid>)s->d_dsgrid;
-            k.S.dsg_cells = (cptr<DSCell>)s->d_dsg_cells;
-            k.S.dsg_on = 1;
-        }
+        s->tr_grids.clear();
+        s->tr_dsg_off = dsg_off;
+        s->tr_grids_on = !dsg_off &&
+                         dir_shadow_grids(s->h_bins, s->tr_bounds, *mm.first, *mm.second, s->tr_grids, cells);
+        (void)hipDeviceSynchronize();  // (frames of the previous camera may still read the cells)
+        (void)hipFree(s->d_dsg_cells);
+        s->d_dsg_cells = nullptr;
+        if (s->tr_grids_on && (rc = upload(&s->d_dsg_cells, cells))) return rc;
+        s->tr_valid = true;
+        s->tr_lo = *mm.first;
+        s->tr_hi = *mm.second;
     }
-    {
-        std::vector<int32_t> bstart, bfaces;
-        std::vector<float> bz;
-        std::vector<uint32_t> bmask, brmask;
-        int32_t bins_x = 0, mesh_bins = 0;
-        const char* e = getenv("RTX_BINS");  // experiment: 0 = no primary-ray bins
-        if (!(e && e[0] == '0') &&
-            primary_bins(s->h_bins, c, nbounds, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins)) {
-            if (bfaces.empty()) { bfaces.push_back(0); bz.push_back(0.0f); }
-            auto upi = [&](int32_t** d, const std::vector<int32_t>& h) -> int {
-                RTX_HIP(hipMalloc((void**)d, sizeof(int32_t) * h.size()));
-                RTX_HIP(hipMemcpy(*d, h.data(), sizeof(int32_t) * h.size(), hipMemcpyHostToDevice));
-                return RTX_OK;
-            };
-            if ((rc = upi(&s->d_bin_start, bstart)) || (rc = upi(&s->d_bin_faces, bfaces))) return rc;
-            RTX_HIP(hipMalloc((void**)&s->d_bin_zmin, sizeof(float) * bz.size()));
-            RTX_HIP(hipMemcpy(s->d_bin_zmin, bz.data(), sizeof(float) * bz.size(), hipMemcpyHostToDevice));
-            bmask.insert(bmask.end(), brmask.begin(), brmask.end());  // [object masks | root masks]
-            RTX_HIP(hipMalloc((void**)&s->d_bin_mask, sizeof(uint32_t) * bmask.size()));
-            RTX_HIP(hipMemcpy(s->d_bin_mask, bmask.data(), sizeof(uint32_t) * bmask.size(), hipMemcpyHostToDevice));
-            k.S.bin_objmask = (cptr<uint32_t>)s->d_bin_mask;
-            k.S.bin_rootmask = (cptr<uint32_t>)s->d_bin_mask + brmask.size();
-            k.S.mesh_bins = mesh_bins;
-            k.S.bin_start = (cptr<int32_t>)s->d_bin_start;
-            k.S.bin_faces = (cptr<int32_t>)s->d_bin_faces;
-            k.S.bin_zmin = (cptr<float>)s->d_bin_zmin;
-            k.S.bins_x = bins_x;
-            k.S.bins_on = 1;
-        }
+    CamStage st;
+    const size_t o_xs = st.put(c->xs, sizeof(float) * c->ncols), o_ys = st.put(c->ys, sizeof(float) * c->height);
+    const size_t o_dof = st.put(c->dof_origins, sizeof(float) * 3 * c->n_dof);
+    const size_t o_aa = st.put(c->aa_origins, sizeof(float) * 3 * nsamp);
+    const size_t o_times = st.put(times);
+    size_t o_noise = 0, o_bounds = 0, o_pself = 0, o_dsg = 0, o_bstart = 0, o_bfaces = 0, o_bz = 0, o_bmask = 0;
+    size_t o_tperm = 0, o_ttime = 0;
+    const bool replay = c->jitter == RTX_JITTER_REPLAY;
+    if (replay) o_noise = st.put(c->noise, sizeof(float) * 3 * (size_t)c->ncols * c->height * nsamp);
+    if (!s->h_nodes.empty()) o_bounds = st.put(split_bounds(s->tr_bounds));
+    // self tests of planes (RTX_SELF_SKIP=0: none). Scenes with secondary rays get none:
+    // MirrorRefraction measured 1.4 % slower with them (most of its shadow rays leave
+    // deeper levels, which pay the check and never skip), TSP 3 % and TM 2 % faster
+    // (profiles/r04/plane_self/)
+    const char* es = getenv("RTX_SELF_SKIP");
+    const bool pself = !(es && es[0] == '0') && s->view.n_plane > 0 && !s->h_bins.lights.empty() && !s->has_secondary;
+    if (pself) o_pself = st.put(plane_self_limits(s->h_bins, omax));
+    if (s->tr_grids_on) {  // the grid headers with this camera's self-test marks
+        std::vector<DSGrid> grids = s->tr_grids;
+        dir_self_boxes(s->h_bins, grids, omax);
+        o_dsg = st.put(grids);
     }
-    k.xs = (cptr<float>)s->d_xs; k.ys = (cptr<float>)s->d_ys; k.dof_o = (cptr<float>)s->d_dof;
-    k.aa_o = (cptr<float>)s->d_aa; k.times = (cptr<float>)s->d_times; k.noise = (cptr<float>)s->d_noise;
-    if (const char* e = getenv("RTX_WAVE_LOG_PTR"))  // tools/wave_timeline.py (RTX_WAVE_LOG kernels)
+    std::vector<int32_t> bstart, bfaces;
+    std::vector<float> bz;
+    std::vector<uint32_t> bmask, brmask;
+    int32_t bins_x = 0, mesh_bins = 0;
+    const char* eb = getenv("RTX_BINS");  // 0 = no primary-ray bins
+    const bool bins = !(eb && eb[0] == '0') &&
+                      primary_bins(s->h_bins, c, s->tr_bounds, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins);
+    if (bins) {
+        if (bfaces.empty()) { bfaces.push_back(0); bz.push_back(0.0f); }
+        bmask.insert(bmask.end(), brmask.begin(), brmask.end());  // [object masks | root masks]
+        o_bstart = st.put(bstart);
+        o_bfaces = st.put(bfaces);
+        o_bz = st.put(bz);
+        o_bmask = st.put(bmask);
+    }
+    // the measured tile schedule (tile_schedule): identity order until measured
+    const bool tsched = tile_sched_enabled() && !s->has_ext && (s->has_secondary || s->has_mesh);
+    int64_t tiles = 0;
+    if (tsched) {
+        const int64_t wpb = kBlock<false> / 64;
+        tiles = (int64_t)((c->ncols + 7) / 8) * ((c->height + 7) / 8);
+        const int64_t nw = (tiles + wpb - 1) / wpb * wpb;
+        std::vector<int32_t> ident((size_t)nw);
+        std::iota(ident.begin(), ident.end(), 0);
+        o_tperm = st.put(ident);
+        o_ttime = st.put(std::vector<uint32_t>((size_t)nw, 0u));
+    }
+    const size_t o_kp = st.put(nullptr, sizeof(KParams));
+    // one device buffer for all of it, reused while large enough; its old contents may still
+    // be read by frames of the previous camera
+    (void)hipDeviceSynchronize();
+    if (s->cam_cap < st.b.size()) {
+        (void)hipFree(s->d_cam);
+        s->d_cam = nullptr;
+        s->cam_cap = 0;
+        const size_t cap = st.b.size() + st.b.size() / 4;
+        RTX_HIP(hipMalloc((void**)&s->d_cam, cap));
+        s->cam_cap = cap;
+    }
+    char* const D = s->d_cam;
+    k.xs = (cptr<float>)(D + o_xs);
+    k.ys = (cptr<float>)(D + o_ys);
+    k.dof_o = (cptr<float>)(D + o_dof);
+    k.aa_o = (cptr<float>)(D + o_aa);
+    k.times = (cptr<float>)(D + o_times);
+    k.noise = replay ? (cptr<float>)(D + o_noise) : nullptr;
+    if (!s->h_nodes.empty()) bind_boxes(k.S, (const DBox*)(D + o_bounds), s->h_nodes.size());
+    if (pself) k.S.plane_self = (cptr<float>)(D + o_pself);
+    if (s->tr_grids_on) {
+        k.S.dsgrid = (cptr<DSGrid>)(D + o_dsg);
+        k.S.dsg_cells = (cptr<DSCell>)s->d_dsg_cells;
+        k.S.dsg_on = 1;
+    }
+    if (bins) {
+        k.S.bin_objmask = (cptr<uint32_t>)(D + o_bmask);
+        k.S.bin_rootmask = (cptr<uint32_t>)(D + o_bmask) + brmask.size();
+        k.S.mesh_bins = mesh_bins;
+        k.S.bin_start = (cptr<int32_t>)(D + o_bstart);
+        k.S.bin_faces = (cptr<int32_t>)(D + o_bfaces);
+        k.S.bin_zmin = (cptr<float>)(D + o_bz);
+        k.S.bins_x = bins_x;
+        k.S.bins_on = 1;
+    }
+#if defined(RTX_WAVE_LOG)  // tools/wave_timeline.py builds only
+    if (const char* e = getenv("RTX_WAVE_LOG_PTR"))
         k.wave_log = reinterpret_cast<unsigned long long*>((uintptr_t)strtoull(e, nullptr, 0));
+#endif
     // one sample, no jitter, static scene: every primary ray starts at aa_o[0], so its
     // origin-only plane and sphere terms are per-frame constants (closest_hit's fp32
     // operations, here once; RTX_PRIM_ORIGIN kernels read them)
@@ -2313,23 +2359,17 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
         }
         k.po_valid = 1;
     }
-    if (tile_sched_enabled() && !s->has_ext && (s->has_secondary || s->has_mesh)) {
-        // the measured tile schedule (tile_schedule): identity order until measured
-        const int64_t wpb = kBlock<false> / 64;
-        const int64_t nt = (int64_t)((c->ncols + 7) / 8) * ((c->height + 7) / 8);
-        const int64_t nw = (nt + wpb - 1) / wpb * wpb;
-        std::vector<int32_t> ident((size_t)nw);
-        std::iota(ident.begin(), ident.end(), 0);
-        if ((rc = upload(&s->d_tile_perm, ident)) ||
-            (rc = upload(&s->d_tile_time, std::vector<uint32_t>((size_t)nw, 0u))))
-            return rc;
-        k.tile_perm = (cptr<int32_t>)s->d_tile_perm;
-        k.tile_time = reinterpret_cast<unsigned int*>(s->d_tile_time);
-        k.tile_n = (int32_t)nt;
+    if (tsched) {
+        k.tile_perm = (cptr<int32_t>)(D + o_tperm);
+        k.tile_time = reinterpret_cast<unsigned int*>(D + o_ttime);
+        k.tile_n = (int32_t)tiles;
+        s->d_tile_perm = D + o_tperm;
+        s->d_tile_time = D + o_ttime;
         s->tile_sched = 1;
     }
-    RTX_HIP(hipMalloc((void**)&s->d_kp, sizeof(KParams)));
-    RTX_HIP(hipMemcpy(s->d_kp, &k, sizeof(KParams), hipMemcpyHostToDevice));
+    memcpy(st.b.data() + o_kp, &k, sizeof(KParams));
+    RTX_HIP(hipMemcpy(D, st.b.data(), st.b.size(), hipMemcpyHostToDevice));
+    s->d_kp = reinterpret_cast<KParams*>(D + o_kp);
     s->kp = k;
     s->cam_set = true;
     return RTX_OK;

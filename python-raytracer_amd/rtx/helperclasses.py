@@ -203,17 +203,61 @@ class ViewportCamera:
         return self
 
 
+_SUNFLOWER_TERMS = {}
+
+
+def _sunflower_terms(num_points):
+    """Per point k: sqrt(k - 0.5), cos(theta_k), sin(theta_k) with theta_k = k * angle_stride,
+    each computed as the reference computes it (numpy fp64 scalar calls); they do not
+    depend on the origin or radius, so they are kept per num_points."""
+    t = _SUNFLOWER_TERMS.get(num_points)
+    if t is None:
+        phi = (1 + np.sqrt(5)) / 2
+        angle_stride = 2 * np.pi / phi
+        sq = np.empty(num_points, np.float64)
+        co = np.empty(num_points, np.float64)
+        si = np.empty(num_points, np.float64)
+        for k in range(1, num_points + 1):
+            theta = k * angle_stride
+            sq[k - 1] = np.sqrt(k - 0.5)
+            co[k - 1] = np.cos(theta)
+            si[k - 1] = np.sin(theta)
+        t = (sq, co, si, np.sqrt(num_points - 0.5))
+        if len(_SUNFLOWER_TERMS) < 64:
+            _SUNFLOWER_TERMS[num_points] = t
+    return t
+
+
 def sunflower(num_points, origin, radius):
-    """Scene._sunflower_spread (scene.py:118-138), evaluated with numpy fp64 scalars as
-    the reference does; points are PyGLM vec3 (float32)."""
-    phi = (1 + np.sqrt(5)) / 2
-    angle_stride = 2 * np.pi / phi
+    """Scene._sunflower_spread (scene.py:118-138), evaluated with numpy fp64 as the
+    reference does -- r = radius * sqrt(k - 0.5) / sqrt(n - 0.5), (r cos(theta) + ox,
+    r sin(theta) + oy, oz) -- each element with the reference's operations in its order;
+    points are PyGLM vec3 (float32)."""
     out = np.zeros((num_points, 3), dtype=np.float32)
+    if num_points <= 0:
+        return out
+    sq, co, si, sn = _sunflower_terms(num_points)
     ox, oy, oz = float(origin[0]), float(origin[1]), origin[2]
-    for k in range(1, num_points + 1):
-        r = radius * np.sqrt(k - 0.5) / np.sqrt(num_points - 0.5)
-        theta = k * angle_stride
-        x = r * np.cos(theta) + ox
-        y = r * np.sin(theta) + oy
-        out[k - 1] = np.array([x, y, oz], dtype=np.float64).astype(np.float32)
+    r = radius * sq / sn
+    out[:, 0] = (r * co + ox).astype(np.float32)
+    out[:, 1] = (r * si + oy).astype(np.float32)
+    out[:, 2] = np.float32(np.float64(oz))
+    return out
+
+
+def sunflower_many(num_points, origins, radius):
+    """sunflower(num_points, o, radius) for every row o of origins (float32 [m, 3]) at once:
+    [m, num_points, 3], the same values (the per-element operations are sunflower's)."""
+    origins = np.asarray(origins)
+    m = len(origins)
+    out = np.zeros((m, num_points, 3), dtype=np.float32)
+    if num_points <= 0 or m == 0:
+        return out
+    sq, co, si, sn = _sunflower_terms(num_points)
+    r = radius * sq / sn
+    ox = origins[:, 0].astype(np.float64)[:, None]
+    oy = origins[:, 1].astype(np.float64)[:, None]
+    out[:, :, 0] = (r * co + ox).astype(np.float32)
+    out[:, :, 1] = (r * si + oy).astype(np.float32)
+    out[:, :, 2] = origins[:, 2].astype(np.float64).astype(np.float32)[:, None]
     return out

@@ -18,13 +18,23 @@ import torch
 from . import _native as N
 from . import f32 as F
 from . import records
-from .helperclasses import sunflower
+from .helperclasses import sunflower, sunflower_many
 
 DEFAULT_SEED = 0x5EED
 
 
 def _ptr(a, ctype):
     return a.ctypes.data_as(C.POINTER(ctype))
+
+
+def running_sum(x0, dx, n):
+    """[x0, x0 + dx, (x0 + dx) + dx, ...] (n values) in fp64, each step one rounded add --
+    the reference's `x += dx` loop (scene.py:39-45); ufunc accumulate adds in order."""
+    if n <= 0:
+        return np.empty(0, np.float64)
+    steps = np.full(n, dx, np.float64)
+    steps[0] = x0
+    return np.add.accumulate(steps)
 
 
 def strip_columns(width, subimage, tasks):
@@ -153,18 +163,12 @@ class Scene:
         col0, ncols = strip_columns(vc.width, subimage, tasks)
         dx = (vc.right - vc.left) / vc.width
         dy = (vc.top - vc.bottom) / vc.height
-        xs = np.empty(ncols, np.float64)
-        x = vc.left + (0.5 + np.int64(col0)) * dx
-        for i in range(ncols):
-            xs[i] = x
-            x += dx
-        ys = np.empty(vc.height, np.float64)
-        y = vc.bottom + 0.5 * dy
-        for j in range(vc.height):
-            ys[j] = y
-            y += dy
+        # the running sums x += dx, y += dy (scene.py:39-45), in order: add.accumulate
+        # adds left to right in fp64, one rounding per step, as the reference's loop does
+        xs = running_sum(vc.left + (0.5 + np.int64(col0)) * dx, dx, ncols)
+        ys = running_sum(vc.bottom + 0.5 * dy, dy, vc.height)
         dof = sunflower(vc.dof_samples, vc.position, vc.aperture)
-        aa = np.stack([sunflower(self.samples, dof[k], 2 * (dx + dy)) for k in range(vc.dof_samples)])
+        aa = sunflower_many(self.samples, dof, 2 * (dx + dy))
         return dict(col0=col0, ncols=ncols, xs=xs.astype(np.float32), ys=ys.astype(np.float32),
                     dof=np.ascontiguousarray(dof), aa=np.ascontiguousarray(aa),
                     times=np.asarray(vc.motion_times, np.float64), jscale=0.1 * (dx + dy))

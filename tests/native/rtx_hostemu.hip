@@ -14,6 +14,7 @@ hipError_t launch_split_m1(int, int, const RenderLaunch&, const Launch&, const S
 }  // namespace rtx
 
 #include <omp.h>
+#include <chrono>
 
 namespace {
 void bind_view(const HostScene& H, SceneView& v) {
@@ -86,7 +87,8 @@ struct DirGrids {
         if (e && e[0] == '0') return;
         std::vector<DBound> nb;
         if (!H.nodes.empty()) nb = compute_bounds(H.nodes, H.objs, H.tris, tlo, thi);
-        if (!dir_shadow_grids(H, nb, tlo, thi, omax, grids, cells)) return;
+        if (!dir_shadow_grids(H, nb, tlo, thi, grids, cells)) return;
+        dir_self_boxes(H, grids, omax);
         v.dsgrid = (cptr<DSGrid>)grids.data();
         v.dsg_cells = (cptr<DSCell>)cells.data();
         v.dsg_on = 1;
@@ -695,4 +697,45 @@ extern "C" int64_t rtx_hostemu_bins(const rtx_scene_desc* sd, const rtx_camera_d
         if (rmask) rmask[b] = brmask[b];
     }
     return n;
+}
+
+// Host cost of rtx_camera_set's steps (ms, best of `reps`): [0] hierarchy bounds, [1] the
+// directional lights' shadow grids, [2] their self-test marks, [3] plane self limits,
+// [4] primary-ray bins. (tools: the per-camera setup budget.)
+extern "C" int rtx_hostemu_camera_cost(const rtx_scene_desc* sd, const rtx_camera_desc* cd, int reps, double* ms) {
+    HostScene H;
+    if (int rc = convert_scene(sd, H)) return rc;
+    std::vector<float> tms(cd->n_times);
+    for (int i = 0; i < cd->n_times; ++i) tms[i] = (float)cd->times[i];
+    const auto tmm = std::minmax_element(tms.begin(), tms.end());
+    const double omax = camera_origin_bound(cd);
+    for (int q = 0; q < 5; ++q) ms[q] = INFINITY;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto dt = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    for (int r = 0; r < reps; ++r) {
+        auto t0 = now();
+        std::vector<DBound> nodeb;
+        if (!H.nodes.empty()) nodeb = compute_bounds(H.nodes, H.objs, H.tris, *tmm.first, *tmm.second);
+        auto t1 = now();
+        std::vector<DSGrid> grids;
+        std::vector<DSCell> cells;
+        dir_shadow_grids(H, nodeb, *tmm.first, *tmm.second, grids, cells);
+        auto t2 = now();
+        dir_self_boxes(H, grids, omax);
+        auto t3 = now();
+        std::vector<float> lim = plane_self_limits(H, omax);
+        auto t4 = now();
+        std::vector<int32_t> bstart, bfaces;
+        std::vector<float> bz;
+        std::vector<uint32_t> bmask, brmask;
+        int32_t bins_x = 0, mesh_bins = 0;
+        primary_bins(H, cd, nodeb, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins);
+        auto t5 = now();
+        ms[0] = std::min(ms[0], dt(t0, t1));
+        ms[1] = std::min(ms[1], dt(t1, t2));
+        ms[2] = std::min(ms[2], dt(t2, t3));
+        ms[3] = std::min(ms[3], dt(t3, t4));
+        ms[4] = std::min(ms[4], dt(t4, t5));
+    }
+    return RTX_OK;
 }
