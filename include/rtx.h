@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define RTX_ABI_VERSION 4
+#define RTX_ABI_VERSION 5
 
 typedef enum rtx_status {
     RTX_OK = 0,
@@ -242,9 +242,22 @@ const char* rtx_last_kernel(const rtx_scene* scene);
 
 /* Observability (no reference counterpart): the number of scene-specialized kernel
  * modules loaded in this process. Kernels whose source carries one scene's record values
- * are unloaded once no scene holds them and more than $RTX_JIT_IDLE_BAKED (default 8)
+ * are unloaded once no scene holds them and more than jit_idle_baked (option, default 8)
  * such idle modules exist, so the count stays bounded as scenes come and go. */
 int32_t rtx_jit_modules(void);
+
+/* Library options (no reference counterpart; INTEGRATION.md "Options"): process-wide
+ * switches of the culling structures, the split hierarchy passes, the scene-specialized
+ * kernels and their caches, by name ("split", "bins", "jit", ...). Each starts from
+ * $RTX_<NAME> when that is set in the environment, else from its default; set them before
+ * rendering (they are read per render / per camera upload, not synchronised with renders
+ * on other threads). Values are text: a number, or a string for "jit_cache" / "jit_flags".
+ * RTX_ERR_INVALID for an unknown name or a malformed number. */
+int rtx_set_option(const char* name, const char* value);
+/* The option's current value as text into value[cap] (RTX_ERR_INVALID if it does not fit). */
+int rtx_get_option(const char* name, char* value, int32_t cap);
+/* Name of option i (0, 1, ...; NULL past the last). */
+const char* rtx_option_name(int32_t i);
 
 #ifdef __cplusplus
 }

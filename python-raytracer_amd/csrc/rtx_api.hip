@@ -62,6 +62,72 @@ int fail(int code, const std::string& msg) {
             return fail(RTX_ERR_HIP, std::string(#call ": ") + hipGetErrorString(e_));    \
     } while (0)
 
+// ------------------------------------------------------------------ library options
+// Process-wide switches of librtx.so (rtx_set_option / rtx_get_option; INTEGRATION.md
+// "Options"): each starts from $RTX_<NAME> when that is set, else from its default, and is
+// read where the library decides (per render or per camera upload). Set them before
+// rendering; they are not synchronised with renders running on other threads.
+enum Opt {
+    OPT_SPLIT, OPT_SPLIT_BYTES, OPT_SPLIT_RATIO, OPT_BINS, OPT_LENS_BINS, OPT_LGRID, OPT_DSGRID, OPT_DSGRID_MIN,
+    OPT_SELF_SKIP, OPT_TILE_SCHED, OPT_PRIM_ORIGIN, OPT_SPP, OPT_SPP_MIN, OPT_JIT, OPT_JIT_BAKE, OPT_JIT_EXT,
+    OPT_JIT_DUMP, OPT_JIT_IDLE_BAKED, OPT_JIT_DISK_BAKED, OPT_JIT_CACHE, OPT_JIT_FLAGS, OPT_COUNT
+};
+struct OptDef {
+    const char* name;
+    double dflt;
+    bool str;  // a string value (kept in OptVal::s)
+};
+constexpr OptDef kOpts[OPT_COUNT] = {
+    {"split", 1, false},                      // hierarchy/texture scenes in three passes (0: one kernel)
+    {"split_bytes", 2147483648.0, false},     // record bytes of one split chunk
+    {"split_ratio", -1, false},               // >= 0: fixed deeper records per sample (else learned)
+    {"bins", 1, false},                       // primary-ray bins (0: every primary ray walks everything)
+    {"lens_bins", 1, false},                  // bins for lens cameras too
+    {"lgrid", 1, false},                      // light grids of point lights (mesh shadow rays)
+    {"dsgrid", 1, false},                     // shadow grids of directional lights
+    {"dsgrid_min", 8, false},                 // the fewest spheres (and nothing else) that get one
+    {"self_skip", 1, false},                  // plane / box self tests skipped where provably passing
+    {"tile_sched", 1, false},                 // measured longest-first tile order
+    {"prim_origin", 1, false},                // host-computed origin terms of pinhole primary rays
+    {"spp", -1, false},                       // sample-parallel mapping: -1 auto, 0 never, 1 always
+    {"spp_min", 16, false},                   // auto: from this many samples per pixel (X scenes)
+    {"jit", 1, false},                        // scene-specialized kernels (hiprtc)
+    {"jit_bake", 1, false},                   // scene records as literals in one-sample kernels
+    {"jit_ext", 0, false},                    // specialize hierarchy/texture kernels too
+    {"jit_dump", 0, false},                   // print each specialized kernel's source and options
+    {"jit_idle_baked", 8, false},             // idle baked kernel modules kept loaded
+    {"jit_disk_baked", 64, false},            // baked code objects kept in the disk cache
+    {"jit_cache", 0, true},                   // code-object cache directory ("" = /tmp/rtx_jit_<uid>)
+    {"jit_flags", 0, true},                   // extra hiprtc options (part of the cache key)
+};
+struct OptVal {
+    double v;
+    std::string s;
+};
+std::mutex g_opt_mu;
+OptVal* opt_table() {
+    static OptVal* t = [] {
+        static OptVal vals[OPT_COUNT];
+        for (int i = 0; i < OPT_COUNT; ++i) {
+            vals[i].v = kOpts[i].dflt;
+            std::string env = "RTX_";
+            for (const char* c = kOpts[i].name; *c; ++c) env += (char)toupper((unsigned char)*c);
+            if (const char* e = getenv(env.c_str())) {
+                if (kOpts[i].str) vals[i].s = e;
+                else if (*e) vals[i].v = atof(e);
+            }
+        }
+        return vals;
+    }();
+    return t;
+}
+double opt(Opt o) { return opt_table()[o].v; }
+bool opt_on(Opt o) { return opt_table()[o].v != 0.0; }
+std::string opt_str(Opt o) {
+    std::lock_guard<std::mutex> lock(g_opt_mu);
+    return opt_table()[o].s;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ host-side conversion
@@ -833,8 +899,7 @@ std::vector<float> plane_self_limits(const HostScene& H, double omax) {
 
 // $RTX_LENS_BINS=0: lens cameras get no primary-ray bins (experiment, A/B)
 bool lens_bins_disabled() {
-    const char* e = getenv("RTX_LENS_BINS");
-    return e && e[0] == '0';
+    return !opt_on(OPT_LENS_BINS);
 }
 
 // Primary-ray bins. With one sample per pixel, no lens (dof origin == camera position)
@@ -1219,7 +1284,6 @@ bool light_grids(const HostScene& H, std::vector<DLGrid>& grids, std::vector<int
         // (G 10 -> 64: 82.5 -> 69.3 us) and the 81,920-face mesh (G 200 -> 400)
         std::nth_element(ext.begin(), ext.begin() + F / 2, ext.end());
         int32_t G = (int32_t)std::min(512.0, std::max(64.0, std::ceil(4.0 * (2.0 * T) / std::max(ext[F / 2], 1e-12))));
-        if (const char* eg = getenv("RTX_LGRID_G"); eg && atoi(eg) > 0) G = std::min(1024, atoi(eg));  // tuning
         DLGrid g{};
         for (int a = 0; a < 3; ++a) { g.L[a] = Lt.vec[a]; g.a[a] = af[a]; g.u[a] = uf[a]; g.v[a] = vf[a]; }
         g.G = G;
@@ -1389,15 +1453,13 @@ bool dir_shadow_grids(const HostScene& H, const std::vector<DBound>& nb, double 
     // A few spheres alone are cheaper to test than the cell lookup (its dependent load):
     // MirrorRefraction, four spheres, measured 1 % slower with a grid (profiles/r04/root_bins/)
     {
-        const char* ef = getenv("RTX_DSGRID_MIN");  // experiment: the fewest static spheres that get one (8)
         const bool spheres_only = std::all_of(obs.begin(), obs.end(), [](const Ob& o) { return o.r >= 0.0; });
-        if (spheres_only && (int32_t)obs.size() < (ef ? atoi(ef) : 8)) return false;
+        if (spheres_only && (double)obs.size() < opt(OPT_DSGRID_MIN)) return false;
     }
     // 512 x 512 cells (2 MB per light): finer grids measured faster up to 512 (DepthOfField
     // 4K 5.09 -> 5.01 ms, NovelScene1 17.48 -> 16.96 ms, NovelScene2 79.2 -> 76.7 ms from 64;
     // 1024 within 0.5 %, profiles/r04/dsgrid_g/)
-    int32_t G = 512;
-    if (const char* eg = getenv("RTX_DSGRID_G"); eg && atoi(eg) > 0) G = std::min(1024, atoi(eg));  // tuning
+    const int32_t G = 512;
     const double pmax = 1.25 * R + 1.0, pm = std::sqrt(3.0) * pmax;  // pm >= |p| of a gridded origin
     bool any = false;
     for (size_t li = 0; li < H.lights.size(); ++li) {
@@ -1494,11 +1556,10 @@ bool dir_shadow_grids(const HostScene& H, const std::vector<DBound>& nb, double 
 // depend on omax (camera_origin_bound); the grids and their cells depend on the frame's
 // time range only.
 void dir_self_boxes(const HostScene& H, std::vector<DSGrid>& grids, double omax) {
-    const char* es = getenv("RTX_SELF_SKIP");  // 0 = every box tests itself
     for (size_t li = 0; li < grids.size() && li < H.lights.size(); ++li) {
         DSGrid& g = grids[li];
         g.self_boxes = 0u;
-        if (g.G == 0 || H.n_box > 16 || !std::isfinite(omax) || (es && es[0] == '0')) continue;
+        if (g.G == 0 || H.n_box > 16 || !std::isfinite(omax) || !opt_on(OPT_SELF_SKIP)) continue;
         const DLight& Lt = H.lights[li];
         double dmin = INFINITY;
         for (int q = 0; q < 3; ++q)
@@ -1564,13 +1625,8 @@ std::map<std::string, JitEntry> g_jit;
 // kJitIdleBaked idle modules the oldest is unloaded (its scenes' buffers were freed with
 // hipFree, which waits for their kernels). The disk cache keeps at most kJitDiskBaked
 // baked code objects (rtx_b_*.co, oldest removed first).
-// ($RTX_JIT_IDLE_BAKED / $RTX_JIT_DISK_BAKED override the caps; the tests lower them.)
-size_t jit_cap(const char* env, size_t dflt) {
-    const char* e = getenv(env);
-    return (e && *e) ? (size_t)std::max(0, atoi(e)) : dflt;
-}
-constexpr size_t kJitIdleBaked = 8;
-constexpr size_t kJitDiskBaked = 64;
+// (options jit_idle_baked / jit_disk_baked set the caps, 8 and 64; the tests lower them.)
+size_t jit_cap(Opt o) { return (size_t)std::max(0.0, opt(o)); }
 std::list<std::string> g_jit_idle;  // baked keys with refs == 0, oldest first
 
 // A scene drops its hold on a resolved kernel (camera change or rtx_scene_destroy).
@@ -1580,7 +1636,7 @@ void jit_release(const std::string& key) {
     auto it = g_jit.find(key);
     if (it == g_jit.end() || --it->second.refs > 0 || !it->second.baked) return;
     g_jit_idle.push_back(key);
-    const size_t cap = jit_cap("RTX_JIT_IDLE_BAKED", kJitIdleBaked);
+    const size_t cap = jit_cap(OPT_JIT_IDLE_BAKED);
     while (g_jit_idle.size() > cap) {
         auto old = g_jit.find(g_jit_idle.front());
         g_jit_idle.pop_front();
@@ -1603,61 +1659,43 @@ void jit_prune_disk(const std::string& dir) {
         if (lstat(path.c_str(), &st) == 0 && S_ISREG(st.st_mode)) files.emplace_back(st.st_mtime, path);
     }
     closedir(d);
-    const size_t cap = jit_cap("RTX_JIT_DISK_BAKED", kJitDiskBaked);
+    const size_t cap = jit_cap(OPT_JIT_DISK_BAKED);
     if (files.size() <= cap) return;
     std::sort(files.begin(), files.end());
     for (size_t i = 0; i + cap < files.size(); ++i) (void)unlink(files[i].second.c_str());
 }
 
 // Sample-parallel mapping (render_body_spp) for the hierarchy/texture kernels when a
-// pixel has >= RTX_SPP_MIN samples (default 16): a wave then traces one pixel's nearly
+// pixel has >= spp_min samples (option, default 16): a wave then traces one pixel's nearly
 // identical AA/time samples, so the wave-uniform subtree culling stays effective
 // (NovelScene1 108 -> 30 ms, NovelScene2 741 -> 161 ms). The flat-scene kernels keep
 // the 8x8-tile mapping, whose waves are already coherent (same lens sample across a
-// tile; DepthOfField 4K: 11.1 ms tiles vs 19.3 ms sample-parallel). RTX_SPP=0 never
-// uses it, RTX_SPP=1 always (tests compare both mappings).
+// tile; DepthOfField 4K: 11.1 ms tiles vs 19.3 ms sample-parallel). Option spp: 0 never
+// uses it, 1 always (tests compare both mappings).
 bool use_spp_mode(int spp, bool ext) {
     if (spp < 1 || spp >= (1 << 20)) return false;  // udiv_small's range
-    const char* e = getenv("RTX_SPP");
-    if (e && e[0] == '0') return false;
-    if (e && e[0] == '1') return true;
-    const char* m = getenv("RTX_SPP_MIN");
-    const int lo = (m && *m) ? atoi(m) : 16;
-    return ext && spp >= lo;
+    const double m = opt(OPT_SPP);
+    if (m == 0.0) return false;
+    if (m == 1.0) return true;
+    return ext && spp >= opt(OPT_SPP_MIN);
 }
 
-// Persistent-wave experiment (rtx_kernels.h RTX_PERSIST): $RTX_PERSIST = resident waves
-// per SIMD the grid is sized for (0 or unset: off).
-int persist_waves() {
-    const char* e = getenv("RTX_PERSIST");
-    return (e && *e) ? std::max(0, atoi(e)) : 0;
-}
+// Host-computed origin terms of primary rays (RTX_PRIM_ORIGIN kernels; option prim_origin).
+bool prim_origin_enabled() { return opt_on(OPT_PRIM_ORIGIN); }
 
-// Host-computed origin terms of primary rays (RTX_PRIM_ORIGIN); $RTX_PRIM_ORIGIN=0: off.
-bool prim_origin_enabled() {
-    const char* e = getenv("RTX_PRIM_ORIGIN");
-    return !(e && e[0] == '0');
-}
+// The measured tile schedule (tile_schedule; option tile_sched).
+bool tile_sched_enabled() { return opt_on(OPT_TILE_SCHED); }
 
-// The measured tile schedule (tile_schedule); $RTX_TILE_SCHED=0: off.
-bool tile_sched_enabled() {
-    const char* e = getenv("RTX_TILE_SCHED");
-    return !(e && e[0] == '0');
-}
+bool jit_enabled() { return opt_on(OPT_JIT); }
 
-bool jit_enabled() {
-    const char* e = getenv("RTX_JIT");
-    return !(e && e[0] == '0');
-}
-
-// The on-disk code-object cache: $RTX_JIT_CACHE or /tmp/rtx_jit_<uid>, created with
+// The on-disk code-object cache: option jit_cache or /tmp/rtx_jit_<uid>, created with
 // mkdir(2) mode 0700. It is used only when it is a real directory (not a symlink) owned
 // by this user and not writable by group or others; otherwise another local user could
 // plant code objects under the predictable names, so kernels are compiled uncached.
 // Returns "" when the cache must not be used.
 std::string jit_cache_dir() {
-    const char* e = getenv("RTX_JIT_CACHE");
-    const std::string dir = (e && *e) ? std::string(e) : "/tmp/rtx_jit_" + std::to_string((long)getuid());
+    const std::string e = opt_str(OPT_JIT_CACHE);
+    const std::string dir = !e.empty() ? e : "/tmp/rtx_jit_" + std::to_string((long)getuid());
     (void)mkdir(dir.c_str(), 0700);
     struct stat st;
     if (lstat(dir.c_str(), &st) != 0 || !S_ISDIR(st.st_mode) || st.st_uid != getuid() ||
@@ -1679,6 +1717,9 @@ const char* const kLibMacros[] = {
     "-DRTX_LB_XWAVES=" RTX_STR(RTX_LB_XWAVES),
     "-DRTX_LB_WAVES(MESH,SEC)=" RTX_STR(RTX_LB_WAVES(MESH, SEC)),
     "-DRTX_ABLATE=" RTX_STR(RTX_ABLATE),
+#if defined(RTX_TOOLS_BUILD)
+    "-DRTX_TOOLS_BUILD",
+#endif
     "-DRTX_HIER_INLINE=" RTX_STR(RTX_HIER_INLINE),
 #ifdef RTX_PAD
     "-DRTX_PAD=" RTX_STR(RTX_PAD),
@@ -1736,10 +1777,7 @@ std::string jit_baked_records(const std::vector<DObj>& objs, const std::vector<D
     return s + "}\n#define RTX_BAKED_RECORDS 1\n";
 }
 
-bool jit_bake_enabled() {
-    const char* e = getenv("RTX_JIT_BAKE");
-    return !(e && e[0] == '0');
-}
+bool jit_bake_enabled() { return opt_on(OPT_JIT_BAKE); }
 
 // What a scene-specialized kernel is built from: its name, hiprtc source and options.
 struct JitSpec {
@@ -1760,10 +1798,7 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
     if (v.n_plane + v.n_sphere + v.n_box + v.n_mesh > 32 || v.n_lights > 8) return false;  // code size
     // CSG/texture kernels: the unrolled loops raise their (already high) register
     // pressure and the specialized kernel measured slower (NovelScene1 105 -> 134 ms)
-    if (ext) {
-        const char* e = getenv("RTX_JIT_EXT");  // experiment: specialize them anyway
-        if (!(e && e[0] == '1')) return false;
-    }
+    if (ext && !opt_on(OPT_JIT_EXT)) return false;  // (option jit_ext: specialize them anyway)
     std::vector<std::string> opts = {"--offload-arch=" + arch, "-O3", "-std=c++17", "-ffp-contract=off",
                                      "-DRTX_FIXED_COUNTS",
                                      "-DRTX_FIXED_NP=" + std::to_string(v.n_plane),
@@ -1784,14 +1819,9 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
                                      "-DRTX_FIXED_DIVPOW2=" + std::to_string(kp.div_pow2),
                                      "-DRTX_FIXED_JMODE=" + std::to_string(kp.jitter)};
     // the strip width too: the tile index arithmetic becomes multiplications by constants
-    // (TSP 1080p 27.85 -> 27.37 us, profiles/r03/ncols/; one compile per strip width).
-    // RTX_JIT_NCOLS=0 leaves it a run-time value.
-    {
-        const char* e = getenv("RTX_JIT_NCOLS");
-        if (!spp && !(e && e[0] == '0')) opts.push_back("-DRTX_FIXED_NCOLS=" + std::to_string(kp.ncols));
-    }
+    // (TSP 1080p 27.85 -> 27.37 us, profiles/r03/ncols/; one compile per strip width)
+    if (!spp) opts.push_back("-DRTX_FIXED_NCOLS=" + std::to_string(kp.ncols));
     if (uniform_hard >= 0) opts.push_back("-DRTX_FIXED_HARD=" + std::to_string(uniform_hard));
-    if (!spp && persist_waves() > 0) opts.push_back("-DRTX_PERSIST=1");
     if (!spp && !ext && kp.tile_time != nullptr) opts.push_back("-DRTX_TILE_SCHED=1");
     if (!spp && !ext && kp.po_valid) opts.push_back("-DRTX_PRIM_ORIGIN=1");
     if (out8) opts.push_back("-DRTX_OUT8=1");  // uint8 framebuffer (rtx_render_rgb8)
@@ -1800,25 +1830,9 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
     opts.push_back(std::string("-DRTX_PRIMARY_BINS=") + (kp.S.bins_on ? "1" : "0"));
     opts.push_back(std::string("-DRTX_LIGHT_GRIDS=") + (v.lgrid_on ? "1" : "0"));
     opts.push_back(std::string("-DRTX_DIR_GRIDS=") + (kp.S.dsg_on ? "1" : "0"));
-    if (!ext && !spp) {  // experiment: per-lane object / material gathers from LDS (RTX_LDS_RECORDS=1)
-        const char* e = getenv("RTX_LDS_RECORDS");
-        const size_t bytes = (size_t)v.n_objs_all * sizeof(DObj) + (size_t)v.n_mats * sizeof(DMat);
-        if (e && e[0] == '1' && v.n_objs_all > 0 && v.n_mats > 0 && bytes <= 16 * 1024) {
-            opts.push_back("-DRTX_LDS_OBJS=" + std::to_string(v.n_objs_all));
-            opts.push_back("-DRTX_LDS_MATS=" + std::to_string(v.n_mats));
-        }
-    }
-    if (mesh && !spp && v.n_mesh > 0) {  // experiment: the meshes' hot records in LDS (RTX_MESH_LDS=1)
-        const char* e = getenv("RTX_MESH_LDS");
-        const size_t bytes = (size_t)v.n_tris * (sizeof(DTri) + sizeof(DFaceBox)) + (size_t)v.n_leaves * sizeof(DLeaf);
-        if (e && e[0] == '1' && bytes <= 48 * 1024) {
-            opts.push_back("-DRTX_LDS_TRIS=" + std::to_string(v.n_tris));
-            opts.push_back("-DRTX_LDS_LEAVES=" + std::to_string(v.n_leaves));
-        }
-    }
-    const char* lm = getenv("RTX_JIT_LIBMACROS");  // experiment: 0 = do not forward them
-    if (!(lm && lm[0] == '0'))
-        for (const char* m : kLibMacros) opts.push_back(m);
+    // (records and mesh data staged in LDS -- RTX_LDS_OBJS / RTX_LDS_TRIS kernels -- measured
+    // slower; jit_flags can still request them)
+    for (const char* m : kLibMacros) opts.push_back(m);
     if (!sec && !ext && (!mesh || fc_mode == 1)) {
         // flat scenes and small meshes (every face box-culled): 6 waves/SIMD. With the
         // host-side box precomputes the DepthOfField kernel fits 80 VGPRs with no more
@@ -1829,8 +1843,8 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
         opts.push_back("-URTX_LB_WAVES");
         opts.push_back("-DRTX_LB_WAVES(MESH,SEC)=6");
     }
-    if (const char* extra = getenv("RTX_JIT_FLAGS")) {  // experiments (tools/ablate.sh); part of the cache key
-        std::istringstream is(extra);
+    {  // option jit_flags (tools: cost probes, occupancy bounds); part of the cache key
+        std::istringstream is(opt_str(OPT_JIT_FLAGS));
         for (std::string o; is >> o;) opts.push_back(o);
     }
     auto b = [](bool x) { return x ? "true" : "false"; };
@@ -1851,7 +1865,13 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
     // (The frame parameters stay behind a pointer: passed by value in the kernel arguments,
     // one dependent scalar load fewer per wave, they measured equal on TSP/MR/TM,
     // profiles/r04/kp_byval/.)
-    const std::string src = prelude + std::string("#include \"rtx_kernels.h\"\nextern \"C\" __global__ RTX_RENDER_BOUNDS(") +
+    // (a product library's kernels are never cost-probe builds, whatever jit_flags say)
+#if defined(RTX_TOOLS_BUILD)
+    const std::string tools_guard;
+#else
+    const std::string tools_guard = "#undef RTX_TOOLS_BUILD\n";
+#endif
+    const std::string src = tools_guard + prelude + std::string("#include \"rtx_kernels.h\"\nextern \"C\" __global__ RTX_RENDER_BOUNDS(") +
                             b(mesh) + ", " + b(sec) + ", " + b(ext) + ") void " + name + "(const rtx::KParams* "
                             "__restrict__ P, const rtx::Launch L) {\n  rtx::" + (spp ? "render_body_spp<" : "render_body<") +
                             b(mesh) + ", " + b(sec) +
@@ -1897,7 +1917,7 @@ hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& k
         std::ifstream f(path, std::ios::binary);
         if (f) { std::stringstream ss; ss << f.rdbuf(); code = ss.str(); }
     }
-    if (const char* dump = getenv("RTX_JIT_DUMP"); dump && dump[0] == '1') {  // tools/jit_resource.sh
+    if (opt_on(OPT_JIT_DUMP)) {  // tools/jit_resource.sh
         fprintf(stderr, "librtx: jit %s:", name.c_str());
         for (const auto& o : opts) fprintf(stderr, " '%s'", o.c_str());
         fprintf(stderr, "\n%s", src.c_str());
@@ -2107,6 +2127,47 @@ extern "C" {
 
 int rtx_abi_version(void) { return RTX_ABI_VERSION; }
 
+int rtx_set_option(const char* name, const char* value) {
+    if (!name || !value) return fail(RTX_ERR_INVALID, "rtx_set_option: null argument");
+    for (int i = 0; i < OPT_COUNT; ++i) {
+        if (strcmp(kOpts[i].name, name) != 0) continue;
+        std::lock_guard<std::mutex> lock(g_opt_mu);
+        OptVal& o = opt_table()[i];
+        if (kOpts[i].str) {
+            o.s = value;
+            return RTX_OK;
+        }
+        char* end = nullptr;
+        const double v = strtod(value, &end);
+        if (end == value || *end != '\0' || !std::isfinite(v))
+            return fail(RTX_ERR_INVALID, std::string("rtx_set_option: ") + name + " takes a number, got '" + value + "'");
+        o.v = v;
+        return RTX_OK;
+    }
+    return fail(RTX_ERR_INVALID, std::string("rtx_set_option: no option '") + name + "'");
+}
+
+int rtx_get_option(const char* name, char* value, int32_t cap) {
+    if (!name || !value || cap < 1) return fail(RTX_ERR_INVALID, "rtx_get_option: bad argument");
+    for (int i = 0; i < OPT_COUNT; ++i) {
+        if (strcmp(kOpts[i].name, name) != 0) continue;
+        std::string v;
+        if (kOpts[i].str) {
+            v = opt_str((Opt)i);
+        } else {
+            char buf[64];
+            snprintf(buf, sizeof(buf), "%.17g", opt((Opt)i));
+            v = buf;
+        }
+        if ((int64_t)v.size() >= cap) return fail(RTX_ERR_INVALID, "rtx_get_option: buffer too small");
+        memcpy(value, v.c_str(), v.size() + 1);
+        return RTX_OK;
+    }
+    return fail(RTX_ERR_INVALID, std::string("rtx_get_option: no option '") + name + "'");
+}
+
+const char* rtx_option_name(int32_t i) { return i >= 0 && i < OPT_COUNT ? kOpts[i].name : nullptr; }
+
 const char* rtx_last_error(void) { return g_last_error.c_str(); }
 
 const char* rtx_last_kernel(const rtx_scene* s) { return s ? s->last_kernel.c_str() : ""; }
@@ -2188,12 +2249,11 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
     v.n_tris = (int32_t)H.tris.size();
     v.n_leaves = (int32_t)H.leaves.size();
     v.hlevels = H.hlevels;
-    {  // light grids for the shadow rays of point lights (RTX_LGRID=0: walk the BVH)
+    {  // light grids for the shadow rays of point lights (option lgrid 0: walk the BVH)
         std::vector<DLGrid> grids;
         std::vector<int32_t> gstart, gfaces;
         std::vector<float> gd2;
-        const char* e = getenv("RTX_LGRID");
-        if (!(e && e[0] == '0') && light_grids(H, grids, gstart, gfaces, gd2)) {
+        if (opt_on(OPT_LGRID) && light_grids(H, grids, gstart, gfaces, gd2)) {
             if (gfaces.empty()) { gfaces.push_back(0); gd2.push_back(0.0f); }
             if ((rc = upload(&s->d_lgrid, grids)) || (rc = upload(&s->d_lg_start, gstart)) ||
                 (rc = upload(&s->d_lg_faces, gfaces)) || (rc = upload(&s->d_lg_d2, gd2))) {
@@ -2230,8 +2290,7 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     const double omax = camera_origin_bound(c);
     k.S = s->view;
     // what depends on the frame's time range only: computed again when it changes
-    const char* edsg = getenv("RTX_DSGRID");  // 0: every shadow ray tests every object
-    const bool dsg_off = edsg && edsg[0] == '0';
+    const bool dsg_off = !opt_on(OPT_DSGRID);  // every shadow ray tests every object
     if (!s->tr_valid || s->tr_lo != *mm.first || s->tr_hi != *mm.second || s->tr_dsg_off != dsg_off) {
         s->tr_bounds.clear();
         if (!s->h_nodes.empty())  // hierarchy bounds over the frame's motion-time range
@@ -2259,12 +2318,11 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     const bool replay = c->jitter == RTX_JITTER_REPLAY;
     if (replay) o_noise = st.put(c->noise, sizeof(float) * 3 * (size_t)c->ncols * c->height * nsamp);
     if (!s->h_nodes.empty()) o_bounds = st.put(split_bounds(s->tr_bounds));
-    // self tests of planes (RTX_SELF_SKIP=0: none). Scenes with secondary rays get none:
+    // self tests of planes (option self_skip 0: none). Scenes with secondary rays get none:
     // MirrorRefraction measured 1.4 % slower with them (most of its shadow rays leave
     // deeper levels, which pay the check and never skip), TSP 3 % and TM 2 % faster
     // (profiles/r04/plane_self/)
-    const char* es = getenv("RTX_SELF_SKIP");
-    const bool pself = !(es && es[0] == '0') && s->view.n_plane > 0 && !s->h_bins.lights.empty() && !s->has_secondary;
+    const bool pself = opt_on(OPT_SELF_SKIP) && s->view.n_plane > 0 && !s->h_bins.lights.empty() && !s->has_secondary;
     if (pself) o_pself = st.put(plane_self_limits(s->h_bins, omax));
     if (s->tr_grids_on) {  // the grid headers with this camera's self-test marks
         std::vector<DSGrid> grids = s->tr_grids;
@@ -2275,8 +2333,7 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     std::vector<float> bz;
     std::vector<uint32_t> bmask, brmask;
     int32_t bins_x = 0, mesh_bins = 0;
-    const char* eb = getenv("RTX_BINS");  // 0 = no primary-ray bins
-    const bool bins = !(eb && eb[0] == '0') &&
+    const bool bins = opt_on(OPT_BINS) &&
                       primary_bins(s->h_bins, c, s->tr_bounds, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins);
     if (bins) {
         if (bfaces.empty()) { bfaces.push_back(0); bz.push_back(0.0f); }
@@ -2479,13 +2536,10 @@ int launch_to_rgb8(const float* fb, uint8_t* out, int64_t n, hipStream_t st) {
 
 // The hierarchy/texture scenes in three passes (rtx_split.h), the default: NovelScene1
 // 2048x1024 AA32 25.8 -> 22.3 ms, NovelScene2 133.9 -> 98.1 ms (twice on one box,
-// profiles/r04/split/). RTX_SPLIT=0 launches the one-kernel form (render_body_spp).
-bool split_enabled() {
-    const char* e = getenv("RTX_SPLIT");
-    return !(e && e[0] == '0');
-}
+// profiles/r04/split/). Option split 0 launches the one-kernel form (render_body_spp).
+bool split_enabled() { return opt_on(OPT_SPLIT); }
 
-// The measured tile schedule ($RTX_TILE_SCHED=0: off). A frame's 8x8 tiles cost very
+// The measured tile schedule (option tile_sched 0: off). A frame's 8x8 tiles cost very
 // different amounts where some pixels follow long reflect/refract chains or cross a mesh
 // (MirrorRefraction 1080p: waves of 2 to 32 us; TorusMesh: 4 to 28 us), and a long wave
 // dispatched late sets the frame's end (profiles/r04/wave_timeline/). The first whole
@@ -2520,19 +2574,12 @@ int tile_schedule(rtx_scene* s, hipStream_t st) {
     return RTX_OK;
 }
 
-// Record bytes of one chunk of the split passes ($RTX_SPLIT_BYTES, default 2 GiB; 40 B per
-// record): NovelScene1 (67 M samples, ~1.8 records each) renders in 3 chunks.
-int64_t split_budget() {
-    const char* e = getenv("RTX_SPLIT_BYTES");
-    const long long v = (e && *e) ? atoll(e) : (2ll << 30);
-    return std::max<long long>(v, 4096);
-}
-// $RTX_SPLIT_RATIO: a fixed deeper-record pool per sample instead of the learned one (the
-// tests force the redo path with a tiny pool).
-double split_fixed_ratio() {
-    const char* e = getenv("RTX_SPLIT_RATIO");
-    return (e && *e) ? std::max(0.0, atof(e)) : -1.0;
-}
+// Record bytes of one chunk of the split passes (option split_bytes, default 2 GiB; 40 B
+// per record): NovelScene1 (67 M samples, ~1.8 records each) renders in 3 chunks.
+int64_t split_budget() { return (int64_t)std::max(4096.0, opt(OPT_SPLIT_BYTES)); }
+// Option split_ratio >= 0: a fixed deeper-record pool per sample instead of the learned
+// one (the tests force the redo path with a tiny pool).
+double split_fixed_ratio() { return opt(OPT_SPLIT_RATIO) >= 0.0 ? opt(OPT_SPLIT_RATIO) : -1.0; }
 
 // The deeper-record pool learns from the counters of an earlier frame once they have
 // arrived on the host (never waits): at least 1/8 more than the fullest chunk needed.
@@ -2738,13 +2785,6 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
             L.tlog = s->tile_sched == 1;
         }
         if (whole) L.tperm = s->tile_sched == 3;
-        if (!spp_mode && persist_waves() > 0) {  // experiment: grid = resident wave slots
-            int cus = 0;
-            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) == hipSuccess && cus > 0) {
-                const int64_t slots = (int64_t)cus * 4 * persist_waves() / (blk / 64);  // blocks
-                nblocks = std::min<int64_t>(nblocks, std::max<int64_t>(1, slots / std::max(1, nframes)));
-            }
-        }
         RTX_HIP(hipModuleLaunchKernel(rs.fn, (unsigned)nblocks, (unsigned)nframes, 1, blk, 1, 1,
                                       s->has_ext ? (unsigned)(hbytes * blk) : 0u, st, args, nullptr));
         if (L.tlog) {  // measured: sorted before the next whole frame

@@ -123,7 +123,7 @@ RTX_HD f3 sample_origin(const KParams& P, int32_t cc, int j, int kd, int ka, con
         if (RTX_JMODE(P) == RTX_JITTER_REPLAY) {
             const int64_t idx = (((int64_t)cc * P.height + j) * RTX_NDOF(P) + kd) * RTX_NAA(P) + ka;
             rnd = ld3(P.noise + 3 * idx);
-        } else if (RTX_ABLATE == 15) {  // cost probe only: no RNG
+        } else if (RTX_PROBE(15)) {  // cost probe only: no RNG
             rnd = mk(0.25f + 0.001f * (float)ka, 0.5f, 0.75f + 0.001f * (float)kd);
         } else if (jr != nullptr) {
             rnd = *jr;
@@ -220,7 +220,7 @@ RTX_HD SceneView sample_scene(const SceneView& S0) {
 template <bool MESH, bool SEC, bool X, bool COUNT, bool JIT>
 RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, int32_t cc, Tally& tl,
                          const FrameStack& fs, const HStack& hs, int32_t bin = -1) {
-    if (RTX_ABLATE == 14) {  // cost probe only: store a constant (launch + framebuffer write)
+    if (RTX_PROBE(14)) {  // cost probe only: store a constant (launch + framebuffer write)
         const int64_t p = (int64_t)rr * P.ncols + cc;
         put_channel(fb, 3 * p, 0.5f); put_channel(fb, 3 * p + 1, 0.25f); put_channel(fb, 3 * p + 2, 0.125f);
         return;
@@ -256,7 +256,7 @@ RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, 
         for (int ka = 0; ka < RTX_NAA(P); ++ka) {
             // the Philox block of samples (2m, 2m + 1), computed at the even one; the odd
             // one's uniforms wait in jr
-            const bool philox = JIT && RTX_JMODE(P) == RTX_JITTER_PHILOX && RTX_ABLATE != 15;
+            const bool philox = JIT && RTX_JMODE(P) == RTX_JITTER_PHILOX && !RTX_PROBE(15);
             const bool odd = ((kd * RTX_NAA(P) + ka) & 1) != 0;
             f3 jr = jr_odd;
             if (philox && !odd) {
@@ -273,7 +273,7 @@ RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, 
         }
     }
     colour = mk(sample_mean(P, colour.x), sample_mean(P, colour.y), sample_mean(P, colour.z));
-#if RTX_ABLATE == 11 && defined(__HIP_DEVICE_COMPILE__)
+#if RTX_PROBE_ON == 11 && defined(__HIP_DEVICE_COMPILE__)
     {  // cost probe only: RTX_PAD extra VALU instructions per pixel in 4 independent chains
         float c0 = colour.x, c1 = colour.y, c2 = colour.z, c3 = (float)cc;
 #pragma unroll
@@ -354,12 +354,6 @@ __host__ __device__ inline int32_t primary_bin(const SceneView& S, int32_t row, 
 // per-wave setup chain: parameters, tables, scene records).
 #ifndef RTX_PPL
 #define RTX_PPL 1
-#endif
-// Persistent waves (experiment, scene-specialized kernels: RTX_PERSIST=1 in the
-// environment): render_body loops over the launch's tiles with a grid of about the
-// resident wave slots (rtx_api.hip render_launch sizes it).
-#ifndef RTX_PERSIST
-#define RTX_PERSIST 0
 #endif
 
 // Output pixel (row, column within the block) of this work-item. RTX_TILE=1 maps each
@@ -500,20 +494,6 @@ __device__ __forceinline__ void render_body(const KParams* __restrict__ Pp, cons
     const FrameStack fs{frames + threadIdx.x, B};
     const HStack hs{hstack + threadIdx.x, B};
     bool any_active = false;
-#if RTX_PERSIST
-    // persistent waves: the grid holds about as many waves as the chip keeps resident, and
-    // each wave renders the tiles w, w + nw, w + 2 nw, ... of the launch (a static stride:
-    // the waves resident at one time cover a contiguous stretch of rows)
-    static_assert(RTX_TILE == 1 && RTX_PPL == 1, "persistent waves take whole 8x8 tiles");
-    const int tiles_x = (ncols + 7) >> 3;
-    const int n_tiles = tiles_x * ((L.nrows + 7) >> 3);
-    const int nw = (int)gridDim.x * (B >> 6);
-    for (int w = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (B >> 6) + (threadIdx.x >> 6))); w < n_tiles;
-         w += nw) {
-        const int lane = threadIdx.x & 63;
-        const int ty = w / tiles_x, tx = w - ty * tiles_x;
-        const PixelRC px{ty * 8 + (lane >> 3), tx * 8 + (lane & 7)};
-#else
 #if RTX_TILE_SCHED && defined(__HIP_DEVICE_COMPILE__)
     static_assert(RTX_TILE == 1 && RTX_PPL == 1, "the tile schedule orders whole 8x8 tiles");
     const unsigned long long tclk0 = L.tlog ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -525,7 +505,6 @@ __device__ __forceinline__ void render_body(const KParams* __restrict__ Pp, cons
 #else
         const PixelRC px = pixel_rc(ncols, sub, L.perm);
 #endif
-#endif
         const bool active = px.r < L.nrows && px.c < ncols;
         any_active = any_active || active;
         // primary-ray face bin of the wave's 8x8 tile (its top-left pixel)
@@ -535,7 +514,7 @@ __device__ __forceinline__ void render_body(const KParams* __restrict__ Pp, cons
             render_pixel<MESH, SEC, X, COUNT, JIT>(*Pp, frame_fb(L), image_row(L, px.r) - px.r, px.r, px.c, tl, fs, hs, bin);
     }
     flush_tally<COUNT>(tl, L.counters, any_active);
-#if RTX_TILE_SCHED && defined(__HIP_DEVICE_COMPILE__) && !RTX_PERSIST
+#if RTX_TILE_SCHED && defined(__HIP_DEVICE_COMPILE__)
     if (L.tlog && (threadIdx.x & 63) == 0 && tile < Pp->tile_n)
         Pp->tile_time[tile] = (unsigned int)(__builtin_amdgcn_s_memrealtime() - tclk0);
 #endif

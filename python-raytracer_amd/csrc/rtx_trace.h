@@ -38,9 +38,20 @@ namespace rtx {
 
 constexpr int kMaxDepth = 10;  // cast_ray(max_recursion=10) (scene.py:81)
 
-// Performance-experiment switch (tools/ablate.sh only; product builds leave it 0).
+// Cost probes (tools/ablate.sh, tools/ab_jitflags.sh): a tools build of the library
+// (-DRTX_TOOLS_BUILD, tools/build_lib_variant.sh) compiles kernels with -DRTX_ABLATE=n that
+// drop or fake one part of the work so that part can be timed. librtx.so is not a tools
+// build: RTX_PROBE(n) is false in it and in every kernel it compiles at run time (its
+// hiprtc sources undefine RTX_TOOLS_BUILD), whatever flags they are given.
 #ifndef RTX_ABLATE
 #define RTX_ABLATE 0
+#endif
+#if defined(RTX_TOOLS_BUILD)
+#define RTX_PROBE(n) (RTX_ABLATE == (n))
+#define RTX_PROBE_ON RTX_ABLATE
+#else
+#define RTX_PROBE(n) false
+#define RTX_PROBE_ON 0
 #endif
 
 // ------------------------------------------------------------------ fp32 vec3 (PyGLM)
@@ -94,7 +105,7 @@ RTX_HD void unspeculated() {
 // glm::normalize = v * inversesqrt(dot(v, v)), inversesqrt(x) = 1 / sqrt(x)
 RTX_HD f3 normalize(f3 v) {
     const float q = dot(v, v);
-#if RTX_ABLATE == 6 && defined(__HIP_DEVICE_COMPILE__)
+#if RTX_PROBE_ON == 6 && defined(__HIP_DEVICE_COMPILE__)
     float inv = __builtin_amdgcn_rsqf(q);  // cost probe only
 #else
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -506,7 +517,7 @@ RTX_HD bool sphere_roots_oc(f3 d, f3 oc, float q, double r2, double& b, double& 
     return true;
 }
 RTX_HD bool sphere_roots(f3 o, f3 d, f3 c, double r2, double& b, double& s, double& two_a) {
-    if (RTX_ABLATE == 4) {  // cost probe only: fp32 quadratic (not parity-correct)
+    if (RTX_PROBE(4)) {  // cost probe only: fp32 quadratic (not parity-correct)
         float a = dot(d, d);
         f3 oc = sub(o, c);
         float bf = 2.0f * dot(d, oc);
@@ -1722,7 +1733,7 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
     Hit h{INFINITY, -1, 0};
     int oi = 0;
     for (int k = 0; k < RTX_NPLANE(S); ++k, ++oi) {  // simple_geometry.py:105-120
-        if (RTX_ABLATE == 18) continue;  // cost probe: no planes in closest_hit
+        if (RTX_PROBE(18)) continue;  // cost probe: no planes in closest_hit
         const DObj ob = S.objs[oi];
         const f3 n = ld3(ob.b);
         const float denom = dot(d, n);
@@ -1745,7 +1756,7 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
 #endif
     for (int k = 0; k < RTX_NSPHERE(S); ++k, ++oi) {  // simple_geometry.py:20-46
         if (!((omask >> (k & 15)) & 1u)) continue;
-        if (RTX_ABLATE == 7) continue;  // cost probe: no spheres in the primary test
+        if (RTX_PROBE(7)) continue;  // cost probe: no spheres in the primary test
         const DObj ob = S.objs[oi];
         const f3 ctr = moved(ob, ob.a, time);
         bool valid = false;
@@ -1760,7 +1771,7 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
 #endif
         if (sphere_disc_sign_oc(d, oc, q, ob.r2f) >= 0) {  // fp64 only where a hit is possible
             double b, s, two_a;
-            if (RTX_ABLATE == 4 ? sphere_roots(o, d, ctr, ob.r2, b, s, two_a) : sphere_roots_oc(d, oc, q, ob.r2, b, s, two_a)) {
+            if (RTX_PROBE(4) ? sphere_roots(o, d, ctr, ob.r2, b, s, two_a) : sphere_roots_oc(d, oc, q, ob.r2, b, s, two_a)) {
                 double t = (-b - s) / two_a;
                 const bool near = t > 0.0;
                 // the far root only where some lane needs it (a ray from inside the sphere)
@@ -1778,7 +1789,7 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
     if (RTX_NBOX(S) > 0 || (MESH && RTX_NMESH(S) > 0)) ri = ray_inv(o, d);
     for (int k = 0; k < RTX_NBOX(S); ++k, ++oi) {  // simple_geometry.py:188-249 (entry precedes exit)
         if (!((omask >> (16 + (k & 15))) & 1u)) continue;
-        if (RTX_ABLATE == 17) continue;  // cost probe: no boxes in closest_hit
+        if (RTX_PROBE(17)) continue;  // cost probe: no boxes in closest_hit
         const DObj ob = S.objs[oi];
         const f3 mn = moved(ob, ob.a, time), mx = moved(ob, ob.b, time);
         double start = 0.0;
@@ -1842,7 +1853,7 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
             }
         }
     }
-    if (X && RTX_ABLATE != 9) {  // hierarchies (hierarchy.py:42-78)
+    if (X && !RTX_PROBE(9)) {  // hierarchies (hierarchy.py:42-78)
 #if defined(RTX_PRIMARY_BINS) && !RTX_PRIMARY_BINS
         hier_closest<MESH>(S, hs, o, d, time, h, hh);
 #else
@@ -1962,7 +1973,7 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
         pm = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
     }
     for (int k = 0; k < RTX_NPLANE(S); ++k, ++oi) {  // simple_geometry.py:122-131
-        if (RTX_ABLATE == 21) continue;  // cost probe: planes never occlude
+        if (RTX_PROBE(21)) continue;  // cost probe: planes never occlude
         // a camera hit on this plane, close enough to the origin: its own test cannot pass
         if (pself != nullptr && k < 4 && RTX_ALL(occ || (oi == self_obj && pm <= pself[k]))) continue;
         const DObj ob = S.objs[oi];
@@ -2013,7 +2024,7 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
 #endif
     const uint32_t smask = sc.obj;
     for (int k = 0; k < RTX_NSPHERE(S); ++k, ++oi) {  // simple_geometry.py:48-72 (shadow_epsilon 1e-3)
-        if (RTX_ABLATE == 19) continue;  // cost probe: spheres never occlude
+        if (RTX_PROBE(19)) continue;  // cost probe: spheres never occlude
         const bool sl = ((smask >> (k & 15)) & 1u) != 0u;
         if (!RTX_ANY(sl && !occ)) continue;
         const DObj ob = S.objs[oi];
@@ -2026,13 +2037,13 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
         const float q = dot(oc, oc);
 #endif
         int dec = -1;
-        if (RTX_SHADOW_F32 && RTX_ABLATE != 4) {
+        if (RTX_SHADOW_F32 && !RTX_PROBE(4)) {
             dec = sphere_shadow_f32(d, oc, q, ob.r2f, tmax_dn, tmax_up);
             if (!occ && sl && dec >= 0) occ = dec == 1;
         }
         if (!occ && sl && dec < 0 && sphere_disc_sign_oc(d, oc, q, ob.r2f) >= 0) {
             double b, s, two_a;
-            if (RTX_ABLATE == 4 ? sphere_roots(o, d, ctr, ob.r2, b, s, two_a)
+            if (RTX_PROBE(4) ? sphere_roots(o, d, ctr, ob.r2, b, s, two_a)
                                 : sphere_roots_oc(d, oc, q, ob.r2, b, s, two_a)) {
                 const double t1 = (-b - s) / two_a;
                 bool hit = 1e-3 < t1 && t1 < t_max;
@@ -2057,7 +2068,7 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
         have_ri = true;
     }
     for (int k = 0; k < RTX_NBOX(S); ++k, ++oi) {  // simple_geometry.py:251-294
-        if (RTX_ABLATE == 20) continue;  // cost probe: boxes never occlude
+        if (RTX_PROBE(20)) continue;  // cost probe: boxes never occlude
         const bool sl = ((smask >> (16 + (k & 15))) & 1u) != 0u && !(oi == self_obj && k < 16 && ((self_boxes >> (16 + k)) & 1u));
         if (!RTX_ANY(sl && !occ)) continue;
         const DObj ob = S.objs[oi];
@@ -2077,16 +2088,16 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
     if (MESH) {
         for (int k = 0; k < RTX_NMESH(S); ++k, ++oi) {  // mesh.py:121-153 (no t_max test)
             const DObj ob = S.objs[oi];
-            if (RTX_ALL(occ) || RTX_ABLATE == 16) break;  // 16: cost probe, meshes never occlude
+            if (RTX_ALL(occ) || RTX_PROBE(16)) break;  // 16: cost probe, meshes never occlude
             if (!have_ri) {
                 ri = ray_inv(o, d);
                 have_ri = true;
             }
             bool live = !occ && bv_maybe(ob, o, ri, INFINITY);  // conservative pre-test
             if (!RTX_ANY(live)) continue;
-            if (RTX_ABLATE == 13) continue;  // cost probe: the padded box pre-test only
+            if (RTX_PROBE(13)) continue;  // cost probe: the padded box pre-test only
             live = live && mesh_bv(ob, o, d);
-            if (!RTX_ANY(live) || RTX_ABLATE == 12) continue;  // 12: cost probe, bounding volumes only
+            if (!RTX_ANY(live) || RTX_PROBE(12)) continue;  // 12: cost probe, bounding volumes only
             // mesh.py:125-151 for stored face f (lanes with maybe set may take it)
             auto shadow_face = [&](int f, bool maybe) {
                 bool fmaybe = maybe;
@@ -2146,7 +2157,7 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
             }
         }
     }
-    if (X && RTX_ABLATE != 10) occ = hier_occluded<MESH>(S, hs, o, d, t_max, time, occ, sc.root);  // hierarchy.py:80-109
+    if (X && !RTX_PROBE(10)) occ = hier_occluded<MESH>(S, hs, o, d, t_max, time, occ, sc.root);  // hierarchy.py:80-109
     return occ;
 }
 
@@ -2226,7 +2237,7 @@ __host__ __device__ __attribute__((noinline)) inline double pow_int_dd(double x,
 // selects, so lanes shading different materials do not diverge; each lane performs
 // exactly the multiplications of `while (n) { if (n & 1) r *= b; b *= b; n >>= 1; }`.
 RTX_HD double spec_pow(double x, const DMat& m, int pow_bits) {
-    if (RTX_ABLATE == 5) return (double)__builtin_powf((float)x, (float)m.hardness);  // cost probe only
+    if (RTX_PROBE(5)) return (double)__builtin_powf((float)x, (float)m.hardness);  // cost probe only
 #ifdef RTX_FIXED_HARD  // scene-specialized: every specular lobe has this integer hardness
     if (true) {
         const int n = RTX_FIXED_HARD;
@@ -2288,10 +2299,10 @@ RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const 
         tally_inc<COUNT>(tl, &Tally::shadow);
         if (occ_mask >= 0) {
             if ((occ_mask >> li) & 1) continue;
-        } else if (RTX_ABLATE != 1 && occluded<MESH, X, COUNT>(S, pos, sdir, t_max, time, tl, hs, otp, li, self_obj)) {
+        } else if (!RTX_PROBE(1) && occluded<MESH, X, COUNT>(S, pos, sdir, t_max, time, tl, hs, otp, li, self_obj)) {
             continue;
         }
-        if (RTX_ABLATE == 3) { colour = add(colour, mul(ld3(L.cp), diffuse)); continue; }
+        if (RTX_PROBE(3)) { colour = add(colour, mul(ld3(L.cp), diffuse)); continue; }
         f3 light_dir = point ? normalize(sdir) : ld3(L.ndir);
         f3 lambert = scale(diffuse, pos_part(dot(normal, light_dir)));
         f3 ls = lambert;
@@ -2367,7 +2378,7 @@ RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const 
     bool in_shape = false;
     for (int level = 0; level < (SEC ? kMaxDepth : 1); ++level) {
         if (COUNT) tl.cast[level]++;
-        if (RTX_ABLATE == 8) { tail = d; break; }  // cost probe: camera + store only
+        if (RTX_PROBE(8)) { tail = d; break; }  // cost probe: camera + store only
         HHit hh;
         const Hit h = closest_hit<MESH, X, COUNT>(S, o, d, time, tl, hs, hh, level == 0 ? bin : -1,
                                                   level == 0 ? prim : nullptr);
@@ -2391,7 +2402,7 @@ RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const 
             next_d = rdir;
             chain = true;
         }
-        if ((RTX_ABLATE == 2 || RTX_ABLATE == 7) && !chain) { tail = ld3(m.diffuse); break; }
+        if ((RTX_PROBE(2) || RTX_PROBE(7)) && !chain) { tail = ld3(m.diffuse); break; }
         // scene.py:143-146: Plane/AABB hits shade with get_diffuse(position)
         const f3 diffuse = (X && sf.gobj >= 0) ? get_diffuse(S, S.objs[sf.gobj], sf.position, time) : ld3(m.diffuse);
         // a camera ray's hit (level 0) tells occluded which flat object it lies on

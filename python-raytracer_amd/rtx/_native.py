@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_lib", "librtx.so")
 # Experiment builds (tools/ablate.sh) point this at another build of the same HIP source.
 LIB_PATH = os.environ.get("RTX_LIB_OVERRIDE", LIB_PATH)
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 RTX_OK, RTX_ERR_INVALID, RTX_ERR_HIP, RTX_ERR_UNSUPPORTED, RTX_ERR_STATE = 0, -1, -2, -3, -4
 RTX_SPHERE, RTX_PLANE, RTX_BOX, RTX_MESH, RTX_NODE = 0, 1, 2, 3, 4
@@ -88,7 +88,7 @@ _lib = None
 EXPORTS = ["rtx_abi_version", "rtx_last_error", "rtx_scene_create", "rtx_scene_destroy", "rtx_camera_set",
            "rtx_render", "rtx_render_groups", "rtx_group_rows", "rtx_intersect", "rtx_occluded", "rtx_fb_to_rgb8",
            "rtx_render_rgb8", "rtx_render_groups_rgb8", "rtx_last_kernel", "rtx_render_frames",
-           "rtx_render_groups_frames", "rtx_jit_modules"]
+           "rtx_render_groups_frames", "rtx_jit_modules", "rtx_set_option", "rtx_get_option", "rtx_option_name"]
 
 
 def load():
@@ -120,12 +120,17 @@ def load():
         lib.rtx_occluded.argtypes = [vp, C.c_int64, vp, vp, vp, C.c_double, vp, vp]
         lib.rtx_fb_to_rgb8.argtypes = [vp, vp, C.c_int64, vp]
         for fn in EXPORTS:  # every status-returning entry point (not the string / count ones)
-            if fn not in ("rtx_abi_version", "rtx_last_error", "rtx_last_kernel", "rtx_group_rows", "rtx_jit_modules"):
+            if fn not in ("rtx_abi_version", "rtx_last_error", "rtx_last_kernel", "rtx_group_rows", "rtx_jit_modules",
+                          "rtx_option_name"):
                 getattr(lib, fn).restype = C.c_int
         lib.rtx_last_kernel.argtypes = [vp]
         lib.rtx_last_kernel.restype = C.c_char_p
         lib.rtx_jit_modules.argtypes = []
         lib.rtx_jit_modules.restype = C.c_int32
+        lib.rtx_set_option.argtypes = [C.c_char_p, C.c_char_p]
+        lib.rtx_get_option.argtypes = [C.c_char_p, C.c_char_p, C.c_int32]
+        lib.rtx_option_name.argtypes = [C.c_int32]
+        lib.rtx_option_name.restype = C.c_char_p
         v = lib.rtx_abi_version()
         if v != ABI_VERSION:
             raise RuntimeError("librtx.so ABI %d != binding ABI %d" % (v, ABI_VERSION))
@@ -140,6 +145,32 @@ def check(fn, rc):
 
 def call(fn, *args):
     check(fn, getattr(load(), fn)(*args))
+
+
+def set_option(name, value):
+    """rtx_set_option: a library option by name (include/rtx.h; INTEGRATION.md "Options")."""
+    call("rtx_set_option", str(name).encode(), str(value).encode())
+
+
+def get_option(name):
+    """rtx_get_option: the option's value (a float, or a str for jit_cache / jit_flags)."""
+    buf = C.create_string_buffer(4096)
+    call("rtx_get_option", str(name).encode(), buf, len(buf))
+    v = buf.value.decode()
+    if name in ("jit_cache", "jit_flags"):
+        return v
+    return float(v)
+
+
+def option_names():
+    lib = load()
+    out, i = [], 0
+    while True:
+        n = lib.rtx_option_name(i)
+        if n is None:
+            return out
+        out.append(n.decode())
+        i += 1
 
 
 def f3(v):

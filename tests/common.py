@@ -64,3 +64,26 @@ def product_scene_dict(data):
     d = copy.deepcopy(data)
     d["__base_dir__"] = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets")
     return rtx.load_scene(d, verbose=False)
+
+
+class _Options:
+    """The library options (rtx.set_option / rtx.get_option) as attributes, so a test can
+    set one for its own duration with monkeypatch.setattr(OPTS, "bins", "0"): the old value
+    is read back and restored at teardown. The host emulation (tests/hostemu.py) includes
+    the library's source and has its own copy of the options: it gets the same value when
+    the test module has imported it."""
+
+    def __getattr__(self, name):
+        import rtx
+        return rtx.get_option(name)
+
+    def __setattr__(self, name, value):
+        import sys
+        import rtx
+        rtx.set_option(name, value)
+        he = sys.modules.get("hostemu")  # (imported by the host-emulation tests only)
+        if he is not None:
+            he.set_option(name, value)
+
+
+OPTS = _Options()

@@ -230,3 +230,10 @@ def jit_baked(scene):
     buf = C.create_string_buffer(int(n) + 1)
     f(C.addressof(sd), buf, n + 1)
     return buf.value.decode()
+
+
+def set_option(name, value):
+    """rtx_set_option of the host emulation's copy of the library options."""
+    f = lib().rtx_set_option
+    f.argtypes = [C.c_char_p, C.c_char_p]
+    _chk(f(str(name).encode(), str(value).encode()))

@@ -60,8 +60,7 @@ struct Grids {
     std::vector<int32_t> start, faces;
     std::vector<float> d2;
     void bind(const HostScene& H, SceneView& v) {
-        const char* e = getenv("RTX_LGRID");
-        if ((e && e[0] == '0') || !light_grids(H, grids, start, faces, d2)) return;
+        if (!opt_on(OPT_LGRID) || !light_grids(H, grids, start, faces, d2)) return;
         if (faces.empty()) { faces.push_back(0); d2.push_back(0.0f); }
         v.lgrid = (cptr<DLGrid>)grids.data();
         v.lg_start = (cptr<int32_t>)start.data();
@@ -78,13 +77,12 @@ struct DirGrids {
     std::vector<DSCell> cells;
     std::vector<float> pself;
     void bind(const HostScene& H, SceneView& v, float tlo, float thi, double omax = INFINITY) {
-        const char* es = getenv("RTX_SELF_SKIP");  // the planes' self tests, as rtx_camera_set
-        if (!(es && es[0] == '0') && H.n_plane > 0 && !H.lights.empty()) {
+        // the planes' self tests, as rtx_camera_set
+        if (opt_on(OPT_SELF_SKIP) && H.n_plane > 0 && !H.lights.empty()) {
             pself = plane_self_limits(H, omax);
             v.plane_self = (cptr<float>)pself.data();
         }
-        const char* e = getenv("RTX_DSGRID");
-        if (e && e[0] == '0') return;
+        if (!opt_on(OPT_DSGRID)) return;
         std::vector<DBound> nb;
         if (!H.nodes.empty()) nb = compute_bounds(H.nodes, H.objs, H.tris, tlo, thi);
         if (!dir_shadow_grids(H, nb, tlo, thi, grids, cells)) return;
@@ -143,8 +141,7 @@ extern "C" int rtx_hostemu_render(const rtx_scene_desc* sd, const rtx_camera_des
     std::vector<float> bz;
     std::vector<uint32_t> bmask, brmask;
     int32_t bins_x = 0, mesh_bins = 0;
-    const char* be = getenv("RTX_BINS");
-    if (!(be && be[0] == '0') && primary_bins(H, cd, nv.bounds, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins)) {
+    if (opt_on(OPT_BINS) && primary_bins(H, cd, nv.bounds, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins)) {
         if (bfaces.empty()) { bfaces.push_back(0); bz.push_back(0.0f); }
         k.S.bin_start = (cptr<int32_t>)bstart.data();
         k.S.bin_faces = (cptr<int32_t>)bfaces.data();
@@ -212,8 +209,7 @@ extern "C" int rtx_hostemu_render_rows(const rtx_scene_desc* sd, const rtx_camer
     std::vector<float> bz;
     std::vector<uint32_t> bmask, brmask;
     int32_t bins_x = 0, mesh_bins = 0;
-    const char* be = getenv("RTX_BINS");
-    if (!(be && be[0] == '0') && primary_bins(H, cd, nv.bounds, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins)) {
+    if (opt_on(OPT_BINS) && primary_bins(H, cd, nv.bounds, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins)) {
         if (bfaces.empty()) { bfaces.push_back(0); bz.push_back(0.0f); }
         k.S.bin_start = (cptr<int32_t>)bstart.data();
         k.S.bin_faces = (cptr<int32_t>)bfaces.data();
@@ -501,10 +497,9 @@ extern "C" int64_t rtx_hostemu_jit_spec(const rtx_scene_desc* sd, const rtx_came
     std::vector<float> bz;
     std::vector<uint32_t> bmask, brmask;
     int32_t bins_x = 0, mesh_bins = 0;
-    const char* be = getenv("RTX_BINS");
     std::vector<DBound> nodeb;
     if (!H.nodes.empty()) nodeb = compute_bounds(H.nodes, H.objs, H.tris, *tmm.first, *tmm.second);
-    if (!(be && be[0] == '0') && primary_bins(H, cd, nodeb, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins))
+    if (opt_on(OPT_BINS) && primary_bins(H, cd, nodeb, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins))
         k.S.bins_on = 1;
     const int spp = k.n_dof * k.n_aa * k.n_times;
     const bool spp_mode = use_spp_mode(spp, H.has_ext);
@@ -633,8 +628,7 @@ extern "C" int rtx_hostemu_render_split(const rtx_scene_desc* sd, const rtx_came
     std::vector<float> bz;
     std::vector<uint32_t> bmask, brmask;
     int32_t bins_x = 0, mesh_bins = 0;
-    const char* be = getenv("RTX_BINS");
-    if (!(be && be[0] == '0') && primary_bins(H, cd, nv.bounds, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins)) {
+    if (opt_on(OPT_BINS) && primary_bins(H, cd, nv.bounds, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins)) {
         if (bfaces.empty()) { bfaces.push_back(0); bz.push_back(0.0f); }
         k.S.bin_start = (cptr<int32_t>)bstart.data();
         k.S.bin_faces = (cptr<int32_t>)bfaces.data();

@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 from common import assert_parity, oracle_render_dict, product_scene_dict
+from common import OPTS
 
 pytestmark = pytest.mark.gpu
 
@@ -22,9 +23,9 @@ def test_baked_kernels_are_bounded(tmp_path, monkeypatch):
     cache = tmp_path / "jit"
     cache.mkdir(mode=0o700)
     os.chmod(cache, 0o700)
-    monkeypatch.setenv("RTX_JIT_CACHE", str(cache))
-    monkeypatch.setenv("RTX_JIT_IDLE_BAKED", "1")
-    monkeypatch.setenv("RTX_JIT_DISK_BAKED", "2")
+    monkeypatch.setattr(OPTS, "jit_cache", str(cache))
+    monkeypatch.setattr(OPTS, "jit_idle_baked", "1")
+    monkeypatch.setattr(OPTS, "jit_disk_baked", "2")
     lib = N.load()
     base = lib.rtx_jit_modules()
     d = bundled_scene_dict("TwoSpheresPlane", resolution=(32, 24), spp=(1, None))  # one sample: baked records

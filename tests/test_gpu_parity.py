@@ -4,6 +4,7 @@ import pytest
 import torch
 
 from common import assert_parity, compare, oracle_render, product_scene
+from common import OPTS
 
 pytestmark = pytest.mark.gpu
 
@@ -347,13 +348,13 @@ def test_scene_specialized_kernel_equals_generic(name, res, edits, monkeypatch):
     kernel: identical framebuffers and counters, and rtx_last_kernel shows that each side
     really ran the kernel it is meant to (hierarchy/texture scenes specialize only under
     RTX_JIT_EXT=1, which this test sets)."""
-    monkeypatch.setenv("RTX_JIT_EXT", "1")
-    monkeypatch.setenv("RTX_SPLIT", "0")  # the generic side: the one-kernel form
+    monkeypatch.setattr(OPTS, "jit_ext", "1")
+    monkeypatch.setattr(OPTS, "split", "0")  # the generic side: the one-kernel form
     sc = product_scene(name, res, **edits)
     cnt_a = torch.zeros(16, dtype=torch.int64, device="cuda")
     a = sc.render_device(counters=cnt_a).clone()
     assert sc.last_kernel.startswith("rtx_jit_render_"), sc.last_kernel
-    monkeypatch.setenv("RTX_JIT", "0")
+    monkeypatch.setattr(OPTS, "jit", "0")
     cnt_b = torch.zeros(16, dtype=torch.int64, device="cuda")
     b = sc.render_device(counters=cnt_b).clone()
     assert sc.last_kernel.startswith("k_render"), sc.last_kernel
@@ -405,8 +406,8 @@ def test_sample_parallel_mapping_matches_oracle(name, res, edits, monkeypatch):
     """The sample-parallel mapping (render_body_spp, forced for every sample count, 1 to
     NovelScene2's 240) vs the oracle: exact, i.e. the owner lanes' in-order LDS sums equal
     the reference's per-pixel accumulation."""
-    monkeypatch.setenv("RTX_SPP", "1")
-    monkeypatch.setenv("RTX_SPLIT", "0")  # hierarchy scenes: the one-kernel form's mapping
+    monkeypatch.setattr(OPTS, "spp", "1")
+    monkeypatch.setattr(OPTS, "split", "0")  # hierarchy scenes: the one-kernel form's mapping
     sc = product_scene(name, res, **edits)
     W, H = res
     fb = torch.full((H, W, 3), float("nan"), dtype=torch.float32, device="cuda")  # every pixel must be written
@@ -428,11 +429,11 @@ def test_sample_parallel_mapping_matches_oracle(name, res, edits, monkeypatch):
 def test_sample_parallel_equals_pixel_mapping(name, res, edits, rows, monkeypatch):
     """Both mappings on the production (Philox) jitter: identical framebuffers (bitwise)
     and ray counters, on row blocks that start mid-frame."""
-    monkeypatch.setenv("RTX_SPLIT", "0")  # hierarchy scenes: the one-kernel form's two mappings
+    monkeypatch.setattr(OPTS, "split", "0")  # hierarchy scenes: the one-kernel form's two mappings
     sc = product_scene(name, res, **edits)
     out = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("RTX_SPP", mode)
+        monkeypatch.setattr(OPTS, "spp", mode)
         cnt = torch.zeros(16, dtype=torch.int64, device="cuda")
         fb = torch.full((rows[1], res[0], 3), float("nan"), dtype=torch.float32, device="cuda")
         out[mode] = (sc.render_device(row0=rows[0], nrows=rows[1], out=fb, counters=cnt), cnt)
@@ -516,10 +517,10 @@ def test_primary_bins_equal_walk(seed, monkeypatch):
     d = bins_scene(seed, res=(97, 61))
     on = product_scene_dict(d)
     a = on.render_device().clone()
-    monkeypatch.setenv("RTX_BINS", "0")
+    monkeypatch.setattr(OPTS, "bins", "0")
     off = product_scene_dict(d)  # RTX_BINS is read when the camera is uploaded
     b = off.render_device().clone()
-    monkeypatch.delenv("RTX_BINS")
+    monkeypatch.setattr(OPTS, "bins", "1")
     assert torch.equal(a, b)
     img = np.ascontiguousarray(np.transpose(a.cpu().numpy()[::-1], (1, 0, 2))).astype(np.float64)
     assert_parity(img, oracle_render_dict(d), "bins seed %d" % seed)
@@ -541,9 +542,9 @@ def test_lens_bins_equal_walk(seed, monkeypatch):
     d = bins_scene(seed, res=(160, 96), lens=True)
     on = product_scene_dict(d)
     a = on.render_device().clone()
-    monkeypatch.setenv("RTX_BINS", "0")
+    monkeypatch.setattr(OPTS, "bins", "0")
     b = product_scene_dict(d).render_device().clone()
-    monkeypatch.delenv("RTX_BINS")
+    monkeypatch.setattr(OPTS, "bins", "1")
     assert torch.equal(a, b)
     if seed % 4 == 0:
         img = np.ascontiguousarray(np.transpose(a.cpu().numpy()[::-1], (1, 0, 2))).astype(np.float64)
@@ -557,7 +558,7 @@ def test_lens_bins_config5_full_frame(monkeypatch):
     edits = {"AA": {"jitter": True, "samples": 2}}
     res = (3840, 2160)
     a = product_scene("DepthOfField", res, **edits).render_device().clone()
-    monkeypatch.setenv("RTX_LENS_BINS", "0")
+    monkeypatch.setattr(OPTS, "lens_bins", "0")
     b = product_scene("DepthOfField", res, **edits).render_device().clone()
     torch.cuda.synchronize()
     assert torch.equal(a, b), float((a != b).float().mean())
@@ -570,12 +571,12 @@ def test_dir_shadow_grids_equal_walk(seed, monkeypatch):
     object (RTX_DSGRID=0) == oracle, 160x120 frames."""
     from common import oracle_render_dict, product_scene_dict
     from scenegen import shadow_scene
-    monkeypatch.setenv("RTX_DSGRID_MIN", "1")  # a grid for every scene, however few its spheres
+    monkeypatch.setattr(OPTS, "dsgrid_min", "1")  # a grid for every scene, however few its spheres
     d = shadow_scene(seed, res=(160, 120))
     a = product_scene_dict(d).render_device().clone()
-    monkeypatch.setenv("RTX_DSGRID", "0")
+    monkeypatch.setattr(OPTS, "dsgrid", "0")
     b = product_scene_dict(d).render_device().clone()
-    monkeypatch.delenv("RTX_DSGRID")
+    monkeypatch.setattr(OPTS, "dsgrid", "1")
     assert torch.equal(a, b)
     img = np.ascontiguousarray(np.transpose(a.cpu().numpy()[::-1], (1, 0, 2))).astype(np.float64)
     assert_parity(img, oracle_render_dict(d), "shadow grids seed %d" % seed)
@@ -587,9 +588,9 @@ def test_dir_shadow_grids_full_frames(name, res, edits, monkeypatch):
     """The BASELINE configs with directional lights, with their shadow grids and without:
     the same frames, bit for bit (MirrorRefraction's four spheres get a grid only when
     RTX_DSGRID_MIN allows it)."""
-    monkeypatch.setenv("RTX_DSGRID_MIN", "1")
+    monkeypatch.setattr(OPTS, "dsgrid_min", "1")
     a = product_scene(name, res, **edits).render_device().clone()
-    monkeypatch.setenv("RTX_DSGRID", "0")
+    monkeypatch.setattr(OPTS, "dsgrid", "0")
     b = product_scene(name, res, **edits).render_device().clone()
     torch.cuda.synchronize()
     assert torch.equal(a, b), float((a != b).float().mean())
@@ -603,13 +604,13 @@ def test_wave_cooperative_mesh_matches_oracle(case, tmp_path, monkeypatch):
     refracted rays reach the meshes from a subset of a wave's lanes, ragged tiles included."""
     from common import oracle_render_dict, product_scene_dict
     from scenegen import blob_obj, blob_scene, bins_scene, random_scene
-    monkeypatch.setenv("RTX_JIT_FLAGS", "-DRTX_WCOOP=1 -DRTX_WCOOP_MIN=1")
+    monkeypatch.setattr(OPTS, "jit_flags", "-DRTX_WCOOP=1 -DRTX_WCOOP_MIN=1")
     if case.startswith("blob"):
         p = str(tmp_path / "blob6.obj")
         blob_obj(p, level=6)
         d = blob_scene(p, (64, 64))
         if case == "blob_walk":
-            monkeypatch.setenv("RTX_BINS", "0")
+            monkeypatch.setattr(OPTS, "bins", "0")
     elif case.startswith("bins"):
         d = bins_scene(int(case[4:]), res=(97, 61))
     else:
@@ -639,7 +640,7 @@ def test_light_grids_equal_walk(case, tmp_path, monkeypatch):
     else:
         d = random_scene(int(case[6:]), res=(64, 48), mesh=True)
     a = product_scene_dict(d).render_device().clone()
-    monkeypatch.setenv("RTX_LGRID", "0")
+    monkeypatch.setattr(OPTS, "lgrid", "0")
     b = product_scene_dict(d).render_device().clone()
     assert torch.equal(a, b)
     img = np.ascontiguousarray(np.transpose(a.cpu().numpy()[::-1], (1, 0, 2))).astype(np.float64)
@@ -654,7 +655,7 @@ def test_render_frames_equals_per_frame_renders(name, res, edits, jit, monkeypat
     """rtx_render_frames (one launch, gridDim.y = frames) writes into every slot exactly
     what rtx_render / rtx_render_rgb8 write for the same rows, for the specialized and the
     generic kernels; the slots' padding rows stay untouched."""
-    monkeypatch.setenv("RTX_JIT", jit)
+    monkeypatch.setattr(OPTS, "jit", jit)
     sc = product_scene(name, res, **edits)
     H, W = res[1], res[0]
     for dtype in (torch.uint8, torch.float32):
@@ -693,8 +694,8 @@ def test_primary_bins_wide_frame(seed, monkeypatch):
     from scenegen import bins_scene
     d = bins_scene(seed, res=(7680, 16))
     a = product_scene_dict(d).render(7, 8)
-    monkeypatch.setenv("RTX_BINS", "0")
+    monkeypatch.setattr(OPTS, "bins", "0")
     b = product_scene_dict(d).render(7, 8)
-    monkeypatch.delenv("RTX_BINS")
+    monkeypatch.setattr(OPTS, "bins", "1")
     assert np.array_equal(a, b)
     assert_parity(a, oracle_render_dict(d, 7, 8), "wide bins seed %d" % seed)

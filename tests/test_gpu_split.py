@@ -7,6 +7,7 @@ import pytest
 import torch
 
 from common import assert_parity, oracle_render, oracle_render_dict, product_scene, product_scene_dict
+from common import OPTS
 
 pytestmark = pytest.mark.gpu
 
@@ -20,7 +21,7 @@ CASES = [
 
 @pytest.fixture
 def split(monkeypatch):
-    monkeypatch.setenv("RTX_SPLIT", "1")
+    monkeypatch.setattr(OPTS, "split", "1")
 
 
 @pytest.mark.parametrize("name,res,edits", CASES)
@@ -54,7 +55,7 @@ def test_split_tallies_match_oracle(split):
 
 def test_split_small_chunks_and_row_groups(split, monkeypatch):
     """Many chunks (RTX_SPLIT_BYTES small) and interleaved 8-row groups: the same frame."""
-    monkeypatch.setenv("RTX_SPLIT_BYTES", str(4000 * 40))
+    monkeypatch.setattr(OPTS, "split_bytes", str(4000 * 40))
     name, res, edits = "NovelScene1", (80, 40), {"AA": {"jitter": False, "samples": 2}}
     sc = product_scene(name, res, **edits)
     ref = oracle_render(name, res, **edits)
@@ -76,10 +77,10 @@ def test_split_equals_one_kernel_full_novel_scene1(monkeypatch):
     H, W = sc.vc.height, sc.vc.width
     a = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
     b = torch.empty_like(a)
-    monkeypatch.setenv("RTX_SPLIT", "0")
+    monkeypatch.setattr(OPTS, "split", "0")
     sc.render_device(out=a)
     one = sc.last_kernel
-    monkeypatch.setenv("RTX_SPLIT", "1")
+    monkeypatch.setattr(OPTS, "split", "1")
     sc.render_device(out=b)
     torch.cuda.synchronize()
     assert one.startswith("k_render_ext") and sc.last_kernel.startswith("k_split_"), (one, sc.last_kernel)
@@ -97,8 +98,8 @@ def test_split_many_roots_bins_and_grids(seed, split, monkeypatch):
     sc = product_scene_dict(d)
     a = sc.render_device().clone()
     assert sc.last_kernel.startswith("k_split_"), sc.last_kernel
-    monkeypatch.setenv("RTX_BINS", "0")
-    monkeypatch.setenv("RTX_DSGRID", "0")
+    monkeypatch.setattr(OPTS, "bins", "0")
+    monkeypatch.setattr(OPTS, "dsgrid", "0")
     b = product_scene_dict(d).render_device().clone()
     assert torch.equal(a, b)
     img = np.ascontiguousarray(np.transpose(a.cpu().numpy()[::-1], (1, 0, 2))).astype(np.float64)
@@ -112,9 +113,9 @@ def test_split_pool_overflow_redo(ratio, budget, split, monkeypatch):
     blocks, and the one-kernel form renders those again after pass C (render_body_spp with
     L.redo) -- the frame is the oracle's, bit for bit, on frames with many mirrors."""
     from scenegen import random_hier_scene
-    monkeypatch.setenv("RTX_SPLIT_RATIO", ratio)
+    monkeypatch.setattr(OPTS, "split_ratio", ratio)
     if budget:
-        monkeypatch.setenv("RTX_SPLIT_BYTES", budget)
+        monkeypatch.setattr(OPTS, "split_bytes", budget)
     for seed in (3, 5):
         d = random_hier_scene(seed, res=(40, 30))
         d["materials"] = [dict(m, type="mirror", tint=m.get("tint", 0.3)) if i % 2 == 0 else m

@@ -6,6 +6,7 @@ import pytest
 
 import hostemu
 from common import assert_parity, oracle_render, product_scene
+from common import OPTS
 
 CASES = [
     ("TwoSpheresPlane", (160, 120), {}),
@@ -238,10 +239,10 @@ def test_hostemu_primary_bins_equal_walk(seed, monkeypatch):
     d = bins_scene(seed)
     sc = product_scene_dict(d)
     img, _ = hostemu.render(sc)
-    monkeypatch.setenv("RTX_BINS", "0")
+    monkeypatch.setattr(OPTS, "bins", "0")
     walk, _ = hostemu.render(sc)
     assert np.array_equal(img, walk)
-    monkeypatch.delenv("RTX_BINS")
+    monkeypatch.setattr(OPTS, "bins", "1")
     assert_parity(img, oracle_render_dict(d), "bins seed %d" % seed)
     for k in range(3):
         strip, _ = hostemu.render(sc, k, 3)
@@ -328,9 +329,9 @@ def test_hostemu_light_grids_frames(blob5, flat, monkeypatch):
     for d in (bundled_scene_dict("TorusMesh", resolution=(48, 48)), blob_scene(blob5, (40, 40), flat)):
         sc = product_scene_dict(d)
         img, _ = hostemu.render(sc)
-        monkeypatch.setenv("RTX_LGRID", "0")
+        monkeypatch.setattr(OPTS, "lgrid", "0")
         walk, _ = hostemu.render(sc)
-        monkeypatch.delenv("RTX_LGRID")
+        monkeypatch.setattr(OPTS, "lgrid", "1")
         assert np.array_equal(img, walk)
         assert_parity(img, oracle_render_dict(d), "light grids")
 
@@ -435,9 +436,9 @@ def test_hostemu_primary_bins_wide_frame(seed, monkeypatch):
     sc = product_scene_dict(d)
     for k in (0, 7):
         img, _ = hostemu.render(sc, k, 8)
-        monkeypatch.setenv("RTX_BINS", "0")
+        monkeypatch.setattr(OPTS, "bins", "0")
         walk, _ = hostemu.render(product_scene_dict(d), k, 8)
-        monkeypatch.delenv("RTX_BINS")
+        monkeypatch.setattr(OPTS, "bins", "1")
         assert np.array_equal(img, walk), k
         assert_parity(img, oracle_render_dict(d, k, 8), "wide bins seed %d strip %d" % (seed, k))
 
@@ -462,9 +463,9 @@ def test_hostemu_lens_bins_equal_walk(seed, monkeypatch):
     d = bins_scene(seed, res=(33, 19), lens=True)
     sc = product_scene_dict(d)
     img, _ = hostemu.render(sc)
-    monkeypatch.setenv("RTX_BINS", "0")
+    monkeypatch.setattr(OPTS, "bins", "0")
     walk, _ = hostemu.render(sc)
-    monkeypatch.delenv("RTX_BINS")
+    monkeypatch.setattr(OPTS, "bins", "1")
     assert np.array_equal(img, walk)
     if seed % 4 == 0:
         assert_parity(img, oracle_render_dict(d, noise=_lens_noise(sc)), "lens bins seed %d" % seed)
@@ -581,8 +582,8 @@ def test_hostemu_many_roots_bins_and_grids(seed, monkeypatch):
     assert hostemu.bins(sc, roots=True) is not None
     img, _ = hostemu.render(sc)
     split, _ = hostemu.render_split(sc)
-    monkeypatch.setenv("RTX_BINS", "0")
-    monkeypatch.setenv("RTX_DSGRID", "0")
+    monkeypatch.setattr(OPTS, "bins", "0")
+    monkeypatch.setattr(OPTS, "dsgrid", "0")
     walk, _ = hostemu.render(product_scene_dict(d))
     assert np.array_equal(img, walk) and np.array_equal(split, walk)
     assert_parity(img, oracle_render_dict(d, noise=_lens_noise(sc)), "many roots seed %d" % seed)
@@ -670,7 +671,7 @@ def _check_dir_shadow_grid(d, p, what):
 def test_hostemu_dir_shadow_grids_hold_every_ray(seed, monkeypatch):
     """Directional shadow grids, ray by ray, on spheres and boxes (static and moving; a
     grid for every scene, however few its spheres)."""
-    monkeypatch.setenv("RTX_DSGRID_MIN", "1")
+    monkeypatch.setattr(OPTS, "dsgrid_min", "1")
     from scenegen import shadow_scene
     d = shadow_scene(seed)
     p = _shadow_probe_points(d, np.random.RandomState(seed))
@@ -682,7 +683,7 @@ def test_hostemu_dir_shadow_grids_hold_every_ray_hierarchies(seed, monkeypatch):
     """Directional shadow grids, ray by ray, on hierarchy roots (their shadow boxes):
     random CSG trees under diagonal, vertical and random directional lights."""
     from scenegen import random_hier_scene
-    monkeypatch.setenv("RTX_DSGRID_MIN", "1")
+    monkeypatch.setattr(OPTS, "dsgrid_min", "1")
     d = random_hier_scene(seed)
     d["objects"] = [o for o in d["objects"] if "ref" not in o]  # (a copy needs its source in the scene)
     d["lights"] = [{"name": "d%d" % k, "type": "directional", "direction": v, "colour": [1.0, 1.0, 1.0], "power": 0.5}
@@ -872,7 +873,7 @@ def test_hostemu_dir_shadow_grids_skip_most_rays(monkeypatch):
     rng = np.random.RandomState(1)
     p = np.c_[rng.uniform(-6, 6, (4000, 1)), np.zeros((4000, 1)), rng.uniform(-8, 3, (4000, 1))].astype(np.float32)
     assert hostemu.dir_shadow_mask(product_scene("MirrorRefraction", (8, 8)), p, 0) is None
-    monkeypatch.setenv("RTX_DSGRID_MIN", "1")
+    monkeypatch.setattr(OPTS, "dsgrid_min", "1")
     for name in ("DepthOfField", "MirrorRefraction"):
         m = hostemu.dir_shadow_mask(product_scene(name, (8, 8)), p, 0)
         assert m is not None
@@ -884,12 +885,12 @@ def test_hostemu_dir_shadow_grids_equal_walk(seed, monkeypatch):
     """Frames with the directional shadow grids == without (RTX_DSGRID=0) == the oracle."""
     from common import oracle_render_dict, product_scene_dict
     from scenegen import shadow_scene
-    monkeypatch.setenv("RTX_DSGRID_MIN", "1")
+    monkeypatch.setattr(OPTS, "dsgrid_min", "1")
     d = shadow_scene(seed)
     img, cnt = hostemu.render(product_scene_dict(d))
-    monkeypatch.setenv("RTX_DSGRID", "0")
+    monkeypatch.setattr(OPTS, "dsgrid", "0")
     walk, cnt2 = hostemu.render(product_scene_dict(d))
-    monkeypatch.delenv("RTX_DSGRID")
+    monkeypatch.setattr(OPTS, "dsgrid", "1")
     assert np.array_equal(img, walk)
     assert np.array_equal(cnt, cnt2)
     assert_parity(img, oracle_render_dict(d), "shadow grids seed %d" % seed)

@@ -1,9 +1,13 @@
 #!/bin/bash
 # Frame time per scene-specialized kernel variant without rebuilding the library:
-# VARIANTS="name=flags;name=flags" (flags go to RTX_JIT_FLAGS, e.g. "-URTX_ABLATE
-# -DRTX_ABLATE=1"); CONFIGS as bench.py names them.
+# VARIANTS="name=flags;name=flags" (flags go to the jit_flags option, RTX_JIT_FLAGS, e.g.
+# "-URTX_ABLATE -DRTX_ABLATE=1"); CONFIGS as bench.py names them. Cost probes (RTX_ABLATE)
+# exist only in a tools build of the library: TOOLS_LIB (default _abl/librtx_tools.so,
+# built by `tools/build_lib_variant.sh tools -DRTX_TOOLS_BUILD`) is used when present.
 set -u
 mkdir -p gpurun_out/abj
+TL=${TOOLS_LIB:-_abl/librtx_tools.so}
+[ -f "$TL" ] && export RTX_LIB_OVERRIDE=$PWD/$TL
 IFS=';' read -ra VS <<< "${VARIANTS:-base=}"
 for c in ${CONFIGS:-tsp1080 tm1080}; do
   st=50; [ $c = dof4k ] && st=10

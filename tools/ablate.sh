@@ -13,7 +13,7 @@ mkdir -p "$OUT" "$ABL_DIR"
 # FLAGS_<name>=none: the built library as is; JFLAGS_<name>: extra flags for the
 # scene-specialized (hiprtc) kernels
 for n in ${VARIANTS:-0 1 2 3}; do
-  fl_var="FLAGS_$n"; fl="${!fl_var:--DRTX_ABLATE=$n}"
+  fl_var="FLAGS_$n"; fl="${!fl_var:--DRTX_TOOLS_BUILD -DRTX_ABLATE=$n}"
   if [ "$fl" = "none" ]; then cp python-raytracer_amd/rtx/_lib/librtx.so "$ABL_DIR/librtx_$n.so"; continue; fi
   if [ -n "${PREBUILT:-}" ] && [ -f "$ABL_DIR/librtx_$n.so" ]; then continue; fi
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared $fl \

@@ -5,7 +5,7 @@ rtx_api.hip's jit_spec (tests/native/librtx_hostemu.so) for a bench.py config.
 
 usage: python tools/jit_offline.py LOG KERNEL OUT.s [extra hipcc flags...]
        python tools/jit_offline.py --config tsp1080 [--rgb8] OUT.s [extra hipcc flags...]
-Environment variables that change the specialization (RTX_PERSIST, RTX_JIT_FLAGS, ...)
+Environment variables that change the specialization (RTX_JIT_FLAGS, RTX_BINS, ...)
 apply in the --config form as they would on the box."""
 import ctypes as C
 import os

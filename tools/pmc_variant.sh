@@ -6,7 +6,7 @@ OUT=gpurun_out/${TAG:-pmcv}
 mkdir -p "$OUT" /tmp/rtx_ablate
 export TMPDIR=/tmp
 for n in ${VARIANTS:-0}; do
-  fl_var="FLAGS_$n"; fl="${!fl_var:--DRTX_ABLATE=$n}"
+  fl_var="FLAGS_$n"; fl="${!fl_var:--DRTX_TOOLS_BUILD -DRTX_ABLATE=$n}"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared $fl \
     -o /tmp/rtx_ablate/librtx_$n.so python-raytracer_amd/csrc/rtx_api.hip python-raytracer_amd/csrc/rtx_kern_ext_m0.hip python-raytracer_amd/csrc/rtx_kern_ext_m1.hip -lhiprtc || exit 1
   RTX_LIB_OVERRIDE=/tmp/rtx_ablate/librtx_$n.so timeout -k 10 240 rocprofv3 --kernel-trace \
