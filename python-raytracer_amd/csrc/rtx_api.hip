@@ -2113,8 +2113,8 @@ struct CamStage {
     std::vector<char> b;
     size_t put(const void* p, size_t n) {
         const size_t off = (b.size() + 255) & ~(size_t)255;
-        b.resize(off + std::max<size_t>(n, 4));
-        if (n) memcpy(b.data() + off, p, n);
+        b.resize(off + std::max<size_t>(n, 4));  // (zero-filled; p == nullptr: only reserve)
+        if (n && p) memcpy(b.data() + off, p, n);
         return off;
     }
     template <class T>

@@ -14,6 +14,7 @@ import torch  # noqa: F401  (loads the process' HIP runtime before librtx.so)
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_lib", "librtx.so")
 # Experiment builds (tools/ablate.sh) point this at another build of the same HIP source.
+_BUILT_PATH = LIB_PATH
 LIB_PATH = os.environ.get("RTX_LIB_OVERRIDE", LIB_PATH)
 ABI_VERSION = 5
 
@@ -120,6 +121,8 @@ def load():
         lib.rtx_occluded.argtypes = [vp, C.c_int64, vp, vp, vp, C.c_double, vp, vp]
         lib.rtx_fb_to_rgb8.argtypes = [vp, vp, C.c_int64, vp]
         for fn in EXPORTS:  # every status-returning entry point (not the string / count ones)
+            if not hasattr(lib, fn):
+                continue  # (an earlier round's library, see below)
             if fn not in ("rtx_abi_version", "rtx_last_error", "rtx_last_kernel", "rtx_group_rows", "rtx_jit_modules",
                           "rtx_option_name"):
                 getattr(lib, fn).restype = C.c_int
@@ -127,13 +130,17 @@ def load():
         lib.rtx_last_kernel.restype = C.c_char_p
         lib.rtx_jit_modules.argtypes = []
         lib.rtx_jit_modules.restype = C.c_int32
-        lib.rtx_set_option.argtypes = [C.c_char_p, C.c_char_p]
-        lib.rtx_get_option.argtypes = [C.c_char_p, C.c_char_p, C.c_int32]
-        lib.rtx_option_name.argtypes = [C.c_int32]
-        lib.rtx_option_name.restype = C.c_char_p
         v = lib.rtx_abi_version()
-        if v != ABI_VERSION:
+        # (tools/ab_lib.sh times an earlier round's library through RTX_LIB_OVERRIDE: ABI 4
+        # lacks only the options, which the render calls do not use)
+        older = v == 4 and LIB_PATH != _BUILT_PATH
+        if v != ABI_VERSION and not older:
             raise RuntimeError("librtx.so ABI %d != binding ABI %d" % (v, ABI_VERSION))
+        if not older:
+            lib.rtx_set_option.argtypes = [C.c_char_p, C.c_char_p]
+            lib.rtx_get_option.argtypes = [C.c_char_p, C.c_char_p, C.c_int32]
+            lib.rtx_option_name.argtypes = [C.c_int32]
+            lib.rtx_option_name.restype = C.c_char_p
         _lib = lib
         return lib
 
