@@ -13,6 +13,7 @@
 #include <hip/hiprtc.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -70,7 +71,7 @@ int fail(int code, const std::string& msg) {
 enum Opt {
     OPT_SPLIT, OPT_SPLIT_BYTES, OPT_SPLIT_RATIO, OPT_BINS, OPT_LENS_BINS, OPT_LGRID, OPT_DSGRID, OPT_DSGRID_MIN,
     OPT_SELF_SKIP, OPT_TILE_SCHED, OPT_PRIM_ORIGIN, OPT_SPP, OPT_SPP_MIN, OPT_JIT, OPT_JIT_BAKE, OPT_JIT_EXT,
-    OPT_JIT_DUMP, OPT_JIT_IDLE_BAKED, OPT_JIT_DISK_BAKED, OPT_JIT_CACHE, OPT_JIT_FLAGS, OPT_COUNT
+    OPT_JIT_DUMP, OPT_JIT_IDLE_BAKED, OPT_JIT_DISK_BAKED, OPT_JIT_CACHE, OPT_JIT_FLAGS, OPT_SETUP_LOG, OPT_COUNT
 };
 struct OptDef {
     const char* name;
@@ -99,6 +100,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"jit_disk_baked", 64, false},            // baked code objects kept in the disk cache
     {"jit_cache", 0, true},                   // code-object cache directory ("" = /tmp/rtx_jit_<uid>)
     {"jit_flags", 0, true},                   // extra hiprtc options (part of the cache key)
+    {"setup_log", 0, false},                  // print the host time of each rtx_camera_set step
 };
 struct OptVal {
     double v;
@@ -2108,6 +2110,27 @@ void free_scene(rtx_scene* s) {
 }  // namespace
 
 namespace {
+// Option setup_log: the host time of each step of a setup call, printed to stderr.
+struct SetupLog {
+    const char* what;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), t = t0;
+    std::string line;
+    explicit SetupLog(const char* w) : what(w) {}
+    void mark(const char* step) {
+        if (!opt_on(OPT_SETUP_LOG)) return;
+        const auto n = std::chrono::steady_clock::now();
+        char buf[96];
+        snprintf(buf, sizeof(buf), " %s %.3f", step, std::chrono::duration<double, std::milli>(n - t).count());
+        line += buf;
+        t = n;
+    }
+    ~SetupLog() {
+        if (opt_on(OPT_SETUP_LOG) && !line.empty())
+            fprintf(stderr, "librtx: %s ms:%s (total %.3f)\n", what, line.c_str(),
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+};
+
 // Host staging of the camera tables: 256-byte aligned segments of one buffer.
 struct CamStage {
     std::vector<char> b;
@@ -2279,6 +2302,7 @@ int rtx_scene_destroy(rtx_scene* s) {
 
 int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     if (!s) return fail(RTX_ERR_INVALID, "rtx_camera_set: null scene");
+    SetupLog slog("rtx_camera_set");
     KParams k;
     int rc = convert_camera(c, k);
     if (rc) return rc;
@@ -2289,6 +2313,7 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     const auto mm = std::minmax_element(times.begin(), times.end());
     const double omax = camera_origin_bound(c);
     k.S = s->view;
+    slog.mark("convert");
     // what depends on the frame's time range only: computed again when it changes
     const bool dsg_off = !opt_on(OPT_DSGRID);  // every shadow ray tests every object
     if (!s->tr_valid || s->tr_lo != *mm.first || s->tr_hi != *mm.second || s->tr_dsg_off != dsg_off) {
@@ -2308,6 +2333,7 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
         s->tr_lo = *mm.first;
         s->tr_hi = *mm.second;
     }
+    slog.mark("time-range grids");
     CamStage st;
     const size_t o_xs = st.put(c->xs, sizeof(float) * c->ncols), o_ys = st.put(c->ys, sizeof(float) * c->height);
     const size_t o_dof = st.put(c->dof_origins, sizeof(float) * 3 * c->n_dof);
@@ -2317,6 +2343,7 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     size_t o_tperm = 0, o_ttime = 0;
     const bool replay = c->jitter == RTX_JITTER_REPLAY;
     if (replay) o_noise = st.put(c->noise, sizeof(float) * 3 * (size_t)c->ncols * c->height * nsamp);
+    slog.mark("tables");
     if (!s->h_nodes.empty()) o_bounds = st.put(split_bounds(s->tr_bounds));
     // self tests of planes (option self_skip 0: none). Scenes with secondary rays get none:
     // MirrorRefraction measured 1.4 % slower with them (most of its shadow rays leave
@@ -2329,6 +2356,7 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
         dir_self_boxes(s->h_bins, grids, omax);
         o_dsg = st.put(grids);
     }
+    slog.mark("self tests");
     std::vector<int32_t> bstart, bfaces;
     std::vector<float> bz;
     std::vector<uint32_t> bmask, brmask;
@@ -2343,6 +2371,7 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
         o_bz = st.put(bz);
         o_bmask = st.put(bmask);
     }
+    slog.mark("bins");
     // the measured tile schedule (tile_schedule): identity order until measured
     const bool tsched = tile_sched_enabled() && !s->has_ext && (s->has_secondary || s->has_mesh);
     int64_t tiles = 0;
@@ -2356,6 +2385,7 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
         o_ttime = st.put(std::vector<uint32_t>((size_t)nw, 0u));
     }
     const size_t o_kp = st.put(nullptr, sizeof(KParams));
+    slog.mark("tile schedule");
     // one device buffer for all of it, reused while large enough; its old contents may still
     // be read by frames of the previous camera
     (void)hipDeviceSynchronize();
@@ -2368,6 +2398,7 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
         s->cam_cap = cap;
     }
     char* const D = s->d_cam;
+    slog.mark("sync+alloc");
     k.xs = (cptr<float>)(D + o_xs);
     k.ys = (cptr<float>)(D + o_ys);
     k.dof_o = (cptr<float>)(D + o_dof);
@@ -2426,6 +2457,7 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     }
     memcpy(st.b.data() + o_kp, &k, sizeof(KParams));
     RTX_HIP(hipMemcpy(D, st.b.data(), st.b.size(), hipMemcpyHostToDevice));
+    slog.mark("upload");
     s->d_kp = reinterpret_cast<KParams*>(D + o_kp);
     s->kp = k;
     s->cam_set = true;

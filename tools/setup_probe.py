@@ -1,6 +1,8 @@
 """Setup cost of a render (outside bench.py's timed region), each step three times:
 host parse, rtx_scene_create, rtx_camera_set and the first frame, with a cold on-disk JIT
-cache (a fresh RTX_JIT_CACHE directory) and then warm. usage: python tools/setup_probe.py [config]"""
+cache (a fresh RTX_JIT_CACHE directory) and then warm; then five camera moves of one scene
+(rtx_camera_set per move). The library prints each camera upload's steps (option setup_log).
+usage: python tools/setup_probe.py [config]"""
 import json
 import os
 import sys
@@ -25,6 +27,8 @@ def main():
     cfg = sys.argv[1] if len(sys.argv) > 1 else "tsp1080"
     torch.cuda.set_device(0)
     torch.zeros(1, device="cuda")
+    import rtx
+    rtx.set_option("setup_log", 1)
     rows = []
     for rep in range(3):
         t = time.perf_counter()
@@ -46,7 +50,17 @@ def main():
         rows.append({"rep": rep, "parse_ms": parse, "scene_create_ms": create, "camera_set_ms": cam,
                      "first_frame_ms": first, "next_frame_ms": second, "kernel": sc.last_kernel})
         sc.invalidate()
-    print(json.dumps({"config": cfg, "runs": rows}))
+    moves = []
+    sc = bench.make_scene(cfg)
+    fb = torch.empty((sc.vc.height, sc.vc.width, 3), dtype=torch.float32, device="cuda")
+    sc.render_device(out=fb)
+    p0 = [float(x) for x in sc.vc.position]
+    for k in range(5):
+        sc.vc.position = [p0[0] + 0.01 * (k + 1), p0[1], p0[2]]
+        t = time.perf_counter()
+        sc._set_camera(0, 1)
+        moves.append(ms(t))
+    print(json.dumps({"config": cfg, "runs": rows, "camera_moves_ms": moves}))
 
 
 if __name__ == "__main__":
