@@ -69,7 +69,7 @@ int fail(int code, const std::string& msg) {
 // read where the library decides (per render or per camera upload). Set them before
 // rendering; they are not synchronised with renders running on other threads.
 enum Opt {
-    OPT_SPLIT, OPT_SPLIT_BYTES, OPT_SPLIT_RATIO, OPT_BINS, OPT_LENS_BINS, OPT_LGRID, OPT_DSGRID, OPT_DSGRID_MIN,
+    OPT_SPLIT, OPT_SPLIT_BYTES, OPT_SPLIT_RATIO, OPT_BINS, OPT_HEAVY_TILES, OPT_LENS_BINS, OPT_LGRID, OPT_DSGRID, OPT_DSGRID_MIN,
     OPT_SELF_SKIP, OPT_TILE_SCHED, OPT_PRIM_ORIGIN, OPT_SPP, OPT_SPP_MIN, OPT_JIT, OPT_JIT_BAKE, OPT_JIT_EXT,
     OPT_JIT_DUMP, OPT_JIT_IDLE_BAKED, OPT_JIT_DISK_BAKED, OPT_JIT_CACHE, OPT_JIT_FLAGS, OPT_SETUP_LOG, OPT_COUNT
 };
@@ -83,6 +83,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"split_bytes", 2147483648.0, false},     // record bytes of one split chunk
     {"split_ratio", -1, false},               // >= 0: fixed deeper records per sample (else learned)
     {"bins", 1, false},                       // primary-ray bins (0: every primary ray walks everything)
+    {"heavy_tiles", 1, false},                // long bin face lists tested in chunks by a pass of their own
     {"lens_bins", 1, false},                  // bins for lens cameras too
     {"lgrid", 1, false},                      // light grids of point lights (mesh shadow rays)
     {"dsgrid", 1, false},                     // shadow grids of directional lights
@@ -1351,6 +1352,28 @@ bool light_grids(const HostScene& H, std::vector<DLGrid>& grids, std::vector<int
     return any;
 }
 
+
+// Heavy tiles of the primary-ray face bins (SceneView::bin_heavy): a bin whose list holds
+// more than kHeavyChunk faces is split into chunks of kHeavyChunk consecutive entries, each
+// tested by one wave of k_mesh_chunks; the bin's chunks are numbered consecutively.
+// Measured on the 81,920-face mesh at 1080p: the silhouette tiles' lists (up to ~770 faces,
+// where lanes that miss the mesh keep the early exit from firing) were tested one face at
+// a time by one wave and set the frame's length. Returns false when no bin is heavy.
+bool heavy_chunks(const std::vector<int32_t>& bstart, std::vector<int32_t>& bheavy, std::vector<int2>& items) {
+    bheavy.clear();
+    items.clear();
+    if (bstart.size() < 2) return false;
+    const size_t nb = bstart.size() - 1;
+    bheavy.assign(nb, -1);
+    for (size_t b = 0; b < nb; ++b) {
+        const int32_t len = bstart[b + 1] - bstart[b];
+        if (len <= kHeavyChunk) continue;
+        bheavy[b] = (int32_t)items.size();  // (items in bin order: a bin's chunks are consecutive)
+        for (int32_t c = 0; c * kHeavyChunk < len; ++c) items.push_back(make_int2((int32_t)b, c));
+    }
+    return !items.empty();
+}
+
 // Shadow grids of directional lights (DSGrid, rtx_trace.h), per camera (the motion-time
 // range [tlo, thi] of the frame bounds the moving objects). Light li's shadow ray from p is
 // the half-line p + t d (d = fl32 -direction, LIGHT.negvec; t > 1e-4 or 1e-3). On two
@@ -2040,6 +2063,11 @@ struct rtx_scene {
     // 4 measured and left in row-major order
     void* d_tile_perm = nullptr;
     void* d_tile_time = nullptr;
+    // heavy tiles of the primary-ray bins (heavy_chunks): chunk items and their per-frame
+    // closest faces, inside d_cam; heavy_n chunks (0: none)
+    const int2* d_heavy_items = nullptr;
+    uint2* d_mesh_hits = nullptr;
+    int32_t heavy_n = 0;
     int tile_sched = 0;
     hipEvent_t tile_event = nullptr;  // recorded after the measuring launch
     // the split hierarchy passes (rtx_split.h, render_split): the record arrays of one
@@ -2371,6 +2399,15 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
         o_bz = st.put(bz);
         o_bmask = st.put(bmask);
     }
+    std::vector<int32_t> bheavy;
+    std::vector<int2> hitems;
+    size_t o_bheavy = 0, o_hitems = 0, o_mhits = 0;
+    const bool heavy = bins && mesh_bins && !s->has_ext && opt_on(OPT_HEAVY_TILES) && heavy_chunks(bstart, bheavy, hitems);
+    if (heavy) {
+        o_bheavy = st.put(bheavy);
+        o_hitems = st.put(hitems);
+        o_mhits = st.put(nullptr, sizeof(uint2) * 64 * hitems.size());
+    }
     slog.mark("bins");
     // the measured tile schedule (tile_schedule): identity order until measured
     const bool tsched = tile_sched_enabled() && !s->has_ext && (s->has_secondary || s->has_mesh);
@@ -2421,6 +2458,16 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
         k.S.bin_zmin = (cptr<float>)(D + o_bz);
         k.S.bins_x = bins_x;
         k.S.bins_on = 1;
+    }
+    s->heavy_n = 0;
+    s->d_heavy_items = nullptr;
+    s->d_mesh_hits = nullptr;
+    if (heavy) {
+        k.S.bin_heavy = (cptr<int32_t>)(D + o_bheavy);
+        k.S.mesh_hits = reinterpret_cast<const uint2*>(D + o_mhits);
+        s->d_heavy_items = reinterpret_cast<const int2*>(D + o_hitems);
+        s->d_mesh_hits = reinterpret_cast<uint2*>(D + o_mhits);
+        s->heavy_n = (int32_t)hitems.size();
     }
 #if defined(RTX_WAVE_LOG)  // tools/wave_timeline.py builds only
     if (const char* e = getenv("RTX_WAVE_LOG_PTR"))
@@ -2798,6 +2845,16 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
         L.tlog = 0;
         L.redo = RedoList{nullptr, nullptr, nullptr};
     }
+    // the heavy tiles' chunks of every frame of a tile-mapped launch, just before it (the
+    // sample-parallel and split kernels pass no pixel-in-tile and walk the lists)
+    auto heavy_pass = [&](bool tiles) -> int {
+        if (s->heavy_n <= 0 || !tiles || s->has_ext) return RTX_OK;
+        for (int32_t f = 0; f < nframes; ++f)
+            hipLaunchKernelGGL(k_mesh_chunks, dim3((unsigned)((s->heavy_n + 3) / 4)), dim3(256), 0, st, kp, L,
+                               s->d_heavy_items, s->heavy_n, s->d_mesh_hits);
+        RTX_HIP(hipGetLastError());
+        return RTX_OK;
+    };
     rtx_scene::Resolved& rs = s->resolved[(out8 ? 8 : 0) | (cnt ? 4 : 0) | (jit ? 2 : 0) | (spp_mode ? 1 : 0)];
     if (!rs.done) {
         rs.fn = jit_render_kernel(s->device, s->view, s->kp, s->traits, s->has_mesh, s->has_secondary, s->has_ext,
@@ -2817,6 +2874,7 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
             L.tlog = s->tile_sched == 1;
         }
         if (whole) L.tperm = s->tile_sched == 3;
+        if (int rc = heavy_pass(!spp_mode)) return rc;
         RTX_HIP(hipModuleLaunchKernel(rs.fn, (unsigned)nblocks, (unsigned)nframes, 1, blk, 1, 1,
                                       s->has_ext ? (unsigned)(hbytes * blk) : 0u, st, args, nullptr));
         if (L.tlog) {  // measured: sorted before the next whole frame
@@ -2872,6 +2930,7 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
     // the flat-scene kernels use the tile mapping here (their sample-parallel variants
     // are reached through the scene-specialized kernels only)
     if (spp_mode) nblocks = blocks(false);
+    if (int rc = heavy_pass(true)) return rc;
 #define RTX_LAUNCH(M, S, C, J) \
     hipLaunchKernelGGL((k_render<M, S, false, C, J>), dim3((unsigned)nblocks, (unsigned)nframes), dim3(kBlock<false>), \
                        0, st, kp, L)

@@ -226,6 +226,7 @@ RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, 
         return;
     }
     const int j = P.height - 1 - (row0 + rr);  // reference row index (y grows upward)
+    const int32_t blane = bin >= 0 ? (((row0 + rr) & 7) << 3) | (cc & 7) : -1;  // the pixel in its tile
 #if defined(RTX_PRIM_ORIGIN) && RTX_PRIM_ORIGIN && defined(RTX_FIXED_COUNTS)
     OriginTerms prim;  // the primary rays' origin-only terms (host-computed)
 #pragma unroll
@@ -269,7 +270,7 @@ RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, 
 #pragma unroll 1
             for (int kt = 0; kt < RTX_NTIMES(P); ++kt)
                 colour = add(colour, cast_ray<MESH, SEC, X, COUNT>(sample_scene<X>(P.S), o, ddir, P.times[kt], tl, fs, hs,
-                                                                   bin, primp));
+                                                                   bin, primp, blane));
         }
     }
     colour = mk(sample_mean(P, colour.x), sample_mean(P, colour.y), sample_mean(P, colour.z));
@@ -287,6 +288,41 @@ RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, 
     put_channel(fb, 3 * p, colour.x);
     put_channel(fb, 3 * p + 1, colour.y);
     put_channel(fb, 3 * p + 2, colour.z);
+}
+
+// Chunk c of a heavy tile's primary-ray face list (SceneView::bin_heavy): for the tile's
+// pixel `lane` (row * 8 + column of its 8x8 tile), the closest of the chunk's faces by
+// closest_hit's tests -- the face's padded box, then the exact test, offered to the same
+// total order -- as (t32 bits, stored face or -1). The primary ray is render_pixel's of a
+// one-sample pinhole camera (the bins' cameras): aa_o[0] toward the pixel's focal point.
+// Every lane of a wave calls it for the same chunk (the loop's votes are the wave's).
+// (Starting chunks c >= 1 from chunk 0's closest face, in a second launch after it,
+// measured slower: blob 1080p 0.275 -> 0.291 ms.)
+RTX_HD uint2 mesh_chunk(const KParams& P, int32_t bin, int32_t c, int lane) {
+    const SceneView& S = P.S;
+    const int32_t ty = bin / S.bins_x, tx = bin - ty * S.bins_x;
+    const int32_t row = ty * 8 + (lane >> 3), cc = tx * 8 + (lane & 7);
+    const bool active = row < P.height && cc < P.ncols;
+    const int j = P.height - 1 - (active ? row : 0);
+    const f3 d = normalize(sub(pixel_focal(P, active ? cc : 0, j), ld3(P.dof_o)));  // scene.py:58
+    const f3 o = ld3(P.aa_o);  // scene.py:60-61 (one sample, no jitter)
+    const int32_t oi = S.n_plane + S.n_sphere + S.n_box;  // the scene's one top-level mesh
+    const DObj ob = S.objs[oi];
+    const float time = P.times[0];
+    const RayInv ri = ray_inv(o, d);
+    Hit h{INFINITY, -1, 0};
+    const int32_t q0 = S.bin_start[bin] + c * kHeavyChunk;
+    const int32_t q1 = min(S.bin_start[bin + 1], q0 + kHeavyChunk);
+    for (int32_t q = q0; q < q1; ++q) {
+        if (RTX_ALL(!active || h.t32 < S.bin_zmin[q])) break;  // nearest first (closest_hit's exit)
+        const int32_t f = S.bin_faces[q];
+        const bool fmaybe = active && leaf_maybe_hit(RTX_FBOX(S, ob.tri_begin + f), o, ri, ob.cmax, h.t32);
+        if (!RTX_ANY(fmaybe)) continue;
+        float t32;
+        const bool valid = tri_hit(RTX_TRI(S, ob.tri_begin + f), o, d, fmaybe, t32);
+        offer(S, h, valid, t32, oi, f, o, d, time);
+    }
+    return make_uint2(__builtin_bit_cast(uint32_t, h.t32), h.obj >= 0 ? (uint32_t)h.sub : 0xFFFFFFFFu);
 }
 
 // Blocks of a split chunk to render again in the one-kernel form (rtx_split.h): n == nullptr
@@ -682,6 +718,22 @@ __global__ __launch_bounds__(256) void k_occluded(SceneView S, int64_t n, const 
 }
 
 #if !defined(RTX_EXT_TU)  // defined once, in rtx_api.hip
+// The heavy tiles' chunks of this frame (one wave per chunk, 4 per block), before the render
+// kernel: items (bin, chunk). A launch of rows (row0, nrows) or 8-row groups
+// (gphase + k gstride) runs only the chunks of its tiles.
+__global__ __launch_bounds__(256) void k_mesh_chunks(const KParams* __restrict__ Pp, const Launch L,
+                                                     const int2* __restrict__ items, int32_t n, uint2* __restrict__ out) {
+    const int32_t w = __builtin_amdgcn_readfirstlane((int32_t)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    if (w >= n) return;
+    const int2 it = items[w];
+    const int32_t ty = it.x / Pp->S.bins_x;  // the tile's 8-row group
+    const bool mine = L.gstride > 0 ? (ty >= L.gphase && (ty - L.gphase) % L.gstride == 0)
+                                    : (ty * 8 + 8 > L.row0 && ty * 8 < L.row0 + L.nrows);
+    if (!mine) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t slot = Pp->S.bin_heavy[it.x];
+    out[(slot + it.y) * 64 + lane] = mesh_chunk(*Pp, it.x, it.y, lane);
+}
 // (v * 255.0) truncated to uint8, four values per thread: one 16-byte load and one 4-byte
 // store (fb 16-byte and out 4-byte aligned; rtx_fb_to_rgb8 checks), the tail one by one.
 __device__ __forceinline__ uint8_t to_u8(float v) { return (uint8_t)(int)((double)v * 255.0); }

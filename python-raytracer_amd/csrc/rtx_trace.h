@@ -37,6 +37,7 @@ using __hip_internal::uint64_t;
 namespace rtx {
 
 constexpr int kMaxDepth = 10;  // cast_ray(max_recursion=10) (scene.py:81)
+constexpr int kHeavyChunk = 32;  // faces per chunk of a heavy tile's primary-ray list (SceneView::bin_heavy)
 
 // Cost probes (tools/ablate.sh, tools/ab_jitflags.sh): a tools build of the library
 // (-DRTX_TOOLS_BUILD, tools/build_lib_variant.sh) compiles kernels with -DRTX_ABLATE=n that
@@ -332,6 +333,15 @@ struct SceneView {
     cptr<uint32_t> bin_objmask;      // per bin: spheres (bits 0-15) and boxes (16-31) a ray may hit
     cptr<uint32_t> bin_rootmask;     // per bin: hierarchy roots (bit q: the q-th; later ones always)
     int32_t bins_x, bins_on, mesh_bins, pad5;
+    // Heavy tiles (rtx_api.hip heavy_chunks): a bin whose face list is longer than
+    // kHeavyChunk faces is tested in chunks of kHeavyChunk faces by a pass of its own
+    // (k_mesh_chunks, one wave per chunk, before the render kernel of each frame), which
+    // leaves per chunk and pixel of the tile the chunk's closest face; the render kernel
+    // then offers those instead of walking the list. bin_heavy[b]: the bin's first chunk
+    // (its chunks are consecutive), or -1. mesh_hits: [chunk][64 pixels of the 8x8 tile]
+    // (t32 bits, stored face or -1). null: no heavy tiles.
+    cptr<int32_t> bin_heavy;
+    const uint2* mesh_hits;
     int32_t n_objs_all, n_mats, pad6, pad7;  // object records (incl. hierarchy leaves), materials
     // Light grids (per light; shadow rays of point lights against the scene's one mesh)
     cptr<DLGrid> lgrid;
@@ -1728,8 +1738,9 @@ template <bool MESH, bool X, bool COUNT>
 // prim (primary rays of one-sample unjittered static cameras, RTX_PRIM_ORIGIN): the
 // origin-only terms of the planes and spheres, computed once on the host (rtx_camera_set,
 // the same fp32 operations) instead of in every wave.
+// blane: with bin, the ray's pixel in the bin's 8x8 tile (row * 8 + column), or -1.
 RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const HStack& hs, HHit& hh,
-                       int32_t bin = -1, const OriginTerms* prim = nullptr) {
+                       int32_t bin = -1, const OriginTerms* prim = nullptr, int32_t blane = -1) {
     Hit h{INFINITY, -1, 0};
     int oi = 0;
     for (int k = 0; k < RTX_NPLANE(S); ++k, ++oi) {  // simple_geometry.py:105-120
@@ -1836,6 +1847,17 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
             if (bin >= 0 && S.mesh_bins && k == 0) {  // a primary ray: its tile's candidate faces
                 const int32_t ub = wave_uniform(bin);  // the same in every lane of the tile's wave
                 const int32_t q1 = S.bin_start[ub + 1];
+                // a heavy tile: its chunks' closest faces, found by k_mesh_chunks this frame
+                // (the same tests; the closest over the chunks is the closest over the list)
+                const int32_t slot = (S.bin_heavy != nullptr && blane >= 0) ? S.bin_heavy[ub] : -1;
+                if (slot >= 0) {
+                    const int32_t nch = (q1 - S.bin_start[ub] + kHeavyChunk - 1) / kHeavyChunk;
+                    for (int32_t c = 0; c < nch; ++c) {
+                        const uint2 e = S.mesh_hits[(int64_t)(slot + c) * 64 + blane];
+                        offer(S, h, (int32_t)e.y >= 0, __builtin_bit_cast(float, e.x), oi, (int32_t)e.y, o, d, time);
+                    }
+                    continue;
+                }
                 for (int32_t q = S.bin_start[ub]; q < q1; ++q) {
                     // faces come nearest first: once every lane's best hit precedes a
                     // face's nearest possible t, no later face can win (or tie)
@@ -2369,7 +2391,7 @@ struct FrameStack {
 
 template <bool MESH, bool SEC, bool X, bool COUNT>
 RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const FrameStack& fs, const HStack& hs,
-                   int32_t bin = -1, const OriginTerms* prim = nullptr) {
+                   int32_t bin = -1, const OriginTerms* prim = nullptr, int32_t blane = -1) {
     int nfr = 0;
     uint64_t fmats = 0;  // RTX_FRAME_MATBITS: the frames' material indices
     f3 deep[kMaxDepth - kFrameLds > 0 ? kMaxDepth - kFrameLds : 1];  // frames kFrameLds.. (private)
@@ -2381,7 +2403,7 @@ RTX_HD f3 cast_ray(const SceneView& S, f3 o, f3 d, float time, Tally& tl, const 
         if (RTX_PROBE(8)) { tail = d; break; }  // cost probe: camera + store only
         HHit hh;
         const Hit h = closest_hit<MESH, X, COUNT>(S, o, d, time, tl, hs, hh, level == 0 ? bin : -1,
-                                                  level == 0 ? prim : nullptr);
+                                                  level == 0 ? prim : nullptr, blane);
         if (h.obj == -1) break;  // miss -> black
         const Surface sf = resolve_hit<MESH, X>(S, h, hh, o, d, time);
         const DMat m = RTX_MAT(S, sf.mat);

@@ -93,6 +93,24 @@ struct DirGrids {
     }
 };
 
+// The heavy tiles' chunks (rtx_api.hip heavy_chunks, rtx_kernels.h mesh_chunk), as the
+// k_mesh_chunks pass computes them before each frame, for every chunk and pixel.
+struct Heavy {
+    std::vector<int32_t> bheavy;
+    std::vector<int2> items;
+    std::vector<uint2> hits;
+    void bind(const HostScene& H, KParams& k, const std::vector<int32_t>& bstart) {
+        if (!k.S.bins_on || !k.S.mesh_bins || H.has_ext || !heavy_chunks(bstart, bheavy, items)) return;
+        hits.resize(items.size() * 64);
+        k.S.bin_heavy = (cptr<int32_t>)bheavy.data();
+#pragma omp parallel for schedule(dynamic, 4)
+        for (int64_t w = 0; w < (int64_t)items.size(); ++w)
+            for (int lane = 0; lane < 64; ++lane)
+                hits[(size_t)w * 64 + lane] = mesh_chunk(k, items[(size_t)w].x, items[(size_t)w].y, lane);
+        k.S.mesh_hits = hits.data();
+    }
+};
+
 // Dispatch over the kernel template flags, as rtx_render's launch switch does.
 template <bool MESH, bool SEC, bool X>
 void pixel_jit(const KParams& k, float* fb, int32_t row0, int32_t rr, int32_t cc, Tally& tl, const FrameStack& fs,
@@ -157,6 +175,8 @@ extern "C" int rtx_hostemu_render(const rtx_scene_desc* sd, const rtx_camera_des
     if (cd->jitter == RTX_JITTER_REPLAY) noise.assign(cd->noise, cd->noise + 3 * (size_t)cd->ncols * cd->height * nsamp);
     k.xs = (cptr<float>)cd->xs; k.ys = (cptr<float>)cd->ys; k.dof_o = (cptr<float>)cd->dof_origins;
     k.aa_o = (cptr<float>)cd->aa_origins; k.times = (cptr<float>)times.data(); k.noise = (cptr<float>)noise.data();
+    Heavy hv;
+    hv.bind(H, k, bstart);
     const int64_t npix = (int64_t)nrows * k.ncols;
     uint64_t tot[RTX_COUNTERS] = {};
 #pragma omp parallel num_threads(threads > 0 ? threads : 1)
@@ -225,6 +245,8 @@ extern "C" int rtx_hostemu_render_rows(const rtx_scene_desc* sd, const rtx_camer
     if (cd->jitter == RTX_JITTER_REPLAY) noise.assign(cd->noise, cd->noise + 3 * (size_t)cd->ncols * cd->height * nsamp);
     k.xs = (cptr<float>)cd->xs; k.ys = (cptr<float>)cd->ys; k.dof_o = (cptr<float>)cd->dof_origins;
     k.aa_o = (cptr<float>)cd->aa_origins; k.times = (cptr<float>)times.data(); k.noise = (cptr<float>)noise.data();
+    Heavy hv;
+    hv.bind(H, k, bstart);
     const int64_t npix = (int64_t)nrows * k.ncols;
 #pragma omp parallel for num_threads(threads > 0 ? threads : 1) schedule(dynamic, 64)
     for (int64_t p = 0; p < npix; ++p) {

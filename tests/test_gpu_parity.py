@@ -338,6 +338,38 @@ def test_large_mesh_bvh_matches_oracle(tmp_path, flat):
     assert s["frac_diff"] == 0.0, s
 
 
+def test_heavy_tiles_equal_walk(tmp_path, monkeypatch):
+    """Heavy primary-ray tiles (a bin's face list longer than kHeavyChunk faces, tested in
+    chunks by k_mesh_chunks before the render kernel, rtx_api.hip heavy_chunks): the
+    81,920-face mesh at 1920x1080 and 256x144 and TorusMesh at 64x64 (its bins are heavy
+    at that size) with and without them, bit for bit; the small frames also against the
+    oracle; groups of 8-row groups too (the pass runs only its launch's tiles)."""
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import blob_obj, blob_scene
+    from rtx.io import bundled_scene_dict
+    p = str(tmp_path / "blob6.obj")
+    blob_obj(p, level=6)
+    cases = [(blob_scene(p, (1920, 1080)), False), (blob_scene(p, (256, 144)), True),
+             (bundled_scene_dict("TorusMesh", resolution=(64, 64)), True)]
+    for d, small in cases:
+        d = {k: v for k, v in d.items() if k != "__base_dir__"}
+        sc = product_scene_dict(d)
+        a = sc.render_device().clone()
+        assert sc.last_kernel.startswith("rtx_jit_render_1"), sc.last_kernel
+        H = a.shape[0]
+        from rtx.scene import group_rows
+        for k in range(3):
+            part = sc.render_device(groups=(k, 3)).clone()
+            assert torch.equal(part, a[torch.as_tensor(group_rows(H, 3, k), device="cuda")])
+        monkeypatch.setattr(OPTS, "heavy_tiles", "0")
+        b = product_scene_dict(d).render_device().clone()
+        monkeypatch.setattr(OPTS, "heavy_tiles", "1")
+        assert torch.equal(a, b), float((a != b).float().mean())
+        if small:
+            img = np.ascontiguousarray(np.transpose(a.cpu().numpy()[::-1], (1, 0, 2))).astype(np.float64)
+            assert_parity(img, oracle_render_dict(d), "heavy tiles")
+
+
 @pytest.mark.parametrize("name,res,edits", [
     ("TwoSpheresPlane", (160, 90), {}), ("MirrorRefraction", (160, 90), {}), ("TorusMesh", (96, 96), {}),
     ("DepthOfField", (64, 48), {"AA": {"jitter": True, "samples": 2}}),
@@ -591,6 +623,19 @@ def test_dir_shadow_grids_full_frames(name, res, edits, monkeypatch):
     monkeypatch.setattr(OPTS, "dsgrid_min", "1")
     a = product_scene(name, res, **edits).render_device().clone()
     monkeypatch.setattr(OPTS, "dsgrid", "0")
+    b = product_scene(name, res, **edits).render_device().clone()
+    torch.cuda.synchronize()
+    assert torch.equal(a, b), float((a != b).float().mean())
+
+
+@pytest.mark.parametrize("name,res,edits", [("DepthOfField", (3840, 2160), {"AA": {"jitter": True, "samples": 2}}),
+                                            ("TwoSpheresPlane", (1920, 1080), {}), ("TorusMesh", (1920, 1080), {})])
+def test_self_skip_full_frames(name, res, edits, monkeypatch):
+    """The plane and box self-test skips (a camera ray's hit skips its own
+    object's shadow test where a rounding bound proves it cannot pass) on and off (option
+    self_skip): the same BASELINE-config frames, bit for bit."""
+    a = product_scene(name, res, **edits).render_device().clone()
+    monkeypatch.setattr(OPTS, "self_skip", "0")
     b = product_scene(name, res, **edits).render_device().clone()
     torch.cuda.synchronize()
     assert torch.equal(a, b), float((a != b).float().mean())
