@@ -296,8 +296,8 @@ RTX_HD void render_pixel(const KParams& P, float* fb, int32_t row0, int32_t rr, 
 // total order -- as (t32 bits, stored face or -1). The primary ray is render_pixel's of a
 // one-sample pinhole camera (the bins' cameras): aa_o[0] toward the pixel's focal point.
 // Every lane of a wave calls it for the same chunk (the loop's votes are the wave's).
-// (Starting chunks c >= 1 from chunk 0's closest face, in a second launch after it,
-// measured slower: blob 1080p 0.275 -> 0.291 ms.)
+// (Measured slower: starting chunks c >= 1 from chunk 0's closest face, in a second launch
+// after it, blob 1080p 0.275 -> 0.291 ms; two faces per step, 0.201 -> 0.208-0.212 ms.)
 RTX_HD uint2 mesh_chunk(const KParams& P, int32_t bin, int32_t c, int lane) {
     const SceneView& S = P.S;
     const int32_t ty = bin / S.bins_x, tx = bin - ty * S.bins_x;

@@ -1922,6 +1922,13 @@ RTX_HD bool shadow_tri(const Tri& T, f3 o, f3 d) {
 #ifndef RTX_LGRID_LANE
 #define RTX_LGRID_LANE 1  // light-grid lists: 1 per lane, 0 one distinct cell of the wave at a time
 #endif
+// Per-lane light-grid lists two faces per step: the 81,920-face mesh at 1080p 0.263-0.277 ->
+// 0.200 ms (its lit points near the shadow's edge run lists of up to ~200 faces, and the
+// frame waited on those waves); TorusMesh (small mesh, short lists) 48.9 -> 53.4 us, so
+// only kernels of scenes whose meshes have no face boxes (RTX_FACE_CULL_MODE 0) pair them.
+#ifndef RTX_LGRID_PAIRS
+#define RTX_LGRID_PAIRS (RTX_FACE_CULL_MODE == 0)
+#endif
 
 // The light-grid cell of a shadow ray from o toward a point light, d = L - o as the
 // shader computes it (so -d = fl(o - L) exactly): >= 0 a cell, -1 the line through o and
@@ -2146,11 +2153,29 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
                         const f3 w = neg(d);
                         // the mesh side of the light: faces farther along a than |w| are out
                         const float wcap = dot(w, ld3(g.a)) > 0.0f ? dot(w, w) : INFINITY;
+#if RTX_LGRID_PAIRS
+                        // two faces per step (their loads and tests overlap): any face before
+                        // the cut that the ray meets occludes, in whatever order they are tested
+                        for (int32_t q = S.lg_start[g.start_off + cell]; q < q1; q += 2) {
+                            const bool two = q + 1 < q1;
+                            const float da = S.lg_d2[q], db = two ? S.lg_d2[q + 1] : INFINITY;
+                            if (da > wcap) break;
+                            const int32_t fa = S.lg_faces[q], fb = S.lg_faces[two ? q + 1 : q];
+                            const DTri Ta = S.tris[ob.tri_begin + fa], Tb = S.tris[ob.tri_begin + fb];
+                            const bool ha = shadow_tri(Ta, o, d);
+                            const bool hb = shadow_tri(Tb, o, d) && db <= wcap;
+                            tally_inc<COUNT>(tl, &Tally::tri);
+                            if (db <= wcap) tally_inc<COUNT>(tl, &Tally::tri);
+                            if (ha || hb) { occ = true; break; }
+                            if (db > wcap) break;
+                        }
+#else
                         for (int32_t q = S.lg_start[g.start_off + cell]; q < q1; ++q) {
                             if (S.lg_d2[q] > wcap) break;
                             tally_inc<COUNT>(tl, &Tally::tri);
                             if (shadow_tri(S.tris[ob.tri_begin + S.lg_faces[q]], o, d)) { occ = true; break; }
                         }
+#endif
                     }
                     todo = false;
 #endif
