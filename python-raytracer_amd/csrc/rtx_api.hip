@@ -1824,8 +1824,14 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
     // CSG/texture kernels: the unrolled loops raise their (already high) register
     // pressure and the specialized kernel measured slower (NovelScene1 105 -> 134 ms)
     if (ext && !opt_on(OPT_JIT_EXT)) return false;  // (option jit_ext: specialize them anyway)
+    // -fno-slp-vectorize: the SLP pass packs pairs of scalar f32 operations into v_pk_*_f32,
+    // which on gfx950 issue at the cost of the two scalar operations and add the v_mov that
+    // gather their register pairs; without it the kernels need fewer VGPRs (TwoSpheresPlane
+    // 68 -> 62: 8 waves/SIMD instead of 7; TorusMesh and DepthOfField lose their scratch
+    // spills) and run faster: TSP 1080p 24.1 -> 21.5 us, MirrorRefraction 40.2 -> 38.3 us,
+    // TorusMesh 48.9 -> 46.7 us, DepthOfField 4K 4.62 -> 4.38 ms (profiles/r05/noslp/).
     std::vector<std::string> opts = {"--offload-arch=" + arch, "-O3", "-std=c++17", "-ffp-contract=off",
-                                     "-DRTX_FIXED_COUNTS",
+                                     "-fno-slp-vectorize", "-DRTX_FIXED_COUNTS",
                                      "-DRTX_FIXED_NP=" + std::to_string(v.n_plane),
                                      "-DRTX_FIXED_NS=" + std::to_string(v.n_sphere),
                                      "-DRTX_FIXED_NB=" + std::to_string(v.n_box),

@@ -2208,6 +2208,111 @@ RTX_HD bool occluded(const SceneView& S, f3 o, f3 d, double t_max, float time, T
     return occ;
 }
 
+// The shadow rays of every light at once, for scene-specialized kernels of flat scenes of
+// planes and spheres whose lights are all point lights (RTX_LIGHTS_TOGETHER): objects in
+// the outer loop, lights in the inner one, so the lights' tests of one object are
+// independent chains of one block instead of one light's whole occluded() after another.
+// Every light's test is occluded()'s, operation for operation (t_max = 1: a point light,
+// scene.py:155-158); returns bit li = light li's ray is occluded.
+#if defined(RTX_FIXED_COUNTS) && !defined(RTX_LIGHTS_TOGETHER)
+#define RTX_LIGHTS_TOGETHER (RTX_FIXED_NB == 0 && RTX_FIXED_NM == 0 && RTX_FIXED_LDIR == 0u && RTX_FIXED_NL >= 2 && \
+                             RTX_FIXED_NL <= 8 && RTX_PLANE_SHADOW_RCP && !RTX_SHADOW_F32)
+#endif
+#if defined(RTX_LIGHTS_TOGETHER) && RTX_LIGHTS_TOGETHER
+RTX_HD uint32_t occluded_points(const SceneView& S, f3 o, const f3* sd, const OriginTerms& ot, int32_t self_obj) {
+    constexpr int NL = RTX_FIXED_NL;
+    const double t_max = 1.0;
+    const float tmax32 = 1.0f, tmax_up = 1.0f, tmax_lim = nextafterf(1.0f, -INFINITY);
+    bool occ[NL];
+#pragma unroll
+    for (int li = 0; li < NL; ++li) occ[li] = false;
+    int oi = 0;
+    const float pm = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
+    for (int k = 0; k < RTX_NPLANE(S); ++k, ++oi) {  // simple_geometry.py:122-131
+        // a camera hit on this plane, close enough to the origin: its own test cannot pass
+        bool skip[NL];
+        bool all_skip = true;
+#pragma unroll
+        for (int li = 0; li < NL; ++li) {
+            skip[li] = S.plane_self != nullptr && k < 4 &&
+                       RTX_ALL(occ[li] || (oi == self_obj && pm <= S.plane_self[4 * li + k]));
+            all_skip = all_skip && skip[li];
+        }
+        if (all_skip) continue;
+        const DObj ob = S.objs[oi];
+        const f3 n = ld3(ob.b);
+        const float num = ot.pnum[k];
+        float den[NL];
+        bool hit[NL], slow[NL];
+        bool any_slow = false;
+#pragma unroll
+        for (int li = 0; li < NL; ++li) {  // occluded()'s quotient filter (RTX_PLANE_SHADOW_RCP)
+            den[li] = dot(sd[li], n);
+            hit[li] = slow[li] = false;
+            if (fabsf(den[li]) >= kEps4Up) {
+                const float ta = num * rcp_approx(den[li]), lo = ta * (1.0f - 0x1p-19f), hi = ta * (1.0f + 0x1p-19f);
+                const float tlo = fminf(lo, hi), thi = fmaxf(lo, hi);
+                const int above = tlo >= kEps4Up ? 1 : (thi < kEps4Near ? 0 : -1);
+                const int below = thi < tmax_lim ? 1 : (tlo >= tmax_up && tlo < INFINITY ? 0 : -1);
+                if (above >= 0 && below >= 0) hit[li] = above == 1 && below == 1;
+                else slow[li] = !skip[li];
+            }
+            any_slow = any_slow || slow[li];
+        }
+        if (RTX_ANY(any_slow)) {
+            unspeculated();  // (the correctly rounded quotient only near a threshold)
+#pragma unroll
+            for (int li = 0; li < NL; ++li)
+                if (slow[li]) {
+                    const float t32 = num / den[li];
+                    hit[li] = quot_gt(t32, num, den[li], 1e-4, kEps4Near) && quot_lt(t32, num, den[li], t_max, tmax32);
+                }
+        }
+#pragma unroll
+        for (int li = 0; li < NL; ++li) occ[li] = occ[li] || (!skip[li] && hit[li]);
+    }
+    for (int k = 0; k < RTX_NSPHERE(S); ++k, ++oi) {  // simple_geometry.py:48-72 (shadow_epsilon 1e-3)
+        bool need[NL];
+        bool any_need = false;
+        const DObj ob = S.objs[oi];
+#pragma unroll
+        for (int li = 0; li < NL; ++li) {
+            need[li] = !occ[li] && sphere_disc_sign_oc(sd[li], ot.soc[k], ot.sq[k], ob.r2f) >= 0;
+            any_need = any_need || need[li];
+        }
+        if (!RTX_ANY(any_need)) continue;
+        double b[NL], sq[NL], two_a[NL];
+        bool roots[NL], hit[NL];
+        bool any_far = false;
+#pragma unroll
+        for (int li = 0; li < NL; ++li) {
+            roots[li] = need[li] && sphere_roots_oc(sd[li], ot.soc[k], ot.sq[k], ob.r2, b[li], sq[li], two_a[li]);
+            hit[li] = false;
+            if (roots[li]) {
+                const double t1 = (-b[li] - sq[li]) / two_a[li];
+                hit[li] = 1e-3 < t1 && t1 < t_max;
+            }
+            any_far = any_far || (roots[li] && !hit[li]);
+        }
+        if (RTX_ANY(any_far)) {  // the second root only where some lane needs it
+            unspeculated();
+#pragma unroll
+            for (int li = 0; li < NL; ++li)
+                if (roots[li] && !hit[li]) {
+                    const double t2 = (-b[li] + sq[li]) / two_a[li];
+                    hit[li] = 1e-3 < t2 && t2 < t_max;
+                }
+        }
+#pragma unroll
+        for (int li = 0; li < NL; ++li) occ[li] = occ[li] || (roots[li] && hit[li]);
+    }
+    uint32_t m = 0u;
+#pragma unroll
+    for (int li = 0; li < NL; ++li) m |= occ[li] ? 1u << li : 0u;
+    return m;
+}
+#endif
+
 struct Surface {
     f3 position, normal;
     int32_t mat;
@@ -2326,6 +2431,14 @@ RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const 
     const OriginTerms* otp = RTX_NLIGHTS(S) > 1 ? &ot : nullptr;
 #else
     const OriginTerms* otp = nullptr;
+#endif
+#if defined(RTX_LIGHTS_TOGETHER) && RTX_LIGHTS_TOGETHER
+    if (!MESH && !X && occ_mask < 0 && !RTX_PROBE(1)) {  // every light's shadow ray at once
+        f3 sd[RTX_FIXED_NL];
+#pragma unroll
+        for (int li = 0; li < RTX_FIXED_NL; ++li) sd[li] = sub(ld3(S.lights[li].vec), pos);
+        occ_mask = (int64_t)occluded_points(S, pos, sd, ot, self_obj);
+    }
 #endif
     for (int li = 0; li < RTX_NLIGHTS(S); ++li) {
         const DLight L = S.lights[li];

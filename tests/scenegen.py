@@ -61,6 +61,53 @@ def random_scene(seed, res=(48, 36), mesh=False):
     return sc
 
 
+def point_lights_scene(seed, res=(64, 48)):
+    """Flat scenes of planes and spheres under two to eight point lights only -- the
+    specialized kernels' all-lights-at-once shadow test (rtx_trace.h occluded_points):
+    lights above and below the ground, inside and next to spheres, on a wall's plane
+    (grazing shadow rays), mirrors and refraction so secondary hits shade too."""
+    rng = np.random.RandomState(9000 + seed)
+    r = lambda lo, hi, n=None: np.round(rng.uniform(lo, hi, n), 3).tolist()  # noqa: E731
+    mats = [{"name": "m%d" % i, "ID": i, "diffuse": r(0, 1, 3), "specular": r(0, 1, 3),
+             "hardness": int(rng.choice([0, 16, 50])), "type": t, "tint": 0.3, "refr_index": 1.3}
+            for i, t in enumerate(["diffuse", "diffuse", "mirror", "refractive"])]
+    objs = [{"name": "ground", "type": "plane", "normal": [0.0, 1.0, 0.0], "position": [0.0, -1.0, 0.0],
+             "materials": [0, 1]}]
+    for k in range(rng.randint(0, 4)):
+        objs.append({"name": "w%d" % k, "type": "plane", "normal": r(-1, 1, 3), "position": r(-4, 4, 3),
+                     "materials": [int(rng.randint(4))]})
+    spheres = []
+    for k in range(rng.randint(1, 7)):
+        o = {"name": "s%d" % k, "type": "sphere", "radius": float(r(0.1, 1.2)), "position": r(-2.5, 2.5, 3),
+             "materials": [int(rng.randint(4))]}
+        if rng.rand() < 0.2:
+            o["speed"] = r(-0.5, 0.5, 3)
+        spheres.append(o)
+        objs.append(o)
+    lights = []
+    for i in range(rng.randint(2, 9)):
+        u = rng.rand()
+        if u < 0.15:  # inside a sphere
+            pos = list(spheres[int(rng.randint(len(spheres)))]["position"])
+        elif u < 0.3:  # under the ground
+            pos = [float(r(-3, 3)), float(r(-4, -1.5)), float(r(-3, 3))]
+        elif u < 0.4:  # on the ground's plane: grazing shadow rays
+            pos = [float(r(-3, 3)), -1.0, float(r(-3, 3))]
+        else:
+            pos = r(-6, 6, 3)
+        lights.append({"name": "p%d" % i, "type": "point", "position": pos, "colour": r(0.2, 1, 3),
+                       "power": float(r(0.2, 1.0))})
+    order = rng.permutation(len(objs))
+    sc = {"resolution": list(res), "AA": {"jitter": False, "samples": int(rng.choice([1, 2]))},
+          "ambient": [0.1, 0.1, 0.1],
+          "camera": {"position": [float(r(-2, 2)), float(r(1, 4)), float(r(6, 9))], "lookAt": [0.0, 0.0, 0.0],
+                     "up": [0.0, 1.0, 0.0], "fov": float(rng.choice([45.0, 70.0]))},
+          "materials": mats, "objects": [objs[i] for i in order], "lights": lights}
+    if rng.rand() < 0.25:
+        sc["motion"] = {"time": 1.0, "samples": 2, "final": 1}
+    return sc
+
+
 def shadow_scene(seed, res=(40, 30)):
     """Scenes for the directional lights' shadow grids (rtx_api.hip dir_shadow_grids):
     spheres from tiny to large, near and far, boxes (some given by swapped corners), some

@@ -257,6 +257,20 @@ def test_random_static_uniform_hardness_scenes_match_oracle(seed):
     assert_parity(product_scene_dict(d).render(), oracle_render_dict(d), "static seed %d" % seed)
 
 
+@pytest.mark.parametrize("seed", range(16))
+def test_point_lights_scenes_match_oracle(seed, monkeypatch):
+    """Planes and spheres under 2-8 point lights: the specialized kernel tests every
+    light's shadow ray at once (rtx_trace.h occluded_points); bit-exact with the oracle,
+    and equal to the one-light-at-a-time kernel (RTX_LIGHTS_TOGETHER=0)."""
+    from common import OPTS, oracle_render_dict, product_scene_dict
+    from scenegen import point_lights_scene
+    d = point_lights_scene(seed)
+    img = product_scene_dict(d).render()
+    assert_parity(img, oracle_render_dict(d), "point lights seed %d" % seed)
+    monkeypatch.setattr(OPTS, "jit_flags", "-DRTX_LIGHTS_TOGETHER=0")
+    assert np.array_equal(product_scene_dict(d).render(), img)
+
+
 def test_ties_follow_scene_order():
     from common import oracle_render_dict, product_scene_dict
     from scenegen import tie_scene

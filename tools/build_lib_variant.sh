@@ -6,7 +6,7 @@ cd "$(dirname "$0")/../python-raytracer_amd"
 name=$1; shift
 out=../_abl/build_$name; mkdir -p $out
 make -s csrc/rtx_jit_sources.inc
-flags="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -Wall"
+flags="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize -fPIC -Wall"
 for t in rtx_api rtx_kern_ext_m0 rtx_kern_ext_m1; do /opt/rocm/bin/hipcc $flags "$@" -c -o $out/$t.o csrc/$t.hip & done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o ../_abl/librtx_$name.so $out/*.o -lhiprtc

@@ -76,7 +76,7 @@ def main():
     subprocess.check_call(base + ["-S", "-o", out, path])
     r = subprocess.run(base + ["-c", "-o", "/tmp/jit_offline.o", "-Rpass-analysis=kernel-resource-usage", path],
                        capture_output=True, text=True)
-    for m in re.findall(r"(VGPRs: \d+|ScratchSize \[bytes/lane\]: \d+|Occupancy \[waves/SIMD\]: \d+|SGPRs Spill: \d+|"
+    for m in re.findall(r"(Function Name: \S+|VGPRs: \d+|ScratchSize \[bytes/lane\]: \d+|Occupancy \[waves/SIMD\]: \d+|SGPRs Spill: \d+|"
                         r"VGPRs Spill: \d+|TotalSGPRs: \d+|LDS Size \[bytes/block\]: \d+)", r.stderr):
         print(m)
     os.unlink(path)
