@@ -70,7 +70,7 @@ int fail(int code, const std::string& msg) {
 // rendering; they are not synchronised with renders running on other threads.
 enum Opt {
     OPT_SPLIT, OPT_SPLIT_BYTES, OPT_SPLIT_RATIO, OPT_BINS, OPT_HEAVY_TILES, OPT_LENS_BINS, OPT_LGRID, OPT_DSGRID, OPT_DSGRID_MIN,
-    OPT_SELF_SKIP, OPT_TILE_SCHED, OPT_PRIM_ORIGIN, OPT_SPP, OPT_SPP_MIN, OPT_JIT, OPT_JIT_BAKE, OPT_JIT_EXT,
+    OPT_SELF_SKIP, OPT_TILE_SCHED, OPT_XCD_MAP, OPT_PRIM_ORIGIN, OPT_SPP, OPT_SPP_MIN, OPT_JIT, OPT_JIT_BAKE, OPT_JIT_EXT,
     OPT_JIT_DUMP, OPT_JIT_IDLE_BAKED, OPT_JIT_DISK_BAKED, OPT_JIT_CACHE, OPT_JIT_FLAGS, OPT_SETUP_LOG, OPT_COUNT
 };
 struct OptDef {
@@ -90,6 +90,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"dsgrid_min", 8, false},                 // the fewest spheres (and nothing else) that get one
     {"self_skip", 1, false},                  // plane / box self tests skipped where provably passing
     {"tile_sched", 1, false},                 // measured longest-first tile order
+    {"xcd_map", 0, false},                    // XCD-aware block order of tile-mapped launches
     {"prim_origin", 1, false},                // host-computed origin terms of pinhole primary rays
     {"spp", -1, false},                       // sample-parallel mapping: -1 auto, 0 never, 1 always
     {"spp_min", 16, false},                   // auto: from this many samples per pixel (X scenes)
@@ -2075,6 +2076,7 @@ struct rtx_scene {
     uint2* d_mesh_hits = nullptr;
     int32_t heavy_n = 0;
     int tile_sched = 0;
+    bool tile_xcd = false;            // the schedule table's layout (option xcd_map when sorted)
     hipEvent_t tile_event = nullptr;  // recorded after the measuring launch
     // the split hierarchy passes (rtx_split.h, render_split): the record arrays of one
     // chunk (kept while the scene lives, reused by every frame), the per-chunk append
@@ -2650,10 +2652,19 @@ int tile_schedule(rtx_scene* s, hipStream_t st) {
         s->tile_sched = 4;
         return RTX_OK;
     }
-    std::vector<int32_t> perm((size_t)n);
-    std::iota(perm.begin(), perm.end(), 0);
-    std::stable_sort(perm.begin(), perm.end(), [&](int32_t a, int32_t b) { return t[a] > t[b]; });
-    RTX_HIP(hipMemcpyAsync(s->d_tile_perm, perm.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
+    std::vector<int32_t> order((size_t)n);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return t[a] > t[b]; });
+    s->tile_xcd = opt_on(OPT_XCD_MAP);  // (the frames that follow this table keep its layout)
+    // dispatch position p (block p / wpb) reads the entry of its slot (pixel_rc's xcd_block):
+    // the p-th dispatched wave renders the p-th longest tile, and each XCD reads its own lines
+    const uint32_t wpb = kBlock<false> / 64, nb = (uint32_t)((n + wpb - 1) / wpb);
+    std::vector<int32_t> perm((size_t)nb * wpb);
+    for (uint32_t p = 0; p < nb * wpb; ++p) {
+        const uint32_t slot = (s->tile_xcd ? xcd_block(p / wpb, nb, wpb) : p / wpb) * wpb + p % wpb;
+        perm[slot] = p < (uint32_t)n ? order[p] : (int32_t)p;
+    }
+    RTX_HIP(hipMemcpyAsync(s->d_tile_perm, perm.data(), sizeof(int32_t) * perm.size(), hipMemcpyHostToDevice, st));
     RTX_HIP(hipStreamSynchronize(st));  // (perm is a local: wait for the copy)
     s->tile_sched = 3;
     return RTX_OK;
@@ -2849,6 +2860,7 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
         L.pix0 = 0;
         L.tperm = 0;
         L.tlog = 0;
+        L.xcd = opt_on(OPT_XCD_MAP) ? 1 : 0;
         L.redo = RedoList{nullptr, nullptr, nullptr};
     }
     // the heavy tiles' chunks of every frame of a tile-mapped launch, just before it (the
@@ -2880,6 +2892,7 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
             L.tlog = s->tile_sched == 1;
         }
         if (whole) L.tperm = s->tile_sched == 3;
+        if (L.tperm) L.xcd = s->tile_xcd ? 1 : 0;
         if (int rc = heavy_pass(!spp_mode)) return rc;
         RTX_HIP(hipModuleLaunchKernel(rs.fn, (unsigned)nblocks, (unsigned)nframes, 1, blk, 1, 1,
                                       s->has_ext ? (unsigned)(hbytes * blk) : 0u, st, args, nullptr));

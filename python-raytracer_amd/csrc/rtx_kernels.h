@@ -348,6 +348,7 @@ struct Launch {
     int32_t pix0;   // split hierarchy passes (rtx_split.h): the chunk's first pixel of the block
     int32_t tperm;  // RTX_TILE_SCHED kernels: 1 = dispatch a whole frame's tiles by P.tile_perm
     int32_t tlog;   // RTX_TILE_SCHED kernels: 1 = record each wave's duration in P.tile_time
+    int32_t xcd;    // 1 = XCD-aware block order (xcd_block; tile-mapped render_body)
     // render_body_spp as the split passes' fallback (rtx_split.h): render only the listed
     // blocks (chains that found the record pool full), pixels from pix0 on
     RedoList redo;
@@ -412,11 +413,29 @@ struct PixelRC {
 #ifndef RTX_TILE_SCHED
 #define RTX_TILE_SCHED 0
 #endif
-__device__ __forceinline__ PixelRC pixel_rc(int32_t ncols, int sub, uint32_t perm = 1,
+// XCD-aware block order (Launch::xcd, option xcd_map): the dispatcher hands workgroups to the 8 XCDs
+// round-robin, so consecutive blocks -- neighbouring tiles, whose bin lists, tile-schedule
+// entries and scene lines share cache lines -- would land in 8 different L2s. Block b
+// instead takes slot block xcd_block(b): each XCD's k-th run of 16 waves (g blocks of
+// 16/g waves) takes 16 consecutive tiles. Blocks of the last incomplete round of 8 runs keep
+// their own index, so the map is a bijection on [0, nb). Host and device share it (the
+// tile schedule's table is laid out through it, rtx_api.hip tile_schedule). Off by default:
+// it cuts the fabric reads of the bins, light grids and schedule table (TorusMesh 1080p
+// 29.8 -> 28.9 MB per frame, TwoSpheresPlane 26.2 -> 25.5, DepthOfField 4K 111.7 -> 109.5)
+// but not the time (TwoSpheresPlane 22.06 -> 22.42 us, the 81,920-face mesh +1 %,
+// DepthOfField -0.6 %; profiles/r05/xcd/).
+__host__ __device__ inline uint32_t xcd_block(uint32_t b, uint32_t nb, uint32_t waves_per_block) {
+    const uint32_t lg = waves_per_block >= 16 ? 0u : (waves_per_block >= 4 ? 2u : (waves_per_block >= 2 ? 3u : 4u));
+    const uint32_t g = 1u << lg, round = 8u * g;
+    if (b >= nb / round * round) return b;
+    const uint32_t x = b & 7u, k = b >> 3;
+    return (((k >> lg) << 3) + x) * g + (k & (g - 1u));
+}
+__device__ __forceinline__ PixelRC pixel_rc(int32_t ncols, int sub, uint32_t perm = 1, int32_t xcd = 0,
                                             const int32_t RTX_CONST* tperm = nullptr, int* tile = nullptr) {
     const int lane = threadIdx.x & 63;
-    int wave = __builtin_amdgcn_readfirstlane(
-        (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RTX_PPL + sub));
+    const uint32_t blk = xcd ? xcd_block(blockIdx.x, gridDim.x, blockDim.x >> 6) : blockIdx.x;
+    int wave = __builtin_amdgcn_readfirstlane((int)((blk * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RTX_PPL + sub));
     const uint32_t T = gridDim.x * (blockDim.x >> 6) * RTX_PPL;
     if (RTX_TILE_SCHED && tperm != nullptr) wave = tperm[wave];
     if (tile) *tile = wave;
@@ -537,9 +556,9 @@ __device__ __forceinline__ void render_body(const KParams* __restrict__ Pp, cons
 #endif
     for (int sub = 0; sub < RTX_PPL; ++sub) {
 #if RTX_TILE_SCHED && defined(__HIP_DEVICE_COMPILE__)
-        const PixelRC px = pixel_rc(ncols, sub, L.perm, L.tperm ? Pp->tile_perm : nullptr, &tile);
+        const PixelRC px = pixel_rc(ncols, sub, L.perm, L.xcd, L.tperm ? Pp->tile_perm : nullptr, &tile);
 #else
-        const PixelRC px = pixel_rc(ncols, sub, L.perm);
+        const PixelRC px = pixel_rc(ncols, sub, L.perm, L.xcd);
 #endif
         const bool active = px.r < L.nrows && px.c < ncols;
         any_active = any_active || active;

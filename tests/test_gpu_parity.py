@@ -50,6 +50,27 @@ def test_config_size_1080p_matches_oracle(name):
     assert kernels[2].endswith("+tiles") == (name != "TwoSpheresPlane"), kernels
 
 
+@pytest.mark.parametrize("name,res", [("MirrorRefraction", (1000, 600)), ("TorusMesh", (1920, 1080)),
+                                      ("TwoSpheresPlane", (333, 257))])
+def test_xcd_block_order_equal(name, res, monkeypatch):
+    """The XCD-aware block order (rtx_kernels.h xcd_block, option xcd_map) renders the same
+    bytes as dispatch order -- sizes whose last round of blocks is incomplete, eager frames
+    through the tile schedule's measure/sort/scheduled states -- and a scene whose schedule
+    table was laid out under one setting keeps rendering right after the option flips."""
+    sc = product_scene(name, res)
+    imgs = [sc.render_device().cpu().numpy() for _ in range(3)]
+    monkeypatch.setattr(OPTS, "xcd_map", "0")
+    imgs.append(sc.render_device().cpu().numpy())  # (the table sorted under xcd_map 1)
+    sc0 = product_scene(name, res)
+    imgs += [sc0.render_device().cpu().numpy() for _ in range(3)]
+    monkeypatch.setattr(OPTS, "xcd_map", "1")
+    imgs.append(sc0.render_device().cpu().numpy())  # (the table sorted under xcd_map 0)
+    imgs.append(sc0.render_device(row0=40, nrows=77).cpu().numpy())
+    for k, a in enumerate(imgs[:-1]):
+        assert np.array_equal(a, imgs[0]), (name, k)
+    assert np.array_equal(imgs[-1], imgs[0][40:117]), name
+
+
 def test_counters_match_oracle_tallies():
     for name, res in (("MirrorRefraction", (192, 108)), ("TorusMesh", (96, 54)), ("TwoSpheresPlane", (192, 108))):
         sc = product_scene(name, res)

@@ -7,6 +7,7 @@ OUT=gpurun_out/${TAG:-pmc}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 CFG=${CFG:-tsp1080}
+# PMC_EXTRA="group;group": more passes after the default ones (e.g. the VALU mix)
 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
 i=0
 while read -r grp; do
@@ -20,5 +21,6 @@ ${PMC_GROUPS:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES 
 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM SQ_INST_CYCLES_VMEM SQ_INSTS_LDS GRBM_GUI_ACTIVE
 FETCH_SIZE
 WRITE_SIZE}
+$(echo "${PMC_EXTRA:-}" | tr ';' '\n')
 GROUPS
 echo PMC_DONE

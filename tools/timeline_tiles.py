@@ -1,5 +1,6 @@
 """The longest waves of a wave timeline (tools/wave_timeline.py --npz, taken with the tile
-schedule off -- RTX_TILE_SCHED=0 -- so wave w renders tile w in row-major order) with their
+schedule and the XCD block order off -- RTX_TILE_SCHED=0 RTX_XCD_MAP=0 -- so wave w renders
+tile w in row-major order) with their
 tiles: (tile row, tile column), duration, and the tile's primary-ray mesh face count from
 the host emulation's bins. usage: python tools/timeline_tiles.py wt.npz config [top]"""
 import os
