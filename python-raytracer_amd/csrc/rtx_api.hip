@@ -1375,6 +1375,8 @@ bool heavy_chunks(const std::vector<int32_t>& bstart, std::vector<int32_t>& bhea
     return !items.empty();
 }
 
+constexpr int32_t kDsgG = 512;  // cells per side of a directional light's shadow grid
+
 // Shadow grids of directional lights (DSGrid, rtx_trace.h), per camera (the motion-time
 // range [tlo, thi] of the frame bounds the moving objects). Light li's shadow ray from p is
 // the half-line p + t d (d = fl32 -direction, LIGHT.negvec; t > 1e-4 or 1e-3). On two
@@ -1401,10 +1403,15 @@ bool heavy_chunks(const std::vector<int32_t>& bstart, std::vector<int32_t>& bhea
 // -- twice the bound -- stays below 1e-4 min |D_a| / 2: their own shadow test cannot pass
 // for such a hit point and is skipped. omax bounds |o| of the camera's sample origins
 // (camera_origin_bound).
+// rects != nullptr: the cells are left to the device (k_dsg_fill) -- `cells` stays empty,
+// *rects gets each object's cell rectangle and *ncells the grids' total cell count.
 bool dir_shadow_grids(const HostScene& H, const std::vector<DBound>& nb, double tlo, double thi,
-                      std::vector<DSGrid>& grids, std::vector<DSCell>& cells) {
+                      std::vector<DSGrid>& grids, std::vector<DSCell>& cells, std::vector<DSRect>* rects = nullptr,
+                      size_t* ncells = nullptr) {
     grids.assign(H.lights.size(), DSGrid{});
     cells.clear();
+    if (rects) rects->clear();
+    size_t ncell = 0;
     struct Ob {
         double lo[3], hi[3];  // bounding box
         double c[3], r;       // a static sphere: centre and radius (r < 0: a box)
@@ -1485,7 +1492,7 @@ bool dir_shadow_grids(const HostScene& H, const std::vector<DBound>& nb, double 
     // 512 x 512 cells (2 MB per light): finer grids measured faster up to 512 (DepthOfField
     // 4K 5.09 -> 5.01 ms, NovelScene1 17.48 -> 16.96 ms, NovelScene2 79.2 -> 76.7 ms from 64;
     // 1024 within 0.5 %, profiles/r04/dsgrid_g/)
-    const int32_t G = 512;
+    const int32_t G = kDsgG;
     const double pmax = 1.25 * R + 1.0, pm = std::sqrt(3.0) * pmax;  // pm >= |p| of a gridded origin
     bool any = false;
     for (size_t li = 0; li < H.lights.size(); ++li) {
@@ -1554,10 +1561,11 @@ bool dir_shadow_grids(const HostScene& H, const std::vector<DBound>& nb, double 
         g.sv = (float)((G - 4) / wv);
         g.u0 = (float)(U0 - 2.0 / g.su);
         g.v0 = (float)(V0 - 2.0 / g.sv);
-        g.off = (int32_t)cells.size();
+        g.off = (int32_t)ncell;
         g.always = always;
         g.always_root = always_root;
-        cells.resize(cells.size() + (size_t)G * G, DSCell{0u, 0u});
+        ncell += (size_t)G * G;
+        if (!rects) cells.resize(ncell, DSCell{0u, 0u});
         auto cell = [&](double u, double o0, double s) {  // as the device maps it, +-1 below
             return (int32_t)std::floor((u - o0) * s);
         };
@@ -1565,6 +1573,10 @@ bool dir_shadow_grids(const HostScene& H, const std::vector<DBound>& nb, double 
             const double* F = &fp[4 * i];
             const int32_t i0 = std::max(0, cell(F[0], g.u0, g.su) - 1), i1 = std::min(G - 1, cell(F[1], g.u0, g.su) + 1);
             const int32_t j0 = std::max(0, cell(F[2], g.v0, g.sv) - 1), j1 = std::min(G - 1, cell(F[3], g.v0, g.sv) + 1);
+            if (rects) {
+                if (i0 <= i1 && j0 <= j1) rects->push_back(DSRect{g.off, i0, i1, j0, j1, obs[i].bit, obs[i].root, 0u});
+                continue;
+            }
             for (int32_t jy = j0; jy <= j1; ++jy)
                 for (int32_t ix = i0; ix <= i1; ++ix) {
                     DSCell& c = cells[(size_t)g.off + (size_t)jy * G + ix];
@@ -1575,6 +1587,7 @@ bool dir_shadow_grids(const HostScene& H, const std::vector<DBound>& nb, double 
         grids[li] = g;
         any = true;
     }
+    if (ncells) *ncells = ncell;
     return any;
 }
 
@@ -2042,6 +2055,8 @@ struct rtx_scene {
     KParams kp{};
     char* d_cam = nullptr;
     size_t cam_cap = 0;
+    char* h_cam = nullptr;  // pinned bounce buffer of the camera uploads (pinned_copy)
+    size_t h_cam_cap = 0;
     KParams* d_kp = nullptr;  // (inside d_cam)
     // per frame time range [tlo, thi] (not per camera): the hierarchy bounds and the
     // directional lights' shadow-grid headers and cells (the cells in their own buffer)
@@ -2112,6 +2127,34 @@ int upload(void** dptr, const std::vector<T>& v) {
     return RTX_OK;
 }
 
+// Host-to-device uploads of rtx_camera_set go through the scene's pinned buffer (grown as
+// needed) and a copy kernel that reads it over the bus: hipMemcpy from pageable memory
+// set up the runtime's staging on a process's first camera upload (~7 ms), and a copy from
+// pinned memory the copy engine (~6 ms); the kernel's first launch costs ~1 ms.
+int pinned_reserve(rtx_scene* s, size_t n) {
+    if (s->h_cam_cap >= n) return RTX_OK;
+    (void)hipHostFree(s->h_cam);
+    s->h_cam = nullptr;
+    s->h_cam_cap = 0;
+    RTX_HIP(hipHostMalloc((void**)&s->h_cam, n + n / 4, hipHostMallocDefault));
+    s->h_cam_cap = n + n / 4;
+    return RTX_OK;
+}
+// The first n bytes of the pinned buffer (whole 16-byte words) to dst (16-byte aligned);
+// blocking, so the buffer can be refilled as soon as it returns.
+int pinned_upload(rtx_scene* s, void* dst, size_t n) {
+    if (n == 0) return RTX_OK;
+    if ((n & 15) || (reinterpret_cast<uintptr_t>(dst) & 15)) return fail(RTX_ERR_INVALID, "pinned_upload: unaligned");
+    void* hp = nullptr;
+    RTX_HIP(hipHostGetDevicePointer(&hp, s->h_cam, 0));
+    const int64_t w = (int64_t)(n / 16);
+    hipLaunchKernelGGL(k_stage_copy, dim3((unsigned)std::min<int64_t>(1024, (w + 255) / 256)), dim3(256), 0, nullptr,
+                       (const uint4*)hp, (uint4*)dst, w);
+    RTX_HIP(hipGetLastError());
+    RTX_HIP(hipStreamSynchronize(nullptr));
+    return RTX_OK;
+}
+
 // Forgets the camera (its kernels are specialized on its sample counts); the device
 // buffers stay for the next camera (free_scene frees them).
 void free_camera(rtx_scene* s) {
@@ -2126,6 +2169,7 @@ void free_camera(rtx_scene* s) {
 void free_scene(rtx_scene* s) {
     free_camera(s);
     (void)hipFree(s->d_cam);
+    (void)hipHostFree(s->h_cam);
     (void)hipFree(s->d_dsg_cells);
     (void)hipFree(s->d_scratch);
     if (s->split_done) (void)hipEventSynchronize(s->split_done);
@@ -2152,12 +2196,19 @@ struct SetupLog {
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), t = t0;
     std::string line;
     explicit SetupLog(const char* w) : what(w) {}
-    void mark(const char* step) {
+    size_t staged = 0;  // bytes of camera tables staged by the earlier steps
+    // staged_total: the staging buffer's size after this step (its tables' bytes are logged)
+    void mark(const char* step, size_t staged_total = SIZE_MAX) {
         if (!opt_on(OPT_SETUP_LOG)) return;
         const auto n = std::chrono::steady_clock::now();
-        char buf[96];
+        char buf[128];
         snprintf(buf, sizeof(buf), " %s %.3f", step, std::chrono::duration<double, std::milli>(n - t).count());
         line += buf;
+        if (staged_total != SIZE_MAX) {
+            snprintf(buf, sizeof(buf), " [%zu B]", staged_total - staged);
+            line += buf;
+            staged = staged_total;
+        }
         t = n;
     }
     ~SetupLog() {
@@ -2167,17 +2218,33 @@ struct SetupLog {
     }
 };
 
-// Host staging of the camera tables: 256-byte aligned segments of one buffer.
+// Layout of the camera tables: 256-byte aligned segments of one device buffer. put()
+// records where a table goes and where it comes from (the source must stay alive until
+// write(); p == nullptr: zero-filled); write() fills the pinned buffer once, with no growing
+// host vector to copy (DepthOfField's 1.5 MB of bins: 0.2 ms of reallocation copies).
 struct CamStage {
-    std::vector<char> b;
+    struct Seg {
+        size_t off;
+        const void* p;
+        size_t n;
+    };
+    std::vector<Seg> segs;
+    size_t bytes = 0;
     size_t put(const void* p, size_t n) {
-        const size_t off = (b.size() + 255) & ~(size_t)255;
-        b.resize(off + std::max<size_t>(n, 4));  // (zero-filled; p == nullptr: only reserve)
-        if (n && p) memcpy(b.data() + off, p, n);
+        const size_t off = (bytes + 255) & ~(size_t)255;
+        segs.push_back(Seg{off, p, n});
+        bytes = off + std::max<size_t>(n, 4);
         return off;
     }
     template <class T>
-    size_t put(const std::vector<T>& v) { return put(v.data(), sizeof(T) * v.size()); }
+    size_t put(const std::vector<T>& v) { return put(v.empty() ? nullptr : v.data(), sizeof(T) * v.size()); }
+    size_t size() const { return (bytes + 15) & ~(size_t)15; }  // (whole 16-byte words)
+    void write(char* h) const {
+        for (const Seg& g : segs) {
+            if (g.p) memcpy(h + g.off, g.p, g.n);
+            else memset(h + g.off, 0, std::max<size_t>(g.n, 4));
+        }
+    }
 };
 
 }  // namespace
@@ -2314,6 +2381,10 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
         std::vector<float> gd2;
         if (opt_on(OPT_LGRID) && light_grids(H, grids, gstart, gfaces, gd2)) {
             if (gfaces.empty()) { gfaces.push_back(0); gd2.push_back(0.0f); }
+            if (opt_on(OPT_SETUP_LOG))
+                fprintf(stderr, "librtx: light grids: %zu grids %zu B, starts %zu B, faces %zu B, d2 %zu B\n", grids.size(),
+                        sizeof(DLGrid) * grids.size(), sizeof(int32_t) * gstart.size(), sizeof(int32_t) * gfaces.size(),
+                        sizeof(float) * gd2.size());
             if ((rc = upload(&s->d_lgrid, grids)) || (rc = upload(&s->d_lg_start, gstart)) ||
                 (rc = upload(&s->d_lg_faces, gfaces)) || (rc = upload(&s->d_lg_d2, gd2))) {
                 free_scene(s);
@@ -2325,6 +2396,14 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
             v.lg_d2 = (cptr<float>)s->d_lg_d2;
             v.lgrid_on = 1;
         }
+    }
+    {  // the first launch of any of the library's kernels loads its code object (~1 ms):
+       // once per process, here rather than in the first camera upload
+        static std::once_flag loaded;
+        std::call_once(loaded, [] {
+            hipLaunchKernelGGL(k_stage_copy, dim3(1), dim3(64), 0, nullptr, nullptr, nullptr, (int64_t)0);
+            (void)hipGetLastError();
+        });
     }
     *out = s;
     return RTX_OK;
@@ -2357,14 +2436,29 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
         if (!s->h_nodes.empty())  // hierarchy bounds over the frame's motion-time range
             s->tr_bounds = compute_bounds(s->h_nodes, s->h_objs, s->h_tris, *mm.first, *mm.second);
         std::vector<DSCell> cells;
+        std::vector<DSRect> rects;
+        size_t ncells = 0;
         s->tr_grids.clear();
         s->tr_dsg_off = dsg_off;
-        s->tr_grids_on = !dsg_off &&
-                         dir_shadow_grids(s->h_bins, s->tr_bounds, *mm.first, *mm.second, s->tr_grids, cells);
+        s->tr_grids_on = !dsg_off && dir_shadow_grids(s->h_bins, s->tr_bounds, *mm.first, *mm.second, s->tr_grids,
+                                                      cells, &rects, &ncells);
         (void)hipDeviceSynchronize();  // (frames of the previous camera may still read the cells)
         (void)hipFree(s->d_dsg_cells);
         s->d_dsg_cells = nullptr;
-        if (s->tr_grids_on && (rc = upload(&s->d_dsg_cells, cells))) return rc;
+        if (s->tr_grids_on) {  // the cells, then the rectangles k_dsg_fill reads
+            const size_t n = sizeof(DSCell) * ncells, nr = sizeof(DSRect) * rects.size();
+            RTX_HIP(hipMalloc(&s->d_dsg_cells, n + std::max<size_t>(nr, 16)));
+            if (nr) {
+                if ((rc = pinned_reserve(s, nr))) return rc;
+                memcpy(s->h_cam, rects.data(), nr);
+                if ((rc = pinned_upload(s, (char*)s->d_dsg_cells + n, nr))) return rc;
+            }
+            hipLaunchKernelGGL(k_dsg_fill, dim3((unsigned)((ncells + 255) / 256)), dim3(256), 0, nullptr,
+                               (const DSRect*)((char*)s->d_dsg_cells + n), (int32_t)rects.size(),
+                               (DSCell*)s->d_dsg_cells, (int64_t)ncells, s->tr_grids.empty() ? 0 : kDsgG);
+            RTX_HIP(hipGetLastError());
+            RTX_HIP(hipStreamSynchronize(nullptr));
+        }
         s->tr_valid = true;
         s->tr_lo = *mm.first;
         s->tr_hi = *mm.second;
@@ -2379,20 +2473,31 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     size_t o_tperm = 0, o_ttime = 0;
     const bool replay = c->jitter == RTX_JITTER_REPLAY;
     if (replay) o_noise = st.put(c->noise, sizeof(float) * 3 * (size_t)c->ncols * c->height * nsamp);
-    slog.mark("tables");
-    if (!s->h_nodes.empty()) o_bounds = st.put(split_bounds(s->tr_bounds));
+    slog.mark("tables", st.size());
+    // (put() keeps pointers: every staged table lives until the upload)
+    std::vector<DBox> boxes;
+    std::vector<float> pself_lim;
+    std::vector<DSGrid> grids;
+    std::vector<int32_t> ident;
+    if (!s->h_nodes.empty()) {
+        boxes = split_bounds(s->tr_bounds);
+        o_bounds = st.put(boxes);
+    }
     // self tests of planes (option self_skip 0: none). Scenes with secondary rays get none:
     // MirrorRefraction measured 1.4 % slower with them (most of its shadow rays leave
     // deeper levels, which pay the check and never skip), TSP 3 % and TM 2 % faster
     // (profiles/r04/plane_self/)
     const bool pself = opt_on(OPT_SELF_SKIP) && s->view.n_plane > 0 && !s->h_bins.lights.empty() && !s->has_secondary;
-    if (pself) o_pself = st.put(plane_self_limits(s->h_bins, omax));
+    if (pself) {
+        pself_lim = plane_self_limits(s->h_bins, omax);
+        o_pself = st.put(pself_lim);
+    }
     if (s->tr_grids_on) {  // the grid headers with this camera's self-test marks
-        std::vector<DSGrid> grids = s->tr_grids;
+        grids = s->tr_grids;
         dir_self_boxes(s->h_bins, grids, omax);
         o_dsg = st.put(grids);
     }
-    slog.mark("self tests");
+    slog.mark("self tests", st.size());
     std::vector<int32_t> bstart, bfaces;
     std::vector<float> bz;
     std::vector<uint32_t> bmask, brmask;
@@ -2416,7 +2521,7 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
         o_hitems = st.put(hitems);
         o_mhits = st.put(nullptr, sizeof(uint2) * 64 * hitems.size());
     }
-    slog.mark("bins");
+    slog.mark("bins", st.size());
     // the measured tile schedule (tile_schedule): identity order until measured
     const bool tsched = tile_sched_enabled() && !s->has_ext && (s->has_secondary || s->has_mesh);
     int64_t tiles = 0;
@@ -2424,21 +2529,21 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
         const int64_t wpb = kBlock<false> / 64;
         tiles = (int64_t)((c->ncols + 7) / 8) * ((c->height + 7) / 8);
         const int64_t nw = (tiles + wpb - 1) / wpb * wpb;
-        std::vector<int32_t> ident((size_t)nw);
+        ident.resize((size_t)nw);
         std::iota(ident.begin(), ident.end(), 0);
         o_tperm = st.put(ident);
-        o_ttime = st.put(std::vector<uint32_t>((size_t)nw, 0u));
+        o_ttime = st.put(nullptr, sizeof(uint32_t) * nw);
     }
     const size_t o_kp = st.put(nullptr, sizeof(KParams));
-    slog.mark("tile schedule");
+    slog.mark("tile schedule", st.size());
     // one device buffer for all of it, reused while large enough; its old contents may still
     // be read by frames of the previous camera
     (void)hipDeviceSynchronize();
-    if (s->cam_cap < st.b.size()) {
+    if (s->cam_cap < st.size()) {
         (void)hipFree(s->d_cam);
         s->d_cam = nullptr;
         s->cam_cap = 0;
-        const size_t cap = st.b.size() + st.b.size() / 4;
+        const size_t cap = st.size() + st.size() / 4;
         RTX_HIP(hipMalloc((void**)&s->d_cam, cap));
         s->cam_cap = cap;
     }
@@ -2510,8 +2615,10 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
         s->d_tile_time = D + o_ttime;
         s->tile_sched = 1;
     }
-    memcpy(st.b.data() + o_kp, &k, sizeof(KParams));
-    RTX_HIP(hipMemcpy(D, st.b.data(), st.b.size(), hipMemcpyHostToDevice));
+    if ((rc = pinned_reserve(s, st.size()))) return rc;
+    st.write(s->h_cam);
+    memcpy(s->h_cam + o_kp, &k, sizeof(KParams));
+    if ((rc = pinned_upload(s, D, st.size()))) return rc;
     slog.mark("upload");
     s->d_kp = reinterpret_cast<KParams*>(D + o_kp);
     s->kp = k;

@@ -765,6 +765,33 @@ __global__ __launch_bounds__(256) void k_to_rgb8(const float* __restrict__ fb, u
         for (int64_t k = i; k < n; ++k) out[k] = to_u8(fb[k]);
     }
 }
+// Shadow-grid cells from their objects' rectangles (rtx_api.hip dir_shadow_grids): cell c of
+// grid `off` ORs the bits of every rectangle of that grid holding it -- the host loop's
+// result, without the host filling (and uploading) 2 MB per light.
+__global__ __launch_bounds__(256) void k_dsg_fill(const DSRect* __restrict__ r, int32_t nr, DSCell* __restrict__ cells,
+                                                  int64_t ncells, int32_t G) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ncells) return;
+    const int64_t gg = (int64_t)G * G, off = c / gg * gg;
+    const int32_t q = (int32_t)(c - off), jy = q / G, ix = q - jy * G;
+    DSCell v{0u, 0u};
+    for (int32_t k = 0; k < nr; ++k) {
+        const DSRect R = r[k];
+        if (R.off == off && ix >= R.i0 && ix <= R.i1 && jy >= R.j0 && jy <= R.j1) {
+            v.obj |= R.bit;
+            v.root |= R.root;
+        }
+    }
+    cells[c] = v;
+}
+
+// Camera uploads (rtx_api.hip pinned_upload): 16-byte words from the scene's pinned host
+// buffer, read over the bus by the kernel itself -- no copy engine.
+__global__ __launch_bounds__(256) void k_stage_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
 __global__ __launch_bounds__(256) void k_to_rgb8_unaligned(const float* __restrict__ fb, uint8_t* __restrict__ out,
                                                            int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

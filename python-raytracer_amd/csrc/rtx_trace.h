@@ -286,6 +286,12 @@ struct alignas(16) DLGrid {
 struct DSCell {
     uint32_t obj, root;
 };
+// One object's cell rectangle of a shadow grid (rtx_api.hip dir_shadow_grids; the device
+// fills the cells from these, k_dsg_fill): cells [i0, i1] x [j0, j1] of the grid at `off`.
+struct DSRect {
+    int32_t off, i0, i1, j0, j1;
+    uint32_t bit, root, pad;
+};
 struct alignas(16) DSGrid {
     float e1[3];
     int32_t G;  // cells per side; 0 = no grid for this light
