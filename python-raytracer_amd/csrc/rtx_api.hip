@@ -71,7 +71,7 @@ int fail(int code, const std::string& msg) {
 enum Opt {
     OPT_SPLIT, OPT_SPLIT_BYTES, OPT_SPLIT_RATIO, OPT_BINS, OPT_HEAVY_TILES, OPT_LENS_BINS, OPT_LGRID, OPT_DSGRID, OPT_DSGRID_MIN,
     OPT_SELF_SKIP, OPT_TILE_SCHED, OPT_XCD_MAP, OPT_PRIM_ORIGIN, OPT_SPP, OPT_SPP_MIN, OPT_JIT, OPT_JIT_BAKE, OPT_JIT_EXT,
-    OPT_JIT_DUMP, OPT_JIT_IDLE_BAKED, OPT_JIT_DISK_BAKED, OPT_JIT_CACHE, OPT_JIT_FLAGS, OPT_SETUP_LOG, OPT_COUNT
+    OPT_JIT_DUMP, OPT_JIT_IDLE_BAKED, OPT_JIT_DISK_BAKED, OPT_JIT_CACHE, OPT_JIT_FLAGS, OPT_JIT_ILP, OPT_SETUP_LOG, OPT_COUNT
 };
 struct OptDef {
     const char* name;
@@ -102,6 +102,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"jit_disk_baked", 64, false},            // baked code objects kept in the disk cache
     {"jit_cache", 0, true},                   // code-object cache directory ("" = /tmp/rtx_jit_<uid>)
     {"jit_flags", 0, true},                   // extra hiprtc options (part of the cache key)
+    {"jit_ilp", 1, false},                    // max-ILP scheduling of one-sample primary+shadow kernels
     {"setup_log", 0, false},                  // print the host time of each rtx_camera_set step
 };
 struct OptVal {
@@ -1887,6 +1888,14 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
         // boxes, keeps the mesh kernels' 4 (1.4 % slower at 5).
         opts.push_back("-URTX_LB_WAVES");
         opts.push_back("-DRTX_LB_WAVES(MESH,SEC)=6");
+    }
+    // one-sample flat scenes of primary and shadow rays: the scheduler's max-ILP strategy
+    // (TwoSpheresPlane 22.2 -> 22.0 us, three times on one box; MirrorRefraction within
+    // noise either way; it spills the mesh and multi-sample kernels' registers: TorusMesh
+    // +7 %, DepthOfField +8 %; profiles/r05/noslp/ab_sched_unroll.log, ab_ilp.log)
+    if (!mesh && !ext && !sec && kp.n_dof * kp.n_aa * kp.n_times == 1 && opt_on(OPT_JIT_ILP)) {
+        opts.push_back("-mllvm");
+        opts.push_back("-amdgpu-sched-strategy=max-ilp");
     }
     {  // option jit_flags (tools: cost probes, occupancy bounds); part of the cache key
         std::istringstream is(opt_str(OPT_JIT_FLAGS));
