@@ -31,7 +31,15 @@
  *     (HBM) pointers owned by the caller; the library never frees them.
  *   - rtx_render / rtx_intersect / rtx_occluded / rtx_fb_to_rgb8 are asynchronous on
  *     the given HIP stream (hipStream_t passed as void*; NULL = the default stream).
- *     Scene and camera uploads are synchronous.
+ *     Scene and camera uploads are synchronous: rtx_camera_set waits for the device to
+ *     go idle and copies its tables with a kernel on the null stream, so it must not be
+ *     called while any stream is capturing a graph.
+ *   - Renders of ONE scene must be stream-ordered (one stream, or events between them):
+ *     the hierarchy/texture scenes' split passes keep per-scene scratch (record arrays,
+ *     counters, the redo list) that every render of the scene reuses. A render may be
+ *     captured into a HIP graph once the scene has rendered eagerly at that size (the
+ *     scratch is allocated then); buffers a captured graph may use live until
+ *     rtx_scene_destroy.
  *   - One device per scene (the current HIP device at rtx_scene_create).
  *   - Numbers carry the reference's types: PyGLM vec3 values are float (fp32), Python
  *     scalars are double (fp64).
