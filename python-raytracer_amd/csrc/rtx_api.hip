@@ -1893,9 +1893,14 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
     // (TwoSpheresPlane 22.2 -> 22.0 us, three times on one box; MirrorRefraction within
     // noise either way; it spills the mesh and multi-sample kernels' registers: TorusMesh
     // +7 %, DepthOfField +8 %; profiles/r05/noslp/ab_sched_unroll.log, ab_ilp.log)
+    // With them, the kernel arguments preloaded into SGPRs (one dependent scalar load fewer
+    // at every wave's start: TwoSpheresPlane 22.08 -> 21.91 us, twice on one box,
+    // profiles/r05/noslp/ab_kernarg.log).
     if (!mesh && !ext && !sec && kp.n_dof * kp.n_aa * kp.n_times == 1 && opt_on(OPT_JIT_ILP)) {
         opts.push_back("-mllvm");
         opts.push_back("-amdgpu-sched-strategy=max-ilp");
+        opts.push_back("-mllvm");
+        opts.push_back("-amdgpu-kernarg-preload-count=16");
     }
     {  // option jit_flags (tools: cost probes, occupancy bounds); part of the cache key
         std::istringstream is(opt_str(OPT_JIT_FLAGS));
