@@ -184,9 +184,12 @@ def cpu_baseline_native(cfg, budget_s, threads=None):
 
 
 # Python-loop baseline: rows j = j0, j0 + R, j0 + 2R, ... (reference row index) of the
-# full-width frame, (R, j0) per config; every row for the 1080p configs whose whole frame
-# fits the budget. NovelScene1 (CSG + textures, ~270 samples/s per process): its middle row.
-PY_ROW_STRIDE = {"tsp1080": (1, 0), "mr1080": (1, 0), "tm1080": (16, 0), "dof4k": (270, 0), "ns1": (1024, 512)}
+# full-width frame, (R, j0[, C]) per config; every row for the 1080p configs whose whole
+# frame fits the budget. NovelScene1 (CSG + textures, ~270 samples/s per process): its
+# middle row. C: only the first C columns of each process's strip -- NovelScene2 (480
+# samples per pixel) and the 81,920-face mesh (a Python loop over every face per ray).
+PY_ROW_STRIDE = {"tsp1080": (1, 0), "mr1080": (1, 0), "tm1080": (16, 0), "dof4k": (270, 0), "ns1": (1024, 512),
+                 "ns2": (512, 256, 4), "blob1080": (1080, 540, 6)}
 _PY = {}
 
 
@@ -202,12 +205,14 @@ def _py_init(cfg):
 
 def _py_strip(args):
     """One np.array_split column strip (render.nu's --subimage k --tasks N process)."""
-    k, tasks, rows = args
+    k, tasks, rows, cols = args
     sc = _PY["scene"]
     ncol = len(np.array_split(np.arange(sc.width), tasks)[k])
+    if cols is not None:
+        ncol = min(ncol, cols)
     noise = np.random.RandomState(k).rand(ncol * len(rows) * sc.samples * sc.dof_samples * 3) if _PY["jitter"] else None
     t0 = time.perf_counter()
-    sc.render(k, tasks, rows=rows, noise=noise)
+    sc.render(k, tasks, rows=rows, noise=noise, cols=cols)
     return ncol * len(rows) * _PY["spp"], time.perf_counter() - t0
 
 
@@ -223,12 +228,13 @@ def cpu_baseline(cfg, processes=None):
     _, res, _, _ = CONFIGS[cfg]
     W, H = res
     P = processes or cpu_threads()
-    stride, j0 = PY_ROW_STRIDE[cfg]
+    stride, j0 = PY_ROW_STRIDE[cfg][:2]
+    cols = PY_ROW_STRIDE[cfg][2] if len(PY_ROW_STRIDE[cfg]) > 2 else None
     rows = list(range(j0, H, stride))
     with mp.get_context("fork").Pool(P, initializer=_py_init, initargs=(cfg,)) as pool:
         pool.map(_py_init, [cfg] * P)  # every worker built its scene before the clock starts
         t0 = time.perf_counter()
-        res_ = pool.map(_py_strip, [(k, P, rows) for k in range(P)], chunksize=1)
+        res_ = pool.map(_py_strip, [(k, P, rows, cols) for k in range(P)], chunksize=1)
         dt = time.perf_counter() - t0
     nsamp = sum(r[0] for r in res_)
     cpu = "unknown"
@@ -240,6 +246,8 @@ def cpu_baseline(cfg, processes=None):
     sample = "full %dx%d frame" % (W, H) if stride == 1 else \
         "rows %s (%d of %d) of the %dx%d frame" % (", ".join(str(r) for r in rows[:3]) + (", ..." if len(rows) > 3 else ""),
                                                    len(rows), H, W, H)
+    if cols is not None:
+        sample += ", the first %d columns of each process's strip" % cols
     return {"value": nsamp / dt / 1e6, "unit": "Mrays/s", "cores": P, "kind": "port",
             "sample": "%s, %d samples in %.1f s; %d processes, one np.array_split column strip each (as render.nu); "
                       "oracle/pyloop.py: the reference's per-sample Python loop, bit-identical to the C oracle; "

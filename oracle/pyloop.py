@@ -718,9 +718,10 @@ class PyLoopScene:
         return add(colour, mul(self.ambient, diffuse))
 
     # scene.py:35-79
-    def render(self, subimage=0, tasks=1, rows=None, noise=None):
+    def render(self, subimage=0, tasks=1, rows=None, noise=None, cols=None):
         """(strip_w, H, 3) float64 like Scene.render; ``rows`` (reference row indices,
-        y from the bottom) restricts the rendered rows (others stay 0)."""
+        y from the bottom) restricts the rendered rows (others stay 0), ``cols`` to the
+        strip's first ``cols`` columns (a bounded CPU-baseline sample)."""
         W, H = self.width, self.height
         strip = np.array_split(np.arange(W), tasks)[subimage]
         dx = (self.right - self.left) / W
@@ -735,7 +736,7 @@ class PyLoopScene:
         divisor = self.samples * self.dof_samples * len(self.motion_times)
         nz = 0
         x = self.left + (0.5 + strip[0]) * dx
-        for i in range(len(strip)):
+        for i in range(len(strip) if cols is None else min(cols, len(strip))):
             for j in rows:
                 colour = ZERO
                 base_dir = normalize(sub(add(scale(self.u, x), scale(self.v, ys[j])), scale(self.w, self.d)))
