@@ -1873,6 +1873,7 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
     if (out8) opts.push_back("-DRTX_OUT8=1");  // uint8 framebuffer (rtx_render_rgb8)
     // secondary-ray frames keep their material index in a register: 3 LDS words per frame
     if (sec && v.n_mats <= 64) opts.push_back("-DRTX_FRAME_MATBITS=6");
+    if (sec && !mesh && !ext) opts.push_back("-DRTX_DEFER_TIES=1");  // (rtx_trace.h closest_hit)
     opts.push_back(std::string("-DRTX_PRIMARY_BINS=") + (kp.S.bins_on ? "1" : "0"));
     opts.push_back(std::string("-DRTX_LIGHT_GRIDS=") + (v.lgrid_on ? "1" : "0"));
     opts.push_back(std::string("-DRTX_DIR_GRIDS=") + (kp.S.dsg_on ? "1" : "0"));

@@ -1728,6 +1728,11 @@ __device__ __forceinline__ void coop_mesh(const SceneView& S, const DObj& ob, in
 }
 #endif
 
+template <bool B>
+struct BoolTag {
+    static constexpr bool value = B;
+};
+
 // Origin-only terms of the plane and sphere shadow tests -- dot(p0 - o, n) per plane,
 // oc = o - c and dot(oc, oc) per sphere -- computed once per shading point and shared by
 // its lights (the same operations, once instead of per light). Scene-specialized kernels
@@ -1749,81 +1754,120 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
                        int32_t bin = -1, const OriginTerms* prim = nullptr, int32_t blane = -1) {
     Hit h{INFINITY, -1, 0};
     int oi = 0;
-    for (int k = 0; k < RTX_NPLANE(S); ++k, ++oi) {  // simple_geometry.py:105-120
-        if (RTX_PROBE(18)) continue;  // cost probe: no planes in closest_hit
-        const DObj ob = S.objs[oi];
-        const f3 n = ld3(ob.b);
-        const float denom = dot(d, n);
-#ifdef RTX_FIXED_COUNTS
-        const float num = prim ? prim->pnum[k] : dot(sub(moved(ob, ob.a, time), o), n);
-#else
-        const float num = dot(sub(moved(ob, ob.a, time), o), n);
-#endif
-        const float t32 = num / denom;
-        // abs(denom) > epsilon and t >= 0
-        const bool valid = fabsf(denom) >= kEps4Up && quot_nonneg(t32, num, denom);
-        offer(S, h, valid, t32, oi, 0, o, d, time);
-    }
-    // primary rays of a binned tile skip the spheres and boxes whose screen footprint
-    // misses the tile (rtx_api.hip primary_bins; wave-uniform)
-#if defined(RTX_PRIMARY_BINS) && !RTX_PRIMARY_BINS
-    constexpr uint32_t omask = ~0u;
-#else
-    const uint32_t omask = bin >= 0 ? S.bin_objmask[wave_uniform(bin)] : ~0u;
-#endif
-    for (int k = 0; k < RTX_NSPHERE(S); ++k, ++oi) {  // simple_geometry.py:20-46
-        if (!((omask >> (k & 15)) & 1u)) continue;
-        if (RTX_PROBE(7)) continue;  // cost probe: no spheres in the primary test
-        const DObj ob = S.objs[oi];
-        const f3 ctr = moved(ob, ob.a, time);
-        bool valid = false;
-        float t32 = INFINITY;
-        int32_t root = 0;
-#ifdef RTX_FIXED_COUNTS
-        const f3 oc = prim ? prim->soc[k] : sub(o, ctr);
-        const float q = prim ? prim->sq[k] : dot(oc, oc);
-#else
-        const f3 oc = sub(o, ctr);
-        const float q = dot(oc, oc);
-#endif
-        if (sphere_disc_sign_oc(d, oc, q, ob.r2f) >= 0) {  // fp64 only where a hit is possible
-            double b, s, two_a;
-            if (RTX_PROBE(4) ? sphere_roots(o, d, ctr, ob.r2, b, s, two_a) : sphere_roots_oc(d, oc, q, ob.r2, b, s, two_a)) {
-                double t = (-b - s) / two_a;
-                const bool near = t > 0.0;
-                // the far root only where some lane needs it (a ray from inside the sphere)
-                if (RTX_ANY(!near)) {
-                    unspeculated();
-                    if (!near) { t = (-b + s) / two_a; root = 1; }
-                }
-                valid = t > 0.0;
-                t32 = (float)t;
-            }
-        }
-        offer(S, h, valid, t32, oi, root, o, d, time);
-    }
+    // The flat objects. RTX_DEFER_TIES (flat scene-specialized kernels with secondary rays:
+    // MirrorRefraction 39.7 -> 38.8 us; TwoSpheresPlane measured 22.0 -> 27.7 us with it,
+    // DepthOfField and TorusMesh equal, profiles/r05/noslp/ab_defer_ties.log): the first pass
+    // takes strictly nearer hits only and notes an equal t (a tie the reference breaks by
+    // the fp64 t and scene order, offer()); a wave that saw one runs the exact pass again.
+    // h.t32 evolves the same in both (a tie never changes it), so without ties the first
+    // pass's result is offer()'s.
     RayInv ri{};
-    if (RTX_NBOX(S) > 0 || (MESH && RTX_NMESH(S) > 0)) ri = ray_inv(o, d);
-    for (int k = 0; k < RTX_NBOX(S); ++k, ++oi) {  // simple_geometry.py:188-249 (entry precedes exit)
-        if (!((omask >> (16 + (k & 15))) & 1u)) continue;
-        if (RTX_PROBE(17)) continue;  // cost probe: no boxes in closest_hit
-        const DObj ob = S.objs[oi];
-        const f3 mn = moved(ob, ob.a, time), mx = moved(ob, ob.b, time);
-        double start = 0.0;
-        int label = 0;
-        bool valid;
-        if (RTX_BOX_IV_CULL) {  // the intervals decide which lanes may hit before their best t
-            const SlabIv iv = box_slabs_iv(o, d, mn, mx, &ri);
-            const bool maybe = !box_iv_out(iv, h.t32);
-            if (!RTX_ANY(maybe)) continue;
-            valid = box_entry_iv(o, d, mn, mx, iv, maybe, start, label);
-        } else {
-            // the fp64 slabs only where some lane's ray may hit the box before its best t
-            const bool maybe = box_maybe_hit_obj(ob, mn, mx, o, ri, h.t32);
-            if (!RTX_ANY(maybe)) continue;
-            valid = box_entry(o, d, mn, mx, maybe, start, label, &ri);
+    bool tie = false;
+    auto flat = [&](auto exact_tag) {
+        constexpr bool EXACT = decltype(exact_tag)::value;
+        auto offer_ = [&](bool valid, float t32, int32_t obj, int32_t sb) {
+            if (EXACT) {
+                offer(S, h, valid, t32, obj, sb, o, d, time);
+            } else {
+                tie = tie || (valid && t32 == h.t32);
+                const bool take = valid && t32 < h.t32;
+                h.t32 = take ? t32 : h.t32;
+                h.obj = take ? obj : h.obj;
+                h.sub = take ? sb : h.sub;
+            }
+        };
+        for (int k = 0; k < RTX_NPLANE(S); ++k, ++oi) {  // simple_geometry.py:105-120
+            if (RTX_PROBE(18)) continue;  // cost probe: no planes in closest_hit
+            const DObj ob = S.objs[oi];
+            const f3 n = ld3(ob.b);
+            const float denom = dot(d, n);
+#ifdef RTX_FIXED_COUNTS
+            const float num = prim ? prim->pnum[k] : dot(sub(moved(ob, ob.a, time), o), n);
+#else
+            const float num = dot(sub(moved(ob, ob.a, time), o), n);
+#endif
+            const float t32 = num / denom;
+            // abs(denom) > epsilon and t >= 0
+            const bool valid = fabsf(denom) >= kEps4Up && quot_nonneg(t32, num, denom);
+            offer_(valid, t32, oi, 0);
         }
-        offer(S, h, valid, (float)start, oi, label, o, d, time);
+        // primary rays of a binned tile skip the spheres and boxes whose screen footprint
+        // misses the tile (rtx_api.hip primary_bins; wave-uniform)
+#if defined(RTX_PRIMARY_BINS) && !RTX_PRIMARY_BINS
+        constexpr uint32_t omask = ~0u;
+#else
+        const uint32_t omask = bin >= 0 ? S.bin_objmask[wave_uniform(bin)] : ~0u;
+#endif
+        for (int k = 0; k < RTX_NSPHERE(S); ++k, ++oi) {  // simple_geometry.py:20-46
+            if (!((omask >> (k & 15)) & 1u)) continue;
+            if (RTX_PROBE(7)) continue;  // cost probe: no spheres in the primary test
+            const DObj ob = S.objs[oi];
+            const f3 ctr = moved(ob, ob.a, time);
+            bool valid = false;
+            float t32 = INFINITY;
+            int32_t root = 0;
+#ifdef RTX_FIXED_COUNTS
+            const f3 oc = prim ? prim->soc[k] : sub(o, ctr);
+            const float q = prim ? prim->sq[k] : dot(oc, oc);
+#else
+            const f3 oc = sub(o, ctr);
+            const float q = dot(oc, oc);
+#endif
+            if (sphere_disc_sign_oc(d, oc, q, ob.r2f) >= 0) {  // fp64 only where a hit is possible
+                double b, s, two_a;
+                if (RTX_PROBE(4) ? sphere_roots(o, d, ctr, ob.r2, b, s, two_a) : sphere_roots_oc(d, oc, q, ob.r2, b, s, two_a)) {
+                    double t = (-b - s) / two_a;
+                    const bool near = t > 0.0;
+                    // the far root only where some lane needs it (a ray from inside the sphere)
+                    if (RTX_ANY(!near)) {
+                        unspeculated();
+                        if (!near) { t = (-b + s) / two_a; root = 1; }
+                    }
+                    valid = t > 0.0;
+                    t32 = (float)t;
+                }
+            }
+            offer_(valid, t32, oi, root);
+        }
+        if (RTX_NBOX(S) > 0 || (MESH && RTX_NMESH(S) > 0)) ri = ray_inv(o, d);
+        for (int k = 0; k < RTX_NBOX(S); ++k, ++oi) {  // simple_geometry.py:188-249 (entry precedes exit)
+            if (!((omask >> (16 + (k & 15))) & 1u)) continue;
+            if (RTX_PROBE(17)) continue;  // cost probe: no boxes in closest_hit
+            const DObj ob = S.objs[oi];
+            const f3 mn = moved(ob, ob.a, time), mx = moved(ob, ob.b, time);
+            double start = 0.0;
+            int label = 0;
+            bool valid;
+            if (RTX_BOX_IV_CULL) {  // the intervals decide which lanes may hit before their best t
+                const SlabIv iv = box_slabs_iv(o, d, mn, mx, &ri);
+                const bool maybe = !box_iv_out(iv, h.t32);
+                if (!RTX_ANY(maybe)) continue;
+                valid = box_entry_iv(o, d, mn, mx, iv, maybe, start, label);
+            } else {
+                // the fp64 slabs only where some lane's ray may hit the box before its best t
+                const bool maybe = box_maybe_hit_obj(ob, mn, mx, o, ri, h.t32);
+                if (!RTX_ANY(maybe)) continue;
+                valid = box_entry(o, d, mn, mx, maybe, start, label, &ri);
+            }
+            offer_(valid, (float)start, oi, label);
+        }
+    };
+#if !defined(RTX_DEFER_TIES)
+#define RTX_DEFER_TIES 0  // (rtx_api.hip jit_spec sets it for the secondary-ray kernels)
+#endif
+#if defined(RTX_FIXED_COUNTS) && RTX_DEFER_TIES
+    if (!MESH && !X && !COUNT) {
+        flat(BoolTag<false>{});
+        if (RTX_ANY(tie)) {
+            unspeculated();
+            h = Hit{INFINITY, -1, 0};
+            oi = 0;
+            flat(BoolTag<true>{});
+        }
+    } else
+#endif
+    {
+        flat(BoolTag<true>{});
     }
     if (MESH) {
         for (int k = 0; k < RTX_NMESH(S); ++k, ++oi) {  // mesh.py:72-119, faces in order

@@ -185,8 +185,19 @@ def many_roots_scene(seed, res=(48, 32), n_roots=40, n_spheres=20):
                        {"name": "p", "type": "point", "position": [3.0, 6.0, 4.0], "colour": [1.0, 1.0, 1.0], "power": 0.5}]}
 
 
-def tie_scene(res=(40, 30)):
-    """Coincident geometry: the first object in scene order must win closest-hit ties."""
+def tie_scene(res=(40, 30), mirror=False):
+    """Coincident geometry: the first object in scene order must win closest-hit ties.
+    mirror: a mirror sphere that reflects the tied objects (secondary rays meet the ties
+    too, and the scene runs the secondary-ray kernels)."""
+    sc = _tie_scene(res)
+    if mirror:
+        sc["materials"].append({"name": "m", "ID": 3, "type": "mirror", "diffuse": [0.2, 0.2, 0.2], "tint": 0.2})
+        sc["objects"].append({"name": "mirror", "type": "sphere", "radius": 0.8, "position": [0.0, 1.2, -2.0],
+                              "materials": [3]})
+    return sc
+
+
+def _tie_scene(res):
     return {"resolution": list(res), "ambient": [0.1, 0.1, 0.1],
             "camera": {"position": [0.0, 3.0, 6.0], "lookAt": [0.0, 0.0, 0.0], "up": [0.0, 1.0, 0.0], "fov": 50.0},
             "materials": [{"name": "a", "ID": 0, "diffuse": [1, 0, 0], "specular": [0.5, 0.5, 0.5], "hardness": 16},

@@ -292,11 +292,17 @@ def test_point_lights_scenes_match_oracle(seed, monkeypatch):
     assert np.array_equal(product_scene_dict(d).render(), img)
 
 
-def test_ties_follow_scene_order():
+@pytest.mark.parametrize("mirror", [False, True])
+def test_ties_follow_scene_order(mirror):
+    """Coincident objects: scene order breaks closest-hit ties (offer()); with a mirror the
+    secondary-ray kernel meets them too, through its deferred tie pass (RTX_DEFER_TIES)."""
     from common import oracle_render_dict, product_scene_dict
     from scenegen import tie_scene
-    d = tie_scene((80, 60))
-    assert compare(product_scene_dict(d).render(), oracle_render_dict(d))["frac_diff"] == 0.0
+    d = tie_scene((80, 60), mirror=mirror)
+    sc = product_scene_dict(d)
+    assert compare(sc.render(), oracle_render_dict(d))["frac_diff"] == 0.0
+    if mirror:
+        assert sc.last_kernel.startswith("rtx_jit_render_01"), sc.last_kernel
 
 
 HIER_CASES = [
