@@ -1873,7 +1873,17 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
     if (out8) opts.push_back("-DRTX_OUT8=1");  // uint8 framebuffer (rtx_render_rgb8)
     // secondary-ray frames keep their material index in a register: 3 LDS words per frame
     if (sec && v.n_mats <= 64) opts.push_back("-DRTX_FRAME_MATBITS=6");
-    if (sec && !mesh && !ext) opts.push_back("-DRTX_DEFER_TIES=1");  // (rtx_trace.h closest_hit)
+    if (sec && !mesh && !ext) {
+        opts.push_back("-DRTX_DEFER_TIES=1");  // (rtx_trace.h closest_hit)
+        // the frames of chain levels 0-5 in LDS (18 KB per block with 3-word frames), deeper
+        // ones in scratch, at <= 72 VGPRs: 7-8 blocks per CU instead of 5.
+        // MirrorRefraction 38.7 -> 36.4 us (twice on one box; levels 8/7/5/4/3 and 6-8 waves
+        // within 36.4-37.2 us, profiles/r05/noslp/ab_frame_levels*.log). Round 4 measured
+        // 8 levels at 6 waves equal: the SLP-free build (§6q) has the registers for it.
+        opts.push_back("-DRTX_FRAME_LDS_LEVELS=6");
+        opts.push_back("-URTX_LB_WAVES");
+        opts.push_back("-DRTX_LB_WAVES(MESH,SEC)=7");
+    }
     opts.push_back(std::string("-DRTX_PRIMARY_BINS=") + (kp.S.bins_on ? "1" : "0"));
     opts.push_back(std::string("-DRTX_LIGHT_GRIDS=") + (v.lgrid_on ? "1" : "0"));
     opts.push_back(std::string("-DRTX_DIR_GRIDS=") + (kp.S.dsg_on ? "1" : "0"));

@@ -2552,9 +2552,9 @@ RTX_HD f3 regular_lighting(const SceneView& S, f3 dir, f3 pos, f3 normal, const 
 static_assert(RTX_FRAME_MATBITS * kMaxDepth <= 64, "frame materials must fit one 64-bit word");
 constexpr int kFrameWords = RTX_FRAME_MATBITS ? 3 : 4;
 // Frames kept in LDS; deeper levels of a chain (rare) go to a per-lane private array
-// (scratch), so a smaller LDS stack lets more blocks share a CU. Experiment knob: 8 levels
-// give MirrorRefraction 6 instead of 5 waves/SIMD but measured equal (51.3 vs 50.4-51.1 us,
-// profiles/r02/s19/), so every level stays in LDS.
+// (scratch), so a smaller LDS stack lets more blocks share a CU. The scene-specialized
+// kernels of flat scenes with secondary rays keep 6 levels in LDS (rtx_api.hip jit_spec:
+// MirrorRefraction 38.7 -> 36.4 us); the precompiled kernels keep every level.
 #ifndef RTX_FRAME_LDS_LEVELS
 #define RTX_FRAME_LDS_LEVELS kMaxDepth
 #endif
