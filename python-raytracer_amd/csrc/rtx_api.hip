@@ -70,7 +70,7 @@ int fail(int code, const std::string& msg) {
 // rendering; they are not synchronised with renders running on other threads.
 enum Opt {
     OPT_SPLIT, OPT_SPLIT_BYTES, OPT_SPLIT_RATIO, OPT_BINS, OPT_HEAVY_TILES, OPT_LENS_BINS, OPT_LGRID, OPT_DSGRID, OPT_DSGRID_MIN,
-    OPT_SELF_SKIP, OPT_TILE_SCHED, OPT_XCD_MAP, OPT_PRIM_ORIGIN, OPT_SPP, OPT_SPP_MIN, OPT_JIT, OPT_JIT_BAKE, OPT_JIT_EXT,
+    OPT_SELF_SKIP, OPT_TILE_SCHED, OPT_XCD_MAP, OPT_TILE_BLOCK, OPT_PRIM_ORIGIN, OPT_SPP, OPT_SPP_MIN, OPT_JIT, OPT_JIT_BAKE, OPT_JIT_EXT,
     OPT_JIT_DUMP, OPT_JIT_IDLE_BAKED, OPT_JIT_DISK_BAKED, OPT_JIT_CACHE, OPT_JIT_FLAGS, OPT_JIT_ILP, OPT_SETUP_LOG, OPT_COUNT
 };
 struct OptDef {
@@ -91,6 +91,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"self_skip", 1, false},                  // plane / box self tests skipped where provably passing
     {"tile_sched", 1, false},                 // measured longest-first tile order
     {"xcd_map", 0, false},                    // XCD-aware block order of tile-mapped launches
+    {"tile_block", 64, false},                // threads per block of the secondary-ray / mesh tile kernels
     {"prim_origin", 1, false},                // host-computed origin terms of pinhole primary rays
     {"spp", -1, false},                       // sample-parallel mapping: -1 auto, 0 never, 1 always
     {"spp_min", 16, false},                   // auto: from this many samples per pixel (X scenes)
@@ -1725,6 +1726,16 @@ bool prim_origin_enabled() { return opt_on(OPT_PRIM_ORIGIN); }
 
 // The measured tile schedule (tile_schedule; option tile_sched).
 bool tile_sched_enabled() { return opt_on(OPT_TILE_SCHED); }
+// Threads per block of a scene-specialized tile-mapped kernel (one 8x8 tile per wave).
+// The secondary-ray and mesh kernels -- the tile-scheduled kinds, whose waves differ most in
+// length -- run in one-wave blocks (option tile_block, 64 or 256): MirrorRefraction 36.7 ->
+// 35.9 us, TorusMesh 47.4 -> 46.4 us; TwoSpheresPlane keeps 256 (64: 21.9 -> 22.3 us;
+// profiles/r05/noslp/abl_block_*.log).
+int jit_block(bool mesh, bool sec, bool ext, bool spp) {
+    if (ext) return kBlock<true>;
+    if (spp || !(mesh || sec)) return kBlock<false>;
+    return opt(OPT_TILE_BLOCK) == 64.0 ? 64 : kBlock<false>;
+}
 
 bool jit_enabled() { return opt_on(OPT_JIT); }
 
@@ -1890,6 +1901,10 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
     // (records and mesh data staged in LDS -- RTX_LDS_OBJS / RTX_LDS_TRIS kernels -- measured
     // slower; jit_flags can still request them)
     for (const char* m : kLibMacros) opts.push_back(m);
+    if (!ext && jit_block(mesh, sec, ext, spp) != kBlock<false>) {
+        opts.push_back("-URTX_BLOCK_FLAT");
+        opts.push_back("-DRTX_BLOCK_FLAT=" + std::to_string(jit_block(mesh, sec, ext, spp)));
+    }
     if (!sec && !ext && (!mesh || fc_mode == 1)) {
         // flat scenes and small meshes (every face box-culled): 6 waves/SIMD. With the
         // host-side box precomputes the DepthOfField kernel fits 80 VGPRs with no more
@@ -2097,6 +2112,7 @@ struct rtx_scene {
     struct Resolved {
         bool done = false;
         hipFunction_t fn = nullptr;
+        int block = 0;    // its threads per block (jit_block when resolved)
         std::string name;
         std::string key;  // its g_jit entry (released by free_camera)
     } resolved[16];
@@ -2768,7 +2784,7 @@ bool split_enabled() { return opt_on(OPT_SPLIT); }
 // order (MirrorRefraction 41.4 -> 38.6 us, TorusMesh 52.8 -> 49.7 us with orders measured
 // on the same box, profiles/r04/tile_order/; TwoSpheresPlane and DepthOfField gain
 // nothing). The order changes when tiles run, not what they compute.
-int tile_schedule(rtx_scene* s, hipStream_t st) {
+int tile_schedule(rtx_scene* s, hipStream_t st, uint32_t wpb) {
     if (s->tile_sched != 2) return RTX_OK;
     if (stream_capturing(st)) return RTX_OK;
     const int32_t n = s->kp.tile_n;
@@ -2788,9 +2804,12 @@ int tile_schedule(rtx_scene* s, hipStream_t st) {
     std::iota(order.begin(), order.end(), 0);
     std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return t[a] > t[b]; });
     s->tile_xcd = opt_on(OPT_XCD_MAP);  // (the frames that follow this table keep its layout)
-    // dispatch position p (block p / wpb) reads the entry of its slot (pixel_rc's xcd_block):
-    // the p-th dispatched wave renders the p-th longest tile, and each XCD reads its own lines
-    const uint32_t wpb = kBlock<false> / 64, nb = (uint32_t)((n + wpb - 1) / wpb);
+    // the launch's blocks: its waves are the table's nw entries (rtx_camera_set pads the
+    // tiles to whole 256-thread blocks), wpb per block. Dispatch position p (block p / wpb)
+    // reads the entry of its slot (pixel_rc's xcd_block): the p-th dispatched wave renders
+    // the p-th longest tile, and each XCD reads its own lines
+    const uint32_t nw = (uint32_t)((n + kBlock<false> / 64 - 1) / (kBlock<false> / 64) * (kBlock<false> / 64));
+    const uint32_t nb = nw / wpb;
     std::vector<int32_t> perm((size_t)nb * wpb);
     for (uint32_t p = 0; p < nb * wpb; ++p) {
         const uint32_t slot = (s->tile_xcd ? xcd_block(p / wpb, nb, wpb) : p / wpb) * wpb + p % wpb;
@@ -3007,6 +3026,7 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
     };
     rtx_scene::Resolved& rs = s->resolved[(out8 ? 8 : 0) | (cnt ? 4 : 0) | (jit ? 2 : 0) | (spp_mode ? 1 : 0)];
     if (!rs.done) {
+        rs.block = jit_block(s->has_mesh, s->has_secondary, s->has_ext, spp_mode);
         rs.fn = jit_render_kernel(s->device, s->view, s->kp, s->traits, s->has_mesh, s->has_secondary, s->has_ext,
                                   cnt, jit, spp_mode, out8, s->jit_baked, &rs.name, &rs.key);
         rs.done = true;
@@ -3020,14 +3040,16 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
         // schedule's state machine follows eager frames only)
         const bool capturing = whole && stream_capturing(st);
         if (whole && !capturing) {
-            if (int rc = tile_schedule(s, st)) return rc;
+            if (int rc = tile_schedule(s, st, (uint32_t)rs.block / 64)) return rc;
             L.tlog = s->tile_sched == 1;
         }
         if (whole) L.tperm = s->tile_sched == 3;
         if (L.tperm) L.xcd = s->tile_xcd ? 1 : 0;
         if (int rc = heavy_pass(!spp_mode)) return rc;
-        RTX_HIP(hipModuleLaunchKernel(rs.fn, (unsigned)nblocks, (unsigned)nframes, 1, blk, 1, 1,
-                                      s->has_ext ? (unsigned)(hbytes * blk) : 0u, st, args, nullptr));
+        // (a one-wave-block kernel: the same waves in four times the blocks)
+        const int64_t jblocks = rs.block == blk ? nblocks : nblocks * (blk / rs.block);  // (blk: 256 here)
+        RTX_HIP(hipModuleLaunchKernel(rs.fn, (unsigned)jblocks, (unsigned)nframes, 1, rs.block, 1, 1,
+                                      s->has_ext ? (unsigned)(hbytes * rs.block) : 0u, st, args, nullptr));
         if (L.tlog) {  // measured: sorted before the next whole frame
             if (!s->tile_event) RTX_HIP(hipEventCreateWithFlags(&s->tile_event, hipEventDisableTiming));
             RTX_HIP(hipEventRecord(s->tile_event, st));
