@@ -3019,7 +3019,7 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
     auto heavy_pass = [&](bool tiles) -> int {
         if (s->heavy_n <= 0 || !tiles || s->has_ext) return RTX_OK;
         for (int32_t f = 0; f < nframes; ++f)
-            hipLaunchKernelGGL(k_mesh_chunks, dim3((unsigned)((s->heavy_n + 3) / 4)), dim3(256), 0, st, kp, L,
+            hipLaunchKernelGGL(k_mesh_chunks, dim3((unsigned)s->heavy_n), dim3(64), 0, st, kp, L,  // (a wave per chunk)
                                s->d_heavy_items, s->heavy_n, s->d_mesh_hits);
         RTX_HIP(hipGetLastError());
         return RTX_OK;

@@ -742,7 +742,7 @@ __global__ __launch_bounds__(256) void k_occluded(SceneView S, int64_t n, const 
 // (gphase + k gstride) runs only the chunks of its tiles.
 __global__ __launch_bounds__(256) void k_mesh_chunks(const KParams* __restrict__ Pp, const Launch L,
                                                      const int2* __restrict__ items, int32_t n, uint2* __restrict__ out) {
-    const int32_t w = __builtin_amdgcn_readfirstlane((int32_t)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    const int32_t w = __builtin_amdgcn_readfirstlane((int32_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
     if (w >= n) return;
     const int2 it = items[w];
     const int32_t ty = it.x / Pp->S.bins_x;  // the tile's 8-row group
