@@ -1858,6 +1858,9 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
 #if defined(RTX_FIXED_COUNTS) && RTX_DEFER_TIES
     if (!MESH && !X && !COUNT) {
         flat(BoolTag<false>{});
+#if defined(RTX_TOOLS_BUILD) && defined(RTX_DEFER_PROBE)
+        if (RTX_DEFER_PROBE == 1) tie = false;  // cost probe: never redo (wrong at ties)
+#endif
         if (RTX_ANY(tie)) {
             unspeculated();
             h = Hit{INFINITY, -1, 0};
