@@ -1755,7 +1755,9 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
     Hit h{INFINITY, -1, 0};
     int oi = 0;
     // The flat objects. RTX_DEFER_TIES (flat scene-specialized kernels with secondary rays:
-    // MirrorRefraction 39.7 -> 38.8 us; TwoSpheresPlane measured 22.0 -> 27.7 us with it,
+    // MirrorRefraction 39.7 -> 38.8 us; TwoSpheresPlane measured 22.0 -> 27.7 us with it --
+    // no wave of it meets a tie, and without the exact pass's code it ran 21.6 us, so the
+    // cost is that code's presence; out of line (noinline) it spilled 400 B/lane --
     // DepthOfField and TorusMesh equal, profiles/r05/noslp/ab_defer_ties.log): the first pass
     // takes strictly nearer hits only and notes an equal t (a tie the reference breaks by
     // the fp64 t and scene order, offer()); a wave that saw one runs the exact pass again.
