@@ -1886,6 +1886,10 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
     if (sec && v.n_mats <= 64) opts.push_back("-DRTX_FRAME_MATBITS=6");
     if (sec && !mesh && !ext) {
         opts.push_back("-DRTX_DEFER_TIES=1");  // (rtx_trace.h closest_hit)
+        // hit_t64 inlined (no call in the kernel): MirrorRefraction 35.7 -> 35.3 us; the
+        // other kernels measured slower with it (TSP +2.3 %, TM +1.8 %, DOF +1.2 %,
+        // profiles/r05/noslp/ab_t64_inline.log)
+        opts.push_back("-DRTX_HIT_T64_INLINE=1");
         // the frames of chain levels 0-5 in LDS (18 KB per block with 3-word frames), deeper
         // ones in scratch, at <= 72 VGPRs: 7-8 blocks per CU instead of 5.
         // MirrorRefraction 38.7 -> 36.4 us (twice on one box; levels 8/7/5/4/3 and 6-8 waves

@@ -881,7 +881,18 @@ RTX_HD bool bv_maybe(const O& ob, f3 o, const RayInv& ri, float tcap) {
 
 // Exact fp64 t of a candidate, recomputed from the object exactly as during its test
 // (used only when two fp32 proxies tie; out of line to keep the hot loop's registers low).
-__host__ __device__ __attribute__((noinline)) inline double hit_t64(const SceneView& S, int32_t obj, int32_t sb, f3 o, f3 d, float time) {
+// (RTX_HIT_T64_INLINE, scene-specialized kernels: inlined, with only the object kinds the
+// scene has -- no call in the kernel, whose ABI constrains the whole kernel's registers)
+#if defined(RTX_FIXED_COUNTS) && defined(RTX_HIT_T64_INLINE) && RTX_HIT_T64_INLINE
+#define RTX_T64_ATTR __forceinline__
+#define RTX_T64_HAS_BOX (RTX_FIXED_NB > 0)
+#define RTX_T64_HAS_TRI (RTX_FIXED_NM > 0)
+#else
+#define RTX_T64_ATTR __attribute__((noinline))
+#define RTX_T64_HAS_BOX 1
+#define RTX_T64_HAS_TRI 1
+#endif
+__host__ __device__ RTX_T64_ATTR inline double hit_t64(const SceneView& S, int32_t obj, int32_t sb, f3 o, f3 d, float time) {
     const DObj ob = S.objs[obj];
     if (ob.type == OBJ_PLANE) {
         const f3 n = ld3(ob.b);
@@ -892,12 +903,13 @@ __host__ __device__ __attribute__((noinline)) inline double hit_t64(const SceneV
         sphere_roots(o, d, moved(ob, ob.a, time), ob.r2, b, s, two_a);
         return sb == 0 ? (-b - s) / two_a : (-b + s) / two_a;
     }
-    if (ob.type == OBJ_BOX) {
+    if (RTX_T64_HAS_BOX && ob.type == OBJ_BOX) {
         double start = 0.0, end = 0.0;
         int label = 0;
         box_slabs(o, d, moved(ob, ob.a, time), moved(ob, ob.b, time), start, label, end);
         return start;
     }
+    if (!RTX_T64_HAS_TRI) return INFINITY;  // (no other kind in the scene)
     const DTri T = S.tris[ob.tri_begin + sb];
     const f3 n = ld3(T.n);
     return (double)dot(sub(ld3(T.v0), o), n) / (double)dot(d, n);
