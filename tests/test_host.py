@@ -26,6 +26,27 @@ def test_library_exports_every_header_symbol():
     assert lib.rtx_abi_version() == N.ABI_VERSION
 
 
+def test_options_table_documented_and_round_trips():
+    """Every library option is named in INTEGRATION.md or DESIGN.md §6s, reads back what
+    was set (rtx_set_option / rtx_get_option, no GPU), and an unknown name or a malformed
+    number is refused."""
+    names = rtx.option_names()
+    docs = open(os.path.join(REPO, "DESIGN.md")).read() + open(os.path.join(REPO, "INTEGRATION.md")).read()
+    for n in names:
+        assert "`%s`" % n in docs, n
+    for n, v in (("tile_block", "256"), ("xcd_map", "1"), ("jit_ilp", "0"), ("split_bytes", "1073741824")):
+        old = rtx.get_option(n)
+        try:
+            rtx.set_option(n, v)
+            assert float(rtx.get_option(n)) == float(v), n
+        finally:
+            rtx.set_option(n, old)
+    with pytest.raises(N.RtxError):
+        rtx.set_option("no_such_option", "1")
+    with pytest.raises(N.RtxError):
+        rtx.set_option("bins", "not-a-number")
+
+
 def test_abi_struct_layouts_match_the_header():
     import hostemu
     lib = hostemu.lib()
