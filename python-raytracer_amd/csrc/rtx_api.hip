@@ -1890,6 +1890,7 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
         // other kernels measured slower with it (TSP +2.3 %, TM +1.8 %, DOF +1.2 %,
         // profiles/r05/noslp/ab_t64_inline.log)
         opts.push_back("-DRTX_HIT_T64_INLINE=1");
+        opts.push_back("-DRTX_TIE_CALL=1");  // (rtx_trace.h tie_takes)
         // the frames of chain levels 0-5 in LDS (18 KB per block with 3-word frames), deeper
         // ones in scratch, at <= 72 VGPRs: 7-8 blocks per CU instead of 5.
         // MirrorRefraction 38.7 -> 36.4 us (twice on one box; levels 8/7/5/4/3 and 6-8 waves

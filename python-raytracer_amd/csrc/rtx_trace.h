@@ -920,11 +920,30 @@ __host__ __device__ RTX_T64_ATTR inline double hit_t64(const SceneView& S, int32
 // any object order but in hit order within an object; a candidate replaces the record
 // iff its t is smaller, or equal with a smaller scene-order id. Proxies decide unless
 // they are equal; then the exact fp64 values (and the ids) do.
+// The tie rule in one out-of-line call (RTX_TIE_CALL, the secondary-ray kernels with
+// hit_t64 inlined: one call site per offer instead of two -- MirrorRefraction 35.6 ->
+// 35.0 us; in the one-sample kernel the call's register constraints spilled 400 B/lane,
+// profiles/r05/noslp/ab_tie_call.log): whether candidate (obj, sb) takes the tie from h.
+__host__ __device__ __attribute__((noinline)) inline bool tie_takes(const SceneView& S, const Hit& h, int32_t obj,
+                                                                  int32_t sb, f3 o, f3 d, float time) {
+    const double a = hit_t64(S, obj, sb, o, d, time);
+    if (h.obj < 0) return a < INFINITY;
+    const double b = hit_t64(S, h.obj, h.sub, o, d, time);
+    const DObj oa = S.objs[obj], ob = S.objs[h.obj];
+    const int32_t fa = oa.type == OBJ_MESH ? S.tri_orig[oa.tri_begin + sb] : 0;
+    const int32_t fb = ob.type == OBJ_MESH ? S.tri_orig[ob.tri_begin + h.sub] : 0;
+    return a < b || (a == b && (oa.oid < ob.oid || (oa.oid == ob.oid && fa < fb)));
+}
 RTX_HD void offer(const SceneView& S, Hit& h, bool valid, float t32, int32_t obj, int32_t sb, f3 o, f3 d,
                   float time) {
     bool take = valid && t32 < h.t32;
     const bool tie = valid && t32 == h.t32;
+#if defined(RTX_TIE_CALL) && RTX_TIE_CALL
+    if (tie) take = tie_takes(S, h, obj, sb, o, d, time);
+    if (false) {
+#else
     if (tie) {
+#endif
         const double a = hit_t64(S, obj, sb, o, d, time);
         if (h.obj < 0) {
             take = a < INFINITY;
