@@ -308,34 +308,44 @@ def timed(fn, steps, use_dist, sync=cuda_sync, device="cuda"):
     return max_over_ranks(t1 - t0, use_dist, device)
 
 
-def sharded_frame(sc, rank, world, steps, warmup, use_dist, device, sync=cuda_sync, stream=None, render_rows=None):
-    """ONE frame sharded over the ranks, frame by frame (the N > 1 value): every step renders
-    this rank's interleaved 8-row groups of the frame straight to uint8 (fused
-    rtx_render_groups_rgb8, one launch per frame) and gathers them to rank 0 (one RCCL
-    gather), awaited before the next frame starts; rank 0 puts the rows in image order. No
-    batching and no overlap across frames: the latency of one frame, the reference's
-    one-frame-per-run strip render + glue (render.nu:10-15, provided/glue.py:17-27).
-    Returns (seconds for `steps` frames, max over ranks; rank 0's last frame [H, W, 3])."""
-    from rtx.distributed import FrameGather
-    H, W = sc.vc.height, sc.vc.width
-    single = FrameGather(H, W, 3, world, rank, torch.uint8, device, interleave=True, dst=0)
-    if render_rows is None:
-        def render_rows(out):
-            sc.render_device(groups=(rank, world), out=out, stream=stream)
-    last = [None]
-
-    def one_frame():
-        if single.nrows:
-            render_rows(single.block)
-        w = single.start(async_op=True)
-        if w is not None:
-            w.wait()
-        if rank == 0:
-            last[0] = single.frame()
+def sharded_frame(sc, rank, world, steps, warmup, use_dist, device, sync=cuda_sync, stream=None, render_rows=None,
+                  graph=True, collective_at_one=False):
+    """ONE frame sharded over the ranks per step (the N > 1 value; rtx.distributed.FrameGraph):
+    every step renders this rank's rows of the frame straight to uint8 (fused, one launch),
+    gathers them to rank 0 (one RCCL gather) and, for interleaved rows, puts them in image
+    order on rank 0 -- recorded once as a HIP graph and replayed per frame, so a frame costs
+    one graph launch of host time. Frames are stream-ordered: each frame's gather completes
+    before the next frame renders. No batching and no overlap across frames: the latency of
+    one frame, the reference's one-frame-per-run strip render + glue (render.nu:10-15,
+    provided/glue.py:17-27). Partition: contiguous row blocks for one-sample frames (in
+    image order when N | H: no reorder), interleaved 8-row groups otherwise.
+    Returns (seconds for `steps` frames, max over ranks; rank 0's last frame [H, W, 3];
+    the loop's host issue cost)."""
+    from rtx.distributed import FrameGraph
+    fg = FrameGraph(sc, rank, world, dst=0, device=device, render_block=render_rows, graph=graph,
+                    collective_at_one=collective_at_one)
     for _ in range(warmup):
-        one_frame()
+        fg.step()
     sync()
-    return timed(one_frame, steps, use_dist, sync, device), last[0]
+    s = timed(fg.step, steps, use_dist, sync, device)
+    # host issue per frame (outside the timed region): the same loop with the clock stopped
+    # before the device finishes, per step() and as one rtx_graph_launch of all frames
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fg.step()
+    t1 = time.perf_counter()
+    sync()
+    t2 = time.perf_counter()
+    fg.run(steps, stream)
+    t3 = time.perf_counter()
+    sync()
+    last = fg.frame()
+    nrows = [len(r) for r in fg.g.rows]
+    info = {"graph": fg.graph is not None, "rows_per_rank": [min(nrows), max(nrows)], "partition": "interleaved 8-row groups" if fg.interleave else
+            "contiguous row blocks (np.array_split)", "in_order": bool(fg.g.in_order),
+            "host_issue_us_per_frame": round((t1 - t0) * 1e6 / steps, 3),
+            "host_issue_c_us_per_frame": round((t3 - t2) * 1e6 / steps, 3)}
+    return s, (last.clone() if last is not None else None), info
 
 
 def sharded_config_field(cfg, sc, rank, world, steps, warmup, use_dist, device, sync=cuda_sync, stream=None,
@@ -343,7 +353,7 @@ def sharded_config_field(cfg, sc, rank, world, steps, warmup, use_dist, device, 
     """The scaling config's sharded frame beside the metric's (DESIGN.md section 7:
     DepthOfField 4K is render-bound at every N, TwoSpheresPlane 1080p is link-bound at
     N = 2): the same one-frame-per-step loop as the value, on `sc`."""
-    s, _ = sharded_frame(sc, rank, world, steps, warmup, use_dist, device, sync, stream, render_rows)
+    s, _, _ = sharded_frame(sc, rank, world, steps, warmup, use_dist, device, sync, stream, render_rows)
     W, H = sc.vc.width, sc.vc.height
     return {"config": cfg, "workload": CONFIGS[cfg][3], "steps": steps, "frame_ms": round(s * 1e3 / steps, 5),
             "Mrays_s": round(W * H * sc.samples_per_pixel * steps / s / 1e6, 3),
@@ -352,7 +362,7 @@ def sharded_config_field(cfg, sc, rank, world, steps, warmup, use_dist, device, 
 
 
 def measure_sharded(sc, rank, world, steps, warmup, use_dist, device, sync=cuda_sync, stream=None,
-                    render_rows=None, render_block=None, render_block_k=None, graph=True):
+                    render_rows=None, render_block=None, render_block_k=None, graph=True, collective_at_one=False):
     """The N > 1 measurements (bench.py's multi-GPU leg; at N = 1 with --pipeline a
     rehearsal). Renderers default to the HIP kernels on this rank's GPU; the CPU tests
     inject the host emulation (tests/test_bench_multirank.py).
@@ -366,7 +376,8 @@ def measure_sharded(sc, rank, world, steps, warmup, use_dist, device, sync=cuda_
     from rtx.distributed import FrameExchange, FramePipeline
     H, W = sc.vc.height, sc.vc.width
     spp = sc.samples_per_pixel
-    frame_s, last_frame = sharded_frame(sc, rank, world, steps, warmup, use_dist, device, sync, stream, render_rows)
+    frame_s, last_frame, loop = sharded_frame(sc, rank, world, steps, warmup, use_dist, device, sync, stream,
+                                              render_rows, graph=graph, collective_at_one=collective_at_one)
 
     def run_frames(loop, n):
         if use_dist:
@@ -392,16 +403,18 @@ def measure_sharded(sc, rank, world, steps, warmup, use_dist, device, sync=cuda_
         pipe.step()
     pipe.flush()
     rank0_s = run_frames(pipe, steps)
-    nrows = [len(r) for r in ex.rows_all]
 
     def rate(s):
         return round(W * H * spp * steps / s / 1e6, 3)
     out = {
         "frame_s": frame_s,
         "frame_ms": round(frame_s * 1e3 / steps, 5),
-        "rows_per_rank": [min(nrows), max(nrows)],
-        "partition": "interleaved 8-row groups r, r+N, ... (rtx_render_groups_rgb8), reordered by rank 0",
-        "collective": "one torch.distributed.gather (RCCL) of the ranks' uint8 rows to rank 0 per frame, awaited",
+        "rows_per_rank": loop["rows_per_rank"],
+        "partition": loop["partition"] + (" (rank 0's buffer is the frame)" if loop["in_order"] else
+                                          ", reordered on rank 0"),
+        "collective": "one torch.distributed.gather (RCCL) of the ranks' uint8 rows to rank 0 per frame, stream-ordered",
+        "frame_loop": dict(loop, note="render + gather + reorder recorded once as a HIP graph (FrameGraph), replayed per "
+                                      "frame; host_issue: Python step() per frame / rtx_graph_launch of all frames"),
         "throughput": {
             "frame_ms": round(stream_s * 1e3 / steps, 5), "Mrays_s": rate(stream_s),
             "launch": ("one batched launch per group of N frames (rtx_render_groups_frames)" if ex.render_frames
@@ -413,7 +426,7 @@ def measure_sharded(sc, rank, world, steps, warmup, use_dist, device, sync=cuda_
             "frame_ms": round(rank0_s * 1e3 / steps, 5), "Mrays_s": rate(rank0_s),
             "note": "FramePipeline: every frame gathered to rank 0, double-buffered (its ingress bounds the rate)"},
         "headline": "value = ONE frame sharded over the N ranks (uint8 rows, fused) and gathered to rank 0, "
-                    "frame by frame, awaited: no batching or overlap across frames",
+                    "frame by frame (one HIP graph launch each), stream-ordered: no batching or overlap across frames",
     }
     return out, last_frame
 
@@ -496,6 +509,8 @@ def main():
             return len(os.listdir(jit_dir))
         except OSError:
             return 0
+    tc = time.perf_counter()
+    torch.zeros(1, device="cuda")  # the process's HIP context (not a scene cost)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     sc = make_scene(a.config)
@@ -515,15 +530,29 @@ def main():
     sc.render_device(out=fb)
     torch.cuda.synchronize()
     t5 = time.perf_counter()
-    setup = {"parse_ms": round((t1 - t0) * 1e3, 3), "scene_create_ms": round((t2 - t1) * 1e3, 3),
-             "camera_set_ms": round((t3 - t2) * 1e3, 3), "first_frame_ms": round((t5 - t4) * 1e3, 3),
-             "first_frame_jit": "compiled (hiprtc)" if n_cached() > cached0 else "code object from the disk cache",
-             "note": "outside the timed region; first_frame_ms includes one render"}
+    first_kernel = sc.last_kernel
+    sc.jit_wait()  # the specialized kernel (compiling on a host thread since the first frame)
+    sc.render_device(out=fb)
+    torch.cuda.synchronize()
+    t6 = time.perf_counter()
+    if first_kernel.startswith("rtx_jit_render_"):
+        how = "specialized kernel, compiled (hiprtc)" if n_cached() > cached0 else \
+            "specialized kernel, code object from the disk cache"
+    else:
+        how = "generic kernel %s while the specialized one compiles on a host thread (%s)" % (
+            first_kernel, "hiprtc" if n_cached() > cached0 else "code object from the disk cache")
+    setup = {"hip_context_ms": round((t0 - tc) * 1e3, 3), "parse_ms": round((t1 - t0) * 1e3, 3),
+             "scene_create_ms": round((t2 - t1) * 1e3, 3), "camera_set_ms": round((t3 - t2) * 1e3, 3),
+             "first_frame_ms": round((t5 - t4) * 1e3, 3), "first_frame_kernel": how,
+             "specialized_ready_ms": round((t6 - t4) * 1e3, 3), "specialized_kernel": sc.last_kernel,
+             "note": "outside the timed region; first_frame_ms includes one render; specialized_ready_ms: from the "
+                     "first frame's start to the end of the first frame with the specialized kernel"}
 
     # ray-segment census for the algorithmic byte model (separate counting launch)
     cnt = torch.zeros(16, dtype=torch.int64, device="cuda")
     sc.render_device(out=fb, counters=cnt)
     c = cnt.cpu().numpy()
+    sc.jit_wait()  # (no compile left running on a host thread during the timed regions)
     cast_rays = int(c[:10].sum())
     shadow_rays = int(c[10])
     segments = cast_rays + shadow_rays
@@ -535,6 +564,12 @@ def main():
     extra = {}
     if world == 1 and not a.pipeline:
         # N = 1: one step = one whole frame into the fp32 framebuffer
+        fb8 = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
+
+        def frame_u8():
+            sc.render_device(out=fb8, stream=stream)
+        frame_u8()  # the uint8 variant of the specialized kernel, compiled before any timing
+        sc.jit_wait()
         warm = clock_warmup(full_frame, a.clock_warmup_s, torch.cuda.synchronize)
         for _ in range(a.warmup):
             full_frame()
@@ -542,12 +577,9 @@ def main():
         wall_s = timed(full_frame, a.steps, use_dist)
         kern_ms = kernel_ms(full_frame, a.steps, stream)  # the render kernel alone, same launches
         kernel = sc.last_kernel
-        fb8 = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
-
-        def frame_u8():
-            sc.render_device(out=fb8, stream=stream)
-        frame_u8()  # (its first call may compile the uint8 variant of the specialized kernel)
-        torch.cuda.synchronize()
+        clock_warmup(frame_u8, min(0.1, a.clock_warmup_s), torch.cuda.synchronize)  # (its own, right before it)
+        for _ in range(a.warmup):
+            frame_u8()
         extra["rgb8"] = rgb8_field(frame_u8, a.steps, lambda fn, n: kernel_ms(fn, n, stream), W, H, spp,
                                    lambda: sc.last_kernel)
         rows_frac = 1.0
@@ -556,16 +588,26 @@ def main():
         # N > 1 (north star): one step = ONE frame sharded across the ranks (uint8 rows
         # rendered by every rank) and gathered to rank 0, awaited, frame by frame
         dev = torch.device("cuda", local)
-        from rtx.distributed import rank_rows
-        my_rows = rank_rows(H, world, rank, True)
+        from rtx.distributed import rank_rows, row_block
+        interleave = spp > 1  # the value loop's partition (rtx.distributed.FrameGraph)
+        my_rows = rank_rows(H, world, rank, interleave)
+        r0, nr = row_block(H, world, rank)
         warm_out = torch.empty((max(len(my_rows), 1), W, 3), dtype=torch.uint8, device="cuda")
+
+        def rank_render(out):
+            if interleave:
+                sc.render_device(groups=(rank, world), out=out, stream=stream)
+            else:
+                sc.render_device(row0=r0, nrows=nr, out=out, stream=stream)
 
         def own_rows():  # clock warm-up on this rank's own rows (no collective)
             if len(my_rows):
-                sc.render_device(groups=(rank, world), out=warm_out, stream=stream)
+                rank_render(warm_out[:len(my_rows)])
+        own_rows()
+        sc.jit_wait()  # (the specialized kernel compiles on a host thread meanwhile)
         warm = clock_warmup(own_rows, a.clock_warmup_s, torch.cuda.synchronize)
         mg, _ = measure_sharded(sc, rank, world, a.steps, a.warmup, use_dist, dev, stream=stream,
-                                graph=not a.no_graph)
+                                graph=not a.no_graph, collective_at_one=a.pipeline)
         wall_s = mg.pop("frame_s")
         # breakdown (outside the timed region): this rank's render alone, fp32 (the kernel
         # the roofline below prices) and uint8 (the one the frame loop runs), from HIP events
@@ -573,8 +615,9 @@ def main():
 
         def fp32_rows():
             if len(my_rows):
-                sc.render_device(groups=(rank, world), out=rank_fb[:len(my_rows)], stream=stream)
+                rank_render(rank_fb[:len(my_rows)])
         fp32_rows()  # (its first call may compile the fp32 variant of the specialized kernel)
+        sc.jit_wait()
         torch.cuda.synchronize()
         kern_ms = max_over_ranks(kernel_ms(fp32_rows, a.steps, stream), use_dist)
         kernel = sc.last_kernel

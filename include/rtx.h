@@ -38,8 +38,10 @@
  *     the hierarchy/texture scenes' split passes keep per-scene scratch (record arrays,
  *     counters, the redo list) that every render of the scene reuses. A render may be
  *     captured into a HIP graph once the scene has rendered eagerly at that size (the
- *     scratch is allocated then); buffers a captured graph may use live until
- *     rtx_scene_destroy.
+ *     scratch is allocated then); the scene's own buffers live until rtx_scene_destroy.
+ *     A captured graph is INVALID after rtx_camera_set: the camera's tables may move and
+ *     the kernel it launches was specialized on the old camera (and may be unloaded), so
+ *     record it again after every camera upload.
  *   - One device per scene (the current HIP device at rtx_scene_create).
  *   - Numbers carry the reference's types: PyGLM vec3 values are float (fp32), Python
  *     scalars are double (fp64).
@@ -266,6 +268,22 @@ int rtx_set_option(const char* name, const char* value);
 int rtx_get_option(const char* name, char* value, int32_t cap);
 /* Name of option i (0, 1, ...; NULL past the last). */
 const char* rtx_option_name(int32_t i);
+
+/* Scene-specialized kernels compiled on a host thread (option jit_async, default 1; no
+ * reference counterpart): a scene's first renders launch the precompiled generic kernel,
+ * which renders the same bytes, while hiprtc compiles the specialized one; a later render
+ * that finds the compile done switches to it. rtx_jit_wait picks up the scene's finished
+ * compiles -- block != 0: waits for all of them first -- and returns how many are still
+ * compiling (0 once every kernel the scene's camera has rendered with is resolved). */
+int32_t rtx_jit_wait(rtx_scene* scene, int32_t block);
+
+/* Multi-GPU frame loop (no reference counterpart; the reference's strip renders and glue,
+ * render.nu:10-15 + provided/glue.py:17-27, as one HIP graph per frame): launches the
+ * instantiated graph graph_exec (a hipGraphExec_t, e.g. one rank's render + RCCL gather of
+ * a frame captured by rtx.distributed.FrameGraph) n times in order on hip_stream, from C,
+ * so a frame costs one hipGraphLaunch of host time. Asynchronous; RTX_ERR_INVALID for a
+ * null graph or n < 0. */
+int rtx_graph_launch(void* graph_exec, int32_t n, void* hip_stream);
 
 #ifdef __cplusplus
 }

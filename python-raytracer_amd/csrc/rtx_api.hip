@@ -20,6 +20,7 @@
 #include <dirent.h>
 #include <fstream>
 #include <functional>
+#include <future>
 #include <list>
 #include <map>
 #include <numeric>
@@ -71,7 +72,8 @@ int fail(int code, const std::string& msg) {
 enum Opt {
     OPT_SPLIT, OPT_SPLIT_BYTES, OPT_SPLIT_RATIO, OPT_BINS, OPT_HEAVY_TILES, OPT_LENS_BINS, OPT_LGRID, OPT_DSGRID, OPT_DSGRID_MIN,
     OPT_SELF_SKIP, OPT_TILE_SCHED, OPT_XCD_MAP, OPT_TILE_BLOCK, OPT_PRIM_ORIGIN, OPT_SPP, OPT_SPP_MIN, OPT_JIT, OPT_JIT_BAKE, OPT_JIT_EXT,
-    OPT_JIT_DUMP, OPT_JIT_IDLE_BAKED, OPT_JIT_DISK_BAKED, OPT_JIT_CACHE, OPT_JIT_FLAGS, OPT_JIT_ILP, OPT_SETUP_LOG, OPT_COUNT
+    OPT_JIT_DUMP, OPT_JIT_IDLE_BAKED, OPT_JIT_DISK_BAKED, OPT_JIT_CACHE, OPT_JIT_FLAGS, OPT_JIT_ILP, OPT_JIT_ASYNC,
+    OPT_SETUP_LOG, OPT_COUNT
 };
 struct OptDef {
     const char* name;
@@ -104,6 +106,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"jit_cache", 0, true},                   // code-object cache directory ("" = /tmp/rtx_jit_<uid>)
     {"jit_flags", 0, true},                   // extra hiprtc options (part of the cache key)
     {"jit_ilp", 1, false},                    // max-ILP scheduling of one-sample primary+shadow kernels
+    {"jit_async", 1, false},                  // compile on a host thread; the generic kernel renders meanwhile
     {"setup_log", 0, false},                  // print the host time of each rtx_camera_set step
 };
 struct OptVal {
@@ -1973,77 +1976,62 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
     return true;
 }
 
-hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& kp, const SceneTraits& tr, bool mesh,
-                                bool sec, bool ext, bool cnt, bool jit, bool spp, bool out8, const std::string& baked,
-                                std::string* name_out, std::string* key_out) {
-    if (!jit_enabled()) return nullptr;
-    const std::string arch = device_arch(device);
-    if (arch.empty()) return nullptr;
-    JitSpec sp;
-    if (!jit_spec(arch, v, kp, tr, mesh, sec, ext, cnt, jit, spp, out8, baked, sp)) return nullptr;
-    const std::string& name = sp.name;
-    const std::string& src = sp.src;
-    const std::vector<std::string>& opts = sp.opts;
-    std::string key = src;
-    for (const auto& o : opts) key += "\n" + o;
-    *name_out = name;
-    const std::string dkey = key + "\n#device " + std::to_string(device);
-    std::lock_guard<std::mutex> lock(g_jit_mu);
+// Scene-specialized kernels compiled on a host thread (option jit_async, the default): a
+// scene's first frames render with the precompiled generic kernel -- the same bytes
+// (tests/test_gpu_parity.py test_scene_specialized_kernel_equals_generic) -- while hiprtc
+// compiles (~0.3 s), and the render that finds the compile done loads and launches the
+// specialized kernel (jit_poll). A cold process's first TwoSpheresPlane 1080p frame then
+// costs a generic launch instead of a compile. rtx_jit_wait blocks until they are ready
+// (bench.py's timed region, graph captures). One compile at a time (g_compile_mu); the
+// jobs of a key are shared by the scenes that ask for it (g_jit_jobs, by device key).
+std::mutex g_compile_mu;
+std::mutex g_jobs_mu;
+std::map<std::string, std::shared_future<std::string>> g_jit_jobs;
+
+// hiprtc's code object of a spec ("" when it fails to compile), stored in the disk cache.
+std::string jit_compile(const JitSpec& sp, const std::string& path, const std::string& dir) {
+    std::lock_guard<std::mutex> lock(g_compile_mu);
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, sp.src.c_str(), "rtx_jit_render.hip", kJitNumHeaders, kJitHeaderSrcs,
+                            kJitHeaderNames) != HIPRTC_SUCCESS)
+        return std::string();
+    std::vector<const char*> copts;
+    for (const auto& o : sp.opts) copts.push_back(o.c_str());
+    const hiprtcResult rc = hiprtcCompileProgram(prog, (int)copts.size(), copts.data());
+    if (rc != HIPRTC_SUCCESS) {
+        size_t n = 0;
+        hiprtcGetProgramLogSize(prog, &n);
+        std::string log(n, '\0');
+        hiprtcGetProgramLog(prog, &log[0]);
+        fprintf(stderr, "librtx: scene-specialized kernel failed to compile, using the generic one:\n%s\n",
+                log.c_str());
+        hiprtcDestroyProgram(&prog);
+        return std::string();
+    }
+    size_t n = 0;
+    hiprtcGetCodeSize(prog, &n);
+    std::string code(n, '\0');
+    hiprtcGetCode(prog, &code[0]);
+    hiprtcDestroyProgram(&prog);
+    if (!path.empty()) {
+        const std::string tmp = path + "." + std::to_string((long)getpid());
+        std::ofstream f(tmp, std::ios::binary);
+        if (f.write(code.data(), (std::streamsize)code.size())) {
+            f.close();
+            (void)rename(tmp.c_str(), path.c_str());
+            if (sp.baked) jit_prune_disk(dir);
+        }
+    }
+    return code;
+}
+
+// The loaded kernel of device key dkey: an existing module (one more scene holds it) or
+// code loaded now; nullptr when it fails to load. Caller holds g_jit_mu.
+hipFunction_t jit_load_locked(const std::string& dkey, const std::string& code, const std::string& name, bool baked) {
     auto it = g_jit.find(dkey);
     if (it != g_jit.end()) {
         if (it->second.refs++ == 0 && it->second.baked) g_jit_idle.remove(dkey);
-        *key_out = dkey;
         return it->second.fn;
-    }
-    std::string all = key;
-    for (int h = 0; h < kJitNumHeaders; ++h) all += kJitHeaderSrcs[h];
-    char hash[32];
-    snprintf(hash, sizeof(hash), "%016zx", std::hash<std::string>{}(all));
-    const bool is_baked = sp.baked;
-    const std::string dir = jit_cache_dir();
-    const std::string path = dir.empty() ? "" : dir + (is_baked ? "/rtx_b_" : "/rtx_") + hash + ".co";
-    std::string code;
-    if (!path.empty()) {
-        std::ifstream f(path, std::ios::binary);
-        if (f) { std::stringstream ss; ss << f.rdbuf(); code = ss.str(); }
-    }
-    if (opt_on(OPT_JIT_DUMP)) {  // tools/jit_resource.sh
-        fprintf(stderr, "librtx: jit %s:", name.c_str());
-        for (const auto& o : opts) fprintf(stderr, " '%s'", o.c_str());
-        fprintf(stderr, "\n%s", src.c_str());
-    }
-    if (code.empty()) {
-        hiprtcProgram prog;
-        if (hiprtcCreateProgram(&prog, src.c_str(), "rtx_jit_render.hip", kJitNumHeaders, kJitHeaderSrcs,
-                                kJitHeaderNames) != HIPRTC_SUCCESS)
-            return nullptr;
-        std::vector<const char*> copts;
-        for (const auto& o : opts) copts.push_back(o.c_str());
-        const hiprtcResult rc = hiprtcCompileProgram(prog, (int)copts.size(), copts.data());
-        if (rc != HIPRTC_SUCCESS) {
-            size_t n = 0;
-            hiprtcGetProgramLogSize(prog, &n);
-            std::string log(n, '\0');
-            hiprtcGetProgramLog(prog, &log[0]);
-            fprintf(stderr, "librtx: scene-specialized kernel failed to compile, using the generic one:\n%s\n",
-                    log.c_str());
-            hiprtcDestroyProgram(&prog);
-            return nullptr;
-        }
-        size_t n = 0;
-        hiprtcGetCodeSize(prog, &n);
-        code.resize(n);
-        hiprtcGetCode(prog, &code[0]);
-        hiprtcDestroyProgram(&prog);
-        if (!path.empty()) {
-            const std::string tmp = path + "." + std::to_string((long)getpid());
-            std::ofstream f(tmp, std::ios::binary);
-            if (f.write(code.data(), (std::streamsize)code.size())) {
-                f.close();
-                (void)rename(tmp.c_str(), path.c_str());
-                if (is_baked) jit_prune_disk(dir);
-            }
-        }
     }
     JitEntry e;
     hipError_t he = hipModuleLoadData(&e.mod, code.data());
@@ -2053,11 +2041,115 @@ hipFunction_t jit_render_kernel(int device, const SceneView& v, const KParams& k
                 name.c_str(), hipGetErrorString(he));
         return nullptr;
     }
-    e.baked = is_baked;
+    e.baked = baked;
     e.refs = 1;
     g_jit[dkey] = e;
-    *key_out = dkey;
     return e.fn;
+}
+
+}  // namespace
+
+// A resolved kernel variant of a scene's camera: the specialized kernel, or the generic one
+// while its compile runs on a host thread (pending) or for good (fn == nullptr).
+struct JitSlot {
+    bool done = false;
+    hipFunction_t fn = nullptr;
+    int block = 0;    // its threads per block (jit_block when resolved)
+    std::string name;
+    std::string key;  // its g_jit entry (released by free_camera)
+    bool pending = false;
+    std::shared_future<std::string> fut;  // the compile (pending)
+    std::string dkey;                     // the device key it loads under (pending)
+    bool baked = false;
+};
+
+namespace {
+
+// Resolves slot r: the specialized kernel from memory or the disk cache, or a compile --
+// started on a host thread (jit_async: r.pending, the generic kernel renders meanwhile) or
+// waited for. r.fn == nullptr and !r.pending: the generic kernel.
+void jit_render_kernel(int device, const SceneView& v, const KParams& kp, const SceneTraits& tr, bool mesh, bool sec,
+                       bool ext, bool cnt, bool jit, bool spp, bool out8, const std::string& baked, JitSlot& r) {
+    r.fn = nullptr;
+    r.pending = false;
+    if (!jit_enabled()) return;
+    const std::string arch = device_arch(device);
+    if (arch.empty()) return;
+    JitSpec sp;
+    if (!jit_spec(arch, v, kp, tr, mesh, sec, ext, cnt, jit, spp, out8, baked, sp)) return;
+    std::string key = sp.src;
+    for (const auto& o : sp.opts) key += "\n" + o;
+    r.name = sp.name;
+    const std::string dkey = key + "\n#device " + std::to_string(device);
+    {
+        std::lock_guard<std::mutex> lock(g_jit_mu);
+        auto it = g_jit.find(dkey);
+        if (it != g_jit.end()) {
+            if (it->second.refs++ == 0 && it->second.baked) g_jit_idle.remove(dkey);
+            r.key = dkey;
+            r.fn = it->second.fn;
+            return;
+        }
+    }
+    if (opt_on(OPT_JIT_DUMP)) {  // tools/jit_resource.sh
+        fprintf(stderr, "librtx: jit %s:", sp.name.c_str());
+        for (const auto& o : sp.opts) fprintf(stderr, " '%s'", o.c_str());
+        fprintf(stderr, "\n%s", sp.src.c_str());
+    }
+    std::shared_future<std::string> fut;
+    {
+        std::lock_guard<std::mutex> lock(g_jobs_mu);
+        auto jt = g_jit_jobs.find(dkey);
+        if (jt != g_jit_jobs.end()) {
+            fut = jt->second;  // another scene's compile of the same kernel
+        } else {
+            std::string all = key;
+            for (int h = 0; h < kJitNumHeaders; ++h) all += kJitHeaderSrcs[h];
+            char hash[32];
+            snprintf(hash, sizeof(hash), "%016zx", std::hash<std::string>{}(all));
+            const std::string dir = jit_cache_dir();
+            const std::string path = dir.empty() ? "" : dir + (sp.baked ? "/rtx_b_" : "/rtx_") + hash + ".co";
+            std::string code;
+            if (!path.empty()) {
+                std::ifstream f(path, std::ios::binary);
+                if (f) { std::stringstream ss; ss << f.rdbuf(); code = ss.str(); }
+            }
+            if (!code.empty()) {
+                std::lock_guard<std::mutex> jl(g_jit_mu);
+                r.fn = jit_load_locked(dkey, code, sp.name, sp.baked);
+                if (r.fn) r.key = dkey;
+                return;
+            }
+            for (auto e = g_jit_jobs.begin(); e != g_jit_jobs.end();)  // finished jobs nobody picked up
+                e = e->second.wait_for(std::chrono::seconds(0)) == std::future_status::ready ? g_jit_jobs.erase(e)
+                                                                                               : std::next(e);
+            fut = std::async(std::launch::async, [sp, path, dir] { return jit_compile(sp, path, dir); }).share();
+            g_jit_jobs[dkey] = fut;
+        }
+    }
+    r.pending = true;
+    r.fut = fut;
+    r.dkey = dkey;
+    r.baked = sp.baked;
+}
+
+// Picks up slot r's finished compile (wait: blocks until it is done): loads the kernel, or
+// settles on the generic one when the compile failed.
+void jit_poll(JitSlot& r, bool wait) {
+    if (!r.pending) return;
+    if (!wait && r.fut.wait_for(std::chrono::seconds(0)) != std::future_status::ready) return;
+    const std::string& code = r.fut.get();
+    r.pending = false;
+    {
+        std::lock_guard<std::mutex> lock(g_jobs_mu);
+        g_jit_jobs.erase(r.dkey);
+    }
+    if (!code.empty()) {
+        std::lock_guard<std::mutex> lock(g_jit_mu);
+        r.fn = jit_load_locked(r.dkey, code, r.name, r.baked);
+        if (r.fn) r.key = r.dkey;
+    }
+    r.fut = std::shared_future<std::string>();
 }
 
 }  // namespace
@@ -2110,17 +2202,12 @@ struct rtx_scene {
     std::vector<DBound> tr_bounds;
     std::vector<DSGrid> tr_grids;
     bool tr_grids_on = false, tr_dsg_off = false;
+    double tr_dsg_min = 0.0;
     void* d_dsg_cells = nullptr;
     // the kernel resolved for each (counters, jitter, sample-parallel) variant of the
     // current camera: looked up (and compiled) once per camera, not per frame; nullptr
     // after a lookup means the generic kernel
-    struct Resolved {
-        bool done = false;
-        hipFunction_t fn = nullptr;
-        int block = 0;    // its threads per block (jit_block when resolved)
-        std::string name;
-        std::string key;  // its g_jit entry (released by free_camera)
-    } resolved[16];
+    JitSlot resolved[16];
     std::string last_kernel;  // name of the kernel the last render call launched
     std::string jit_baked;    // the scene records as constant arrays (jit_baked_records)
     // fp32 staging of the rgb8 entry points when no scene-specialized kernel is available
@@ -2208,7 +2295,7 @@ void free_camera(rtx_scene* s) {
     s->cam_set = false;
     for (auto& r : s->resolved) {  // specialized on the camera's sample counts
         jit_release(r.key);
-        r = rtx_scene::Resolved{};
+        r = JitSlot{};
     }
 }
 
@@ -2339,6 +2426,23 @@ int rtx_get_option(const char* name, char* value, int32_t cap) {
 }
 
 const char* rtx_option_name(int32_t i) { return i >= 0 && i < OPT_COUNT ? kOpts[i].name : nullptr; }
+
+int32_t rtx_jit_wait(rtx_scene* s, int32_t block) {
+    if (!s) return fail(RTX_ERR_INVALID, "rtx_jit_wait: null scene");
+    int32_t n = 0;
+    for (JitSlot& r : s->resolved) {
+        jit_poll(r, block != 0);
+        n += r.pending ? 1 : 0;
+    }
+    return n;
+}
+
+int rtx_graph_launch(void* graph_exec, int32_t n, void* stream) {
+    if (!graph_exec || n < 0) return fail(RTX_ERR_INVALID, "rtx_graph_launch: null graph or n < 0");
+    for (int32_t i = 0; i < n; ++i)
+        RTX_HIP(hipGraphLaunch(static_cast<hipGraphExec_t>(graph_exec), static_cast<hipStream_t>(stream)));
+    return RTX_OK;
+}
 
 const char* rtx_last_error(void) { return g_last_error.c_str(); }
 
@@ -2477,7 +2581,9 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     slog.mark("convert");
     // what depends on the frame's time range only: computed again when it changes
     const bool dsg_off = !opt_on(OPT_DSGRID);  // every shadow ray tests every object
-    if (!s->tr_valid || s->tr_lo != *mm.first || s->tr_hi != *mm.second || s->tr_dsg_off != dsg_off) {
+    const double dsg_min = opt(OPT_DSGRID_MIN);  // (dir_shadow_grids reads it)
+    if (!s->tr_valid || s->tr_lo != *mm.first || s->tr_hi != *mm.second || s->tr_dsg_off != dsg_off ||
+        s->tr_dsg_min != dsg_min) {
         s->tr_bounds.clear();
         if (!s->h_nodes.empty())  // hierarchy bounds over the frame's motion-time range
             s->tr_bounds = compute_bounds(s->h_nodes, s->h_objs, s->h_tris, *mm.first, *mm.second);
@@ -2486,6 +2592,7 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
         size_t ncells = 0;
         s->tr_grids.clear();
         s->tr_dsg_off = dsg_off;
+        s->tr_dsg_min = dsg_min;
         s->tr_grids_on = !dsg_off && dir_shadow_grids(s->h_bins, s->tr_bounds, *mm.first, *mm.second, s->tr_grids,
                                                       cells, &rects, &ncells);
         (void)hipDeviceSynchronize();  // (frames of the previous camera may still read the cells)
@@ -3008,33 +3115,41 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
     };
     int64_t nblocks = blocks(spp_mode);
     if (nblocks > 0x7fffffff || blocks(false) > 0x7fffffff) return fail(RTX_ERR_INVALID, "rtx_render: launch too large");
-    {  // RTX_TILE_ORDER 2 (experiment): a multiplier coprime to the launch's wave count
+    {
+#if RTX_TILE_ORDER == 2  // (experiment builds only): a multiplier coprime to the launch's wave count
         const uint64_t T = (uint64_t)nblocks * (blk / 64) * RTX_PPL;
         uint64_t m = std::max<uint64_t>(1, (uint64_t)((double)T * 0.6180339887498949));
         while (T > 1 && std::gcd(m, T) != 1) ++m;
         L.perm = (uint32_t)(T > 1 ? m % T : 1);
+#else
+        L.perm = 1;
+#endif
         L.pix0 = 0;
         L.tperm = 0;
         L.tlog = 0;
         L.xcd = opt_on(OPT_XCD_MAP) ? 1 : 0;
         L.redo = RedoList{nullptr, nullptr, nullptr};
     }
-    // the heavy tiles' chunks of every frame of a tile-mapped launch, just before it (the
-    // sample-parallel and split kernels pass no pixel-in-tile and walk the lists)
+    // the heavy tiles' chunks of a tile-mapped launch, just before it (the sample-parallel
+    // and split kernels pass no pixel-in-tile and walk the lists). One pass serves every
+    // frame of a batched launch: the frames share the camera, and the chunks test the mesh
+    // at times[0] (meshes do not move, provided/geometry/mesh.py ignores speed)
     auto heavy_pass = [&](bool tiles) -> int {
         if (s->heavy_n <= 0 || !tiles || s->has_ext) return RTX_OK;
-        for (int32_t f = 0; f < nframes; ++f)
-            hipLaunchKernelGGL(k_mesh_chunks, dim3((unsigned)s->heavy_n), dim3(64), 0, st, kp, L,  // (a wave per chunk)
-                               s->d_heavy_items, s->heavy_n, s->d_mesh_hits);
+        hipLaunchKernelGGL(k_mesh_chunks, dim3((unsigned)s->heavy_n), dim3(64), 0, st, kp, L,  // (a wave per chunk)
+                           s->d_heavy_items, s->heavy_n, s->d_mesh_hits);
         RTX_HIP(hipGetLastError());
         return RTX_OK;
     };
-    rtx_scene::Resolved& rs = s->resolved[(out8 ? 8 : 0) | (cnt ? 4 : 0) | (jit ? 2 : 0) | (spp_mode ? 1 : 0)];
+    JitSlot& rs = s->resolved[(out8 ? 8 : 0) | (cnt ? 4 : 0) | (jit ? 2 : 0) | (spp_mode ? 1 : 0)];
     if (!rs.done) {
         rs.block = jit_block(s->has_mesh, s->has_secondary, s->has_ext, spp_mode);
-        rs.fn = jit_render_kernel(s->device, s->view, s->kp, s->traits, s->has_mesh, s->has_secondary, s->has_ext,
-                                  cnt, jit, spp_mode, out8, s->jit_baked, &rs.name, &rs.key);
+        jit_render_kernel(s->device, s->view, s->kp, s->traits, s->has_mesh, s->has_secondary, s->has_ext, cnt, jit,
+                          spp_mode, out8, s->jit_baked, rs);
+        if (rs.pending && !opt_on(OPT_JIT_ASYNC) && !stream_capturing(st)) jit_poll(rs, true);
         rs.done = true;
+    } else if (rs.pending && !stream_capturing(st)) {
+        jit_poll(rs, false);  // (a capture records the kernel that runs now: no module load inside it)
     }
     if (rs.fn && jit_enabled()) {
         void* args[] = {(void*)&kp, (void*)&L};

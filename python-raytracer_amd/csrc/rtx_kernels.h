@@ -737,8 +737,8 @@ __global__ __launch_bounds__(256) void k_occluded(SceneView S, int64_t n, const 
 }
 
 #if !defined(RTX_EXT_TU)  // defined once, in rtx_api.hip
-// The heavy tiles' chunks of this frame (one wave per chunk, 4 per block), before the render
-// kernel: items (bin, chunk). A launch of rows (row0, nrows) or 8-row groups
+// The heavy tiles' chunks (one wave per chunk, launched as one-wave blocks), before the
+// render kernel: items (bin, chunk). A launch of rows (row0, nrows) or 8-row groups
 // (gphase + k gstride) runs only the chunks of its tiles.
 __global__ __launch_bounds__(256) void k_mesh_chunks(const KParams* __restrict__ Pp, const Launch L,
                                                      const int2* __restrict__ items, int32_t n, uint2* __restrict__ out) {
@@ -775,9 +775,16 @@ __global__ __launch_bounds__(256) void k_dsg_fill(const DSRect* __restrict__ r, 
     const int64_t gg = (int64_t)G * G, off = c / gg * gg;
     const int32_t q = (int32_t)(c - off), jy = q / G, ix = q - jy * G;
     DSCell v{0u, 0u};
-    for (int32_t k = 0; k < nr; ++k) {
+    // the rectangles come grid by grid (off ascending, dir_shadow_grids): this grid's range
+    int32_t lo = 0, hi = nr;
+    while (lo < hi) {
+        const int32_t mid = (lo + hi) >> 1;
+        if (r[mid].off < off) lo = mid + 1;
+        else hi = mid;
+    }
+    for (int32_t k = lo; k < nr && r[k].off == off; ++k) {
         const DSRect R = r[k];
-        if (R.off == off && ix >= R.i0 && ix <= R.i1 && jy >= R.j0 && jy <= R.j1) {
+        if (ix >= R.i0 && ix <= R.i1 && jy >= R.j0 && jy <= R.j1) {
             v.obj |= R.bit;
             v.root |= R.root;
         }

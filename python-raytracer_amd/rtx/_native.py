@@ -89,7 +89,8 @@ _lib = None
 EXPORTS = ["rtx_abi_version", "rtx_last_error", "rtx_scene_create", "rtx_scene_destroy", "rtx_camera_set",
            "rtx_render", "rtx_render_groups", "rtx_group_rows", "rtx_intersect", "rtx_occluded", "rtx_fb_to_rgb8",
            "rtx_render_rgb8", "rtx_render_groups_rgb8", "rtx_last_kernel", "rtx_render_frames",
-           "rtx_render_groups_frames", "rtx_jit_modules", "rtx_set_option", "rtx_get_option", "rtx_option_name"]
+           "rtx_render_groups_frames", "rtx_jit_modules", "rtx_set_option", "rtx_get_option", "rtx_option_name",
+           "rtx_graph_launch", "rtx_jit_wait"]
 
 
 def load():
@@ -124,7 +125,7 @@ def load():
             if not hasattr(lib, fn):
                 continue  # (an earlier round's library, see below)
             if fn not in ("rtx_abi_version", "rtx_last_error", "rtx_last_kernel", "rtx_group_rows", "rtx_jit_modules",
-                          "rtx_option_name"):
+                          "rtx_option_name", "rtx_jit_wait"):
                 getattr(lib, fn).restype = C.c_int
         lib.rtx_last_kernel.argtypes = [vp]
         lib.rtx_last_kernel.restype = C.c_char_p
@@ -141,6 +142,10 @@ def load():
             lib.rtx_get_option.argtypes = [C.c_char_p, C.c_char_p, C.c_int32]
             lib.rtx_option_name.argtypes = [C.c_int32]
             lib.rtx_option_name.restype = C.c_char_p
+        if hasattr(lib, "rtx_graph_launch"):
+            lib.rtx_graph_launch.argtypes = [vp, C.c_int32, vp]
+            lib.rtx_jit_wait.argtypes = [vp, C.c_int32]
+            lib.rtx_jit_wait.restype = C.c_int32
         _lib = lib
         return lib
 

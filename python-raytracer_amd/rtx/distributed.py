@@ -13,6 +13,8 @@ on its GPU (``rtx_fb_to_rgb8``: main.py:33's truncation, 4x fewer bytes on the w
 gathered to rank 0 with one collective (RCCL over xGMI on MI355X; gloo in the CPU tests),
 which puts the rows back in image order with one index_select.
 """
+import ctypes
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -134,6 +136,135 @@ def render_frame(scene, rank, world, render_rows=None, dtype=torch.float32, dst=
     if dtype == torch.uint8 and block.dtype != torch.uint8:
         block = to_rgb8(block)
     return gather_rows(block, H, world, rank, dst=dst, group=group, interleave=interleave)
+
+
+class FrameGraph:
+    """ONE frame sharded over the ranks per step, gathered to ``dst`` and awaited before the
+    next step (bench.py's N > 1 value; the reference's strip renders + glue,
+    render.nu:10-15, provided/glue.py:17-27), issued without per-frame Python: this rank's
+    render of its rows (uint8, main.py:33's conversion fused), the RCCL gather
+    (FrameGather) and, on ``dst``, the reorder into image order are recorded ONCE as a HIP
+    graph and replayed per frame -- ``step()`` is one graph launch, ``run(n)`` launches n
+    frames from C (rtx_graph_launch: one hipGraphLaunch of host time per frame).
+
+    Partition: contiguous np.array_split row blocks for one-sample frames (``interleave``
+    None and samples_per_pixel == 1): with N | H they arrive in image order and the gathered
+    buffer IS the frame; interleaved 8-row groups otherwise (render-bound multi-sample
+    frames balance better), put in order by an index_select recorded into the graph.
+
+    The graph bakes in the scene's device buffers: it is recorded again when the scene's
+    upload generation changes (a camera upload or an edit re-upload, checked per ``step``;
+    ``run`` checks once). ``graph=False`` (or a CPU device: the gloo tests' host
+    emulation) issues the same three steps eagerly. ``collective_at_one``: issue the
+    (one-rank) gather even at world 1, so a one-rank group records RCCL's calls too
+    (tests/test_gpu_frame_loop.py); otherwise world 1 has no collective at all.
+    ``render_block(out)`` fills this rank's rows (uint8 [nrows, W, 3]) -- the CPU tests
+    inject the host emulation."""
+
+    def __init__(self, scene, rank, world, dst=0, group=None, device=None, interleave=None, render_block=None,
+                 graph=True, collective_at_one=False):
+        H, W = scene.vc.height, scene.vc.width
+        device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if interleave is None:
+            interleave = scene.samples_per_pixel > 1
+        self.scene, self.rank, self.world, self.dst, self.interleave = scene, rank, world, dst, interleave
+        self.g = FrameGather(H, W, 3, world, rank, torch.uint8, device, interleave=interleave, dst=dst, group=group)
+        self.rows = self.g.rows[rank]
+        self.collective = world > 1 or collective_at_one
+        self.out = None
+        if rank == dst and not self.g.in_order:
+            self.out = torch.empty((H, W, 3), dtype=torch.uint8, device=device)
+        if render_block is None:
+            if interleave:
+                def render_block(out):
+                    scene.render_device(groups=(rank, world), out=out)
+            else:
+                r0, n = row_block(H, world, rank)
+
+                def render_block(out):
+                    scene.render_device(row0=r0, nrows=n, out=out)
+        self.render_block = render_block
+        self.graph_on = graph and device.type == "cuda"
+        self.graph = None
+        self._state = None
+
+    def _issue(self):
+        """The frame's three steps, in stream order on the current stream."""
+        g = self.g
+        if g.nrows:
+            self.render_block(g.block)
+        if self.collective:
+            if self.rank != self.dst:
+                dist.gather(g.send, dst=self.dst, group=g.group)
+            else:
+                dist.gather(g.send, gather_list=g.recv_list, dst=self.dst, group=g.group)
+        if self.out is not None:
+            flat = g.recv.view((g.world * g.maxrows,) + tuple(g.recv.shape[2:]))
+            torch.index_select(flat, 0, g.index, out=self.out)
+
+    def _scene_state(self):
+        sc = self.scene
+        if hasattr(sc, "_set_camera"):  # a changed camera or scene is uploaded (new tables) first
+            sc._set_camera(0, 1)
+        return getattr(sc, "_gen", None)
+
+    def capture(self):
+        """Record the frame as a HIP graph: the specialized kernels are compiled and the
+        frame issued eagerly first (allocations, the tile schedule's measuring frames), then
+        recorded without executing. Scenes whose uint8 renders run the generic kernels
+        (which stage through a library scratch buffer) stay eager."""
+        if hasattr(self.scene, "jit_wait"):
+            self._issue()
+            self.scene.jit_wait()
+        for _ in range(3):
+            self._issue()
+        torch.cuda.synchronize()
+        self._state = self._scene_state()
+        if self.g.nrows and not getattr(self.scene, "last_kernel", "rtx_jit_render_").startswith("rtx_jit_render_"):
+            self.graph_on = False
+            self.graph = None
+            return
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, capture_error_mode="thread_local"):
+            self._issue()
+        torch.cuda.synchronize()
+        self.graph = gr
+
+    def step(self):
+        """Issue one frame (asynchronous; frames are stream-ordered, so each one's gather is
+        complete before the next frame's render writes the buffers)."""
+        if not self.graph_on:
+            self._issue()
+            return
+        if self.graph is None or self._scene_state() != self._state:
+            self.capture()
+            if not self.graph_on:
+                self._issue()
+                return
+        self.graph.replay()
+
+    def run(self, n, stream=None):
+        """Issue n frames: one rtx_graph_launch call (n hipGraphLaunch from C) when the frame
+        is a graph, else n eager frames."""
+        if n <= 0:
+            return
+        if self.graph_on and (self.graph is None or self._scene_state() != self._state):
+            self.capture()
+        if not self.graph_on:
+            for _ in range(n):
+                self._issue()
+            return
+        from . import _native as N
+        st = stream if stream is not None else torch.cuda.current_stream()
+        N.call("rtx_graph_launch", ctypes.c_void_p(self.graph.raw_cuda_graph_exec()), int(n),
+               ctypes.c_void_p(st.cuda_stream))
+
+    def frame(self):
+        """The last frame on ``dst`` ([H, W, 3] uint8, valid until the next step), None
+        elsewhere. Synchronize the stream first to read it."""
+        if self.rank != self.dst:
+            return None
+        return self.out if self.out is not None else self.g.frame()
 
 
 class FramePipeline:
@@ -348,6 +479,10 @@ class FrameExchange:
             return
         for j in range(self.world):
             self.render_block(self.slot(buf, j), self.rows, j)
+        if hasattr(self.scene, "jit_wait"):  # the specialized kernels (compiling on a host thread)
+            self.scene.jit_wait()
+            for j in range(self.world):
+                self.render_block(self.slot(buf, j), self.rows, j)
         torch.cuda.synchronize()
         if not getattr(self.scene, "last_kernel", "rtx_jit_render_").startswith("rtx_jit_render_"):
             # the generic kernels' uint8 renders stage through a library scratch buffer that

@@ -12,12 +12,14 @@ import os
 import numpy as np
 
 from . import f32 as F
+from .track import TList, Tracked
 
 epsilon = 10 ** (-4)  # geometry/__init__.py:12
 
 
-class Geometry:
-    """geometry/__init__.py:38-63."""
+class Geometry(Tracked):
+    """geometry/__init__.py:38-63. Attribute edits, in-place array writes and changes of
+    TList attributes are tracked (rtx.track), so a Scene re-uploads an edited object."""
     shadow_epsilon = 10 ** (-4)
 
     def __init__(self, name, gtype, materials, speed):
@@ -135,7 +137,7 @@ class Mesh(Geometry):
         return "Mesh(%s)" % self.name
 
 
-class BoundingSphere:
+class BoundingSphere(Tracked):
     """bounding_volumes.py:12-16 (the cull itself runs on the device: mesh_bv)."""
 
     def __init__(self, center, radius, geometry):
@@ -144,7 +146,7 @@ class BoundingSphere:
         self.geometry = geometry
 
 
-class BoundingAABB:
+class BoundingAABB(Tracked):
     """bounding_volumes.py:43-47."""
 
     def __init__(self, minpos, maxpos, geometry):
@@ -169,7 +171,7 @@ class Hierarchy(Geometry):
     def __init__(self, name, gtype, materials, hierarchy_type, t, r, s, speed):
         super().__init__(name, gtype, materials, speed)
         self.hierarchy_type = hierarchy_type
-        self.children = []
+        self.children = TList()
         self.make_matrices(t, r, s)
 
     def make_matrices(self, t, r, s):

@@ -10,6 +10,7 @@ import weakref
 import numpy as np
 
 from . import f32 as F
+from .track import Tracked
 
 
 class Ray:
@@ -29,8 +30,8 @@ class Ray:
         return "Ray(origin: %s, dir: %s)" % (self.origin, self.direction)
 
 
-class Material:
-    """helperclasses.py:28-47."""
+class Material(Tracked):
+    """helperclasses.py:28-47 (edits are tracked: rtx.track)."""
 
     def __init__(self, name, specular, diffuse, hardness, ID, mat_type="diffuse", mat_tint=0.0):
         self.name = name
@@ -51,8 +52,8 @@ class Material:
             self.name, self.mat_type, self.specular, self.diffuse, self.hardness, self.ID)
 
 
-class Light:
-    """helperclasses.py:50-59."""
+class Light(Tracked):
+    """helperclasses.py:50-59 (edits are tracked: rtx.track)."""
 
     def __init__(self, ltype, name, colour, vector, power):
         self.type = ltype
@@ -194,7 +195,8 @@ class ViewportCamera:
         self._bump()
 
     def _bump(self):
-        object.__setattr__(self, "_version", self._version + 1)
+        # (a deep copy restores motion_times before _version)
+        object.__setattr__(self, "_version", self.__dict__.get("_version", 0) + 1)
 
     def set_motion(self, time, motion_samples, motion_final):
         dt = time / motion_samples

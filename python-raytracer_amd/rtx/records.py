@@ -19,6 +19,7 @@ Materials (ID, name, mat_type, diffuse, specular, hardness, tint, refr_index) an
 (type, colour, vector, power) are read the same way (helperclasses.py:28-59).
 """
 import ctypes as C
+import hashlib
 
 import numpy as np
 
@@ -212,3 +213,12 @@ def desc_bytes(desc):
         t = desc.textures[i]
         out.append(b"%d,%d" % (t.width, t.height) + C.string_at(t.rgb, 3 * t.width * t.height))
     return out
+
+
+def desc_digest(desc):
+    """A digest of desc_bytes: equal for descriptors the library would upload alike."""
+    h = hashlib.blake2b(digest_size=16)
+    for b in desc_bytes(desc):
+        h.update(len(b).to_bytes(8, "little"))
+        h.update(b)
+    return h.digest()

@@ -18,6 +18,7 @@ import torch
 from . import _native as N
 from . import f32 as F
 from . import records
+from . import track
 from .helperclasses import sunflower, sunflower_many
 
 DEFAULT_SEED = 0x5EED
@@ -103,6 +104,10 @@ class _NativeScene:
 
 
 class Scene:
+    # the attributes whose values the uploaded records are made of (with the objects,
+    # materials and lights they hold): assigning one counts the edit epoch up (rtx.track)
+    _RECORDS = ("objects", "materials", "lights", "ambient")
+
     def __init__(self, vc, jitter, samples, ambient, lights, materials, objects):
         self.vc = vc
         self.jitter = jitter
@@ -116,6 +121,18 @@ class Scene:
         self._native = None
         self._cam_key = None
         self._gen = next(_GENERATION)  # upload generation: new on every re-create / camera upload
+        self._digest = None            # digest of the uploaded descriptor's bytes
+        self._epoch = -1               # rtx.track epoch at the last check against the upload
+        self._tracked = False          # every record reports its edits (rtx.track.scene_tracked)
+
+    def __setattr__(self, name, value):
+        if name in self._RECORDS:
+            if isinstance(value, np.ndarray) and not isinstance(value, track.TArray):
+                value = value.view(track.TArray)
+            object.__setattr__(self, name, value)
+            track.bump()
+            return
+        object.__setattr__(self, name, value)
 
     @classmethod
     def from_reference(cls, ref):
@@ -142,6 +159,18 @@ class Scene:
             return ""
         return N.load().rtx_last_kernel(self._native.h).decode()
 
+    def jit_wait(self, block=True):
+        """rtx_jit_wait: the scene-specialized kernels compile on a host thread (option
+        jit_async) while the generic kernel renders the same bytes; this picks up finished
+        compiles -- block=True: waits for them first -- and returns how many are still
+        compiling. Call it before timing frames or capturing them into a graph."""
+        if self._native is None or not self._native.h:
+            return 0
+        n = N.load().rtx_jit_wait(self._native.h, 1 if block else 0)
+        if n < 0:
+            N.check("rtx_jit_wait", n)
+        return n
+
     # ------------------------------------------------------------------ scene upload
     def scene_desc(self):
         """Flatten the objects into the rtx_scene_desc ABI arrays (scene order kept;
@@ -150,10 +179,28 @@ class Scene:
         return records.scene_desc(self.objects, self.materials, self.lights, self.ambient)
 
     def native(self):
-        if self._native is None or self._native.device != torch.cuda.current_device():
-            self._native = _NativeScene(self.scene_desc())
+        """The uploaded scene (rtx_scene_create), kept current with the description: the
+        reference reads every object, material and light on every render
+        (provided/scene.py:86-88, :148, :161-164), so an edit since the upload re-uploads
+        the scene. A scene whose records all report their edits (this package's parser and
+        classes, rtx.track) is checked with one epoch compare and flattened again only after
+        some edit; other scenes (the reference's own objects, Scene.from_reference) are
+        flattened and compared on every call. Either way the upload is redone only when the
+        descriptor's bytes differ."""
+        dev = torch.cuda.current_device()
+        nat = self._native
+        if nat is not None and nat.device == dev and self._tracked and track.epoch() == self._epoch:
+            return nat
+        ep = track.epoch()
+        desc = self.scene_desc()
+        digest = records.desc_digest(desc)
+        if nat is None or nat.device != dev or digest != self._digest:
+            self._native = _NativeScene(desc)
             self._cam_key = None
             self._gen = next(_GENERATION)
+            self._digest = digest
+        self._epoch = ep
+        self._tracked = track.scene_tracked(self.objects, self.materials, self.lights, self.ambient)
         return self._native
 
     # ------------------------------------------------------------------ camera tables
@@ -336,7 +383,7 @@ class Scene:
         o = torch.as_tensor(np.ascontiguousarray(np.asarray(origins, np.float32).reshape(-1, 3).T)).cuda()
         d = torch.as_tensor(np.ascontiguousarray(np.asarray(directions, np.float32).reshape(-1, 3).T)).cuda()
         n = o.shape[1]
-        tm = torch.as_tensor(np.ascontiguousarray(np.broadcast_to(np.asarray(t_max, np.float64), (n,)))).cuda()
+        tm = torch.as_tensor(np.array(np.broadcast_to(np.asarray(t_max, np.float64), (n,)))).cuda()
         occ = torch.empty(n, dtype=torch.uint8, device="cuda")
         vp = C.c_void_p
         N.call("rtx_occluded", nat.h, n, vp(o.data_ptr()), vp(d.data_ptr()), vp(tm.data_ptr()), float(time),

@@ -31,6 +31,7 @@ from . import f32 as F
 from . import geometry as geom
 from . import helperclasses as hc
 from .scene import Scene
+from .track import TList
 
 # Optional camera sections: (JSON key, fields, fallbacks, message). A missing section or
 # field takes every fallback of the section (scene_parser.py:67-96).
@@ -121,7 +122,7 @@ class _SceneBuilder:
         return self.materials
 
     def materials_of(self, spec):
-        return [m for i in spec.get("materials", []) for m in self.materials if m.ID == i]
+        return TList(m for i in spec.get("materials", []) for m in self.materials if m.ID == i)
 
     # ------------------------------------------------------------ geometry
     def asset(self, path):
@@ -221,7 +222,8 @@ def load_scene(infile, verbose=True):
     materials = b.read_materials()
     objects = b.objects()
     log("Parsing complete")
-    sc = Scene(vc, b.jitter, b.samples, b.ambient, lights, materials, objects)
+    # the scene's own lists, tracked (rtx.track): edits between renders are re-uploaded
+    sc = Scene(vc, b.jitter, b.samples, b.ambient, TList(lights), TList(materials), TList(objects))
     for g in objects:
         g.set_scene(sc)
     return sc

@@ -1,6 +1,12 @@
 import os
 import sys
 
+# The tests pin which kernel renders: scene-specialized kernels compile before the render
+# that needs them returns (the product default, option jit_async 1, renders with the
+# generic kernel meanwhile; tests/test_gpu_jit_cache.py covers that path). Read by the
+# library once, at its first option lookup.
+os.environ.setdefault("RTX_JIT_ASYNC", "0")
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 for p in (REPO, os.path.join(REPO, "python-raytracer_amd"), HERE):

@@ -45,9 +45,10 @@ def _worker(rank, world, port, res, steps, out_q):
         calls[0] += 1
         return cache[key]
 
-    mine = rank_rows(res[1], world, rank, True)
+    # the value loop (rtx.distributed.FrameGraph): one-sample frames in contiguous row blocks
+    mine = rank_rows(res[1], world, rank, sc.samples_per_pixel > 1)
 
-    def render_rows(out):  # the value loop: this rank's interleaved groups
+    def render_rows(out):  # the value loop: this rank's rows
         out.copy_(rows_u8(mine))
 
     def render_block(out, rows):  # FramePipeline
@@ -92,7 +93,10 @@ def test_bench_sharded_frame_loop(world, res):
     assert mg0["frame_s"] > 0 and mg0["frame_ms"] == round(mg0["frame_s"] * 1e3 / steps, 5)
     W, H = res
     assert mg0["throughput"]["Mrays_s"] > 0 and mg0["gather_to_rank0"]["Mrays_s"] > 0
-    assert mg0["rows_per_rank"] == [min(len(r) for r in _parts(H, world)), max(len(r) for r in _parts(H, world))]
+    blocks = [len(b) for b in np.array_split(np.arange(H), world)]
+    assert mg0["rows_per_rank"] == [min(blocks), max(blocks)]
+    loop = mg0["frame_loop"]
+    assert loop["partition"].startswith("contiguous") and not loop["graph"]  # (gloo: eager)
     # the fields the 1 -> N comparison needs: the scaling config's sharded frame at N > 1 ...
     sc_f = mg0["scaling_config"]
     assert sc_f["config"] == "dof4k" and sc_f["frame_ms"] > 0 and sc_f["Mrays_s"] > 0
@@ -128,11 +132,3 @@ def test_bench_n1_line_has_rgb8_frame():
     f = bench.rgb8_field(frame_u8, 2, timer, res[0], res[1], 1, lambda: "hostemu")
     assert f["frame_ms"] > 0 and f["Mrays_s"] > 0 and f["kernel"] == "hostemu"
     assert np.array_equal(out["f"].numpy(), O.to_png_array(oracle_render("TwoSpheresPlane", res)))
-
-
-def _parts(H, world):
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    sys.path.insert(0, os.path.join(os.path.dirname(here), "python-raytracer_amd"))
-    from rtx.scene import group_rows
-    return [group_rows(H, world, r) for r in range(world)]

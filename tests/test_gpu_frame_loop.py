@@ -93,3 +93,35 @@ def test_frame_exchange_graph_mode_recaptures_after_camera_change(pg):
     assert not np.array_equal(want_a, want_b)
     for k, f in got:
         assert np.array_equal(f.cpu().numpy(), want_a if k < 2 else want_b), k
+
+
+@pytest.mark.parametrize("name,interleave", [("TwoSpheresPlane", None), ("MirrorRefraction", True)])
+def test_frame_graph_replays_render_and_gather(pg, name, interleave):
+    """bench.py's N > 1 value loop (rtx.distributed.FrameGraph): this rank's render, the RCCL
+    gather (issued even at world 1: collective_at_one) and -- for interleaved rows -- rank
+    0's reorder, recorded once as a HIP graph and replayed per frame (step) or launched
+    from C (run, rtx_graph_launch). Every frame is the published PNG; the graph is
+    recorded again after a camera change."""
+    from rtx.distributed import FrameGraph
+    sc = product_scene(name)
+    want = _png(name)
+    fg = FrameGraph(sc, 0, 1, interleave=interleave, collective_at_one=True)
+    assert fg.interleave == (interleave is True)  # one-sample frames: contiguous blocks by default
+    for _ in range(3):
+        fg.step()
+    torch.cuda.synchronize()
+    assert fg.graph is not None, sc.last_kernel
+    assert np.array_equal(fg.frame().cpu().numpy(), want)
+    fg.g.recv.zero_()
+    fg.run(4)
+    torch.cuda.synchronize()
+    assert np.array_equal(fg.frame().cpu().numpy(), want)
+    first = fg.graph
+    # a camera change uploads new tables: the next step records a new graph
+    sc.vc.set_camera([1.0, 2.5, 6.0], [0.0, 0.5, 0.0], [0.0, 1.0, 0.0], 40)
+    fg.step()
+    torch.cuda.synchronize()
+    assert fg.graph is not first
+    moved = product_scene(name)
+    moved.vc.set_camera([1.0, 2.5, 6.0], [0.0, 0.5, 0.0], [0.0, 1.0, 0.0], 40)
+    assert np.array_equal(fg.frame().cpu().numpy(), moved.render_rgb8())

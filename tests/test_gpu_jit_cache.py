@@ -48,3 +48,42 @@ def test_baked_kernels_are_bounded(tmp_path, monkeypatch):
     sc = product_scene_dict(d)
     img = sc.render()
     assert np.array_equal(img, oracle_render_dict(d))
+
+
+@pytest.mark.parametrize("name,res", [("TwoSpheresPlane", (1920, 1080)), ("MirrorRefraction", (160, 90)),
+                                      ("TorusMesh", (96, 96))])
+def test_async_compile_renders_generic_then_specialized(name, res, tmp_path, monkeypatch):
+    """Option jit_async (the product default; this suite pins 0 in conftest.py): with a cold
+    code-object cache the first frames launch the precompiled generic kernel while hiprtc
+    compiles on a host thread, and after rtx_jit_wait the specialized kernel renders.
+    Every frame -- fp32 and the fused uint8 path -- is bit-identical to the oracle, and the
+    first frame does not wait for the compile."""
+    import time
+    import torch
+    from rtx.io import bundled_scene_dict
+    cache = tmp_path / "jit"
+    cache.mkdir(mode=0o700)
+    os.chmod(cache, 0o700)
+    monkeypatch.setattr(OPTS, "jit_cache", str(cache))
+    monkeypatch.setattr(OPTS, "jit_async", "1")
+    d = bundled_scene_dict(name, resolution=res, spp=(1, None))
+    d.pop("__base_dir__", None)
+    d["lights"][0]["power"] = 0.6180339887  # record values no earlier test compiled
+    sc = product_scene_dict(d)
+    ref = oracle_render_dict(d)
+    t0 = time.perf_counter()
+    img = sc.render()
+    first_s = time.perf_counter() - t0
+    first = sc.last_kernel
+    assert first.startswith("k_render_"), first
+    assert_parity(img, ref, name + " generic")
+    assert first_s < 0.2, first_s  # (a compile takes ~0.3 s)
+    want8 = (np.rot90(ref, k=1, axes=(0, 1)) * 255).astype(np.uint8)
+    assert np.array_equal(sc.render_rgb8(), want8)
+    assert sc.jit_wait() == 0
+    img = sc.render()
+    assert sc.last_kernel.startswith("rtx_jit_render_"), sc.last_kernel
+    assert_parity(img, ref, name + " specialized")
+    assert np.array_equal(sc.render_rgb8(), want8)
+    assert sc.last_kernel.startswith("rtx_jit_render_") and "_rgb8" in sc.last_kernel, sc.last_kernel
+    torch.cuda.synchronize()

@@ -434,6 +434,25 @@ def test_scene_specialized_kernel_equals_generic(name, res, edits, monkeypatch):
     assert torch.equal(a, b) and torch.equal(cnt_a, cnt_b)
 
 
+@pytest.mark.parametrize("name", ["TwoSpheresPlane", "MirrorRefraction", "TorusMesh"])
+@pytest.mark.parametrize("opt,value", [("tile_block", "256"), ("jit_ilp", "0"), ("prim_origin", "0")])
+def test_codegen_options_render_the_default_bytes(name, opt, value, monkeypatch):
+    """The code-generation options off their defaults -- 256-thread
+    blocks for the secondary-ray / mesh kernels, no max-ILP scheduling or kernel-argument
+    preload, no host-computed primary-ray origin terms -- render the default kernel's bytes
+    at the configs' 1920x1080 size (three frames: the tile schedule's measured and sorted
+    orders too)."""
+    sc = product_scene(name, (1920, 1080), AA={"jitter": False, "samples": 1})
+    base = sc.render_device().clone()
+    k0 = sc.last_kernel
+    monkeypatch.setattr(OPTS, opt, value)
+    sc.invalidate()  # (options are read when a camera's kernels are resolved)
+    for _ in range(3):
+        alt = sc.render_device()
+        assert torch.equal(base, alt), (name, opt, k0, sc.last_kernel)
+    assert sc.last_kernel.startswith("rtx_jit_render_"), sc.last_kernel
+
+
 def test_default_flat_scenes_run_the_specialized_kernel():
     """The production path for flat scenes is the scene-specialized kernel (bench.py reports
     its name); hierarchy/texture scenes run the split passes (csrc/rtx_split.h)."""
@@ -466,6 +485,50 @@ def test_camera_changes_rerender():
     fresh.invalidate()
     sc.invalidate()
     assert np.array_equal(sc.render(), fresh.render())
+
+
+def test_edits_between_renders_match_oracle():
+    """a sphere centre, a material's diffuse colour, a light's power, a
+    plane's checker material and an appended object are edited between renders -- in
+    place, with no invalidate() -- and every render equals the oracle of the edited scene
+    JSON (the reference reads the objects, materials and lights on every render,
+    provided/scene.py:86-88, :148, :161-164). Both the fp32 frame (render) and the fused
+    uint8 path (render_rgb8) re-upload."""
+    from common import oracle_render_dict, product_scene_dict
+    from rtx.geometry import Sphere
+    from rtx.io import bundled_scene_dict
+    d = bundled_scene_dict("TwoSpheresPlane", resolution=(96, 72))
+    d.pop("__base_dir__", None)
+    sc = product_scene_dict(d)
+    assert_parity(sc.render(), oracle_render_dict(d), "before edits")
+    k = next(i for i, o in enumerate(d["objects"]) if o["type"] == "sphere")
+    steps = [
+        ("sphere centre", lambda: sc.objects[k].center.__setitem__(1, np.float32(0.75)),
+         lambda: d["objects"][k]["position"].__setitem__(1, 0.75)),
+        ("material diffuse", lambda: sc.materials[1].diffuse.__setitem__(slice(None), (0.25, 0.5, 0.125)),
+         lambda: d["materials"][1].__setitem__("diffuse", [0.25, 0.5, 0.125])),
+        ("light power", lambda: setattr(sc.lights[0], "power", 0.25),
+         lambda: d["lights"][0].__setitem__("power", 0.25)),
+        ("checker material", lambda: sc.objects[0].materials.__setitem__(1, sc.materials[0]),
+         lambda: d["objects"][0]["materials"].__setitem__(1, 0)),
+        ("appended sphere", lambda: sc.objects.append(Sphere("s2", "sphere", [sc.materials[3]],
+                                                             np.array([1.5, 0.4, 0.5], np.float32), 0.4, None)),
+         lambda: d["objects"].append({"materials": [3], "name": "s2", "position": [1.5, 0.4, 0.5], "radius": 0.4,
+                                      "type": "sphere"})),
+    ]
+    prev = sc.render()
+    for what, edit_product, edit_json in steps:
+        gen = sc._gen
+        edit_product()
+        edit_json()
+        ref = oracle_render_dict(d)
+        img = sc.render()
+        assert_parity(img, ref, what)
+        assert not np.array_equal(img, prev), what  # the edit shows
+        assert sc._gen != gen, what                 # one re-upload
+        assert np.array_equal(sc.render_rgb8(), (np.rot90(ref, k=1, axes=(0, 1)) * 255).astype(np.uint8)), what
+        prev = img
+    assert isinstance(sc.objects[k], Sphere)
 
 
 SPP_CASES = CASES + [
