@@ -33,6 +33,7 @@
 
 #include "../../include/rtx.h"
 #include "rtx_kernels.h"
+#include "rtx_bins.h"
 #include "rtx_launch.h"
 #include "rtx_split.h"
 
@@ -73,7 +74,7 @@ enum Opt {
     OPT_SPLIT, OPT_SPLIT_BYTES, OPT_SPLIT_RATIO, OPT_BINS, OPT_HEAVY_TILES, OPT_LENS_BINS, OPT_LGRID, OPT_DSGRID, OPT_DSGRID_MIN,
     OPT_SELF_SKIP, OPT_TILE_SCHED, OPT_XCD_MAP, OPT_TILE_BLOCK, OPT_PRIM_ORIGIN, OPT_SPP, OPT_SPP_MIN, OPT_JIT, OPT_JIT_BAKE, OPT_JIT_EXT,
     OPT_JIT_DUMP, OPT_JIT_IDLE_BAKED, OPT_JIT_DISK_BAKED, OPT_JIT_CACHE, OPT_JIT_FLAGS, OPT_JIT_ILP, OPT_JIT_ASYNC,
-    OPT_SETUP_LOG, OPT_COUNT
+    OPT_DEV_BINS, OPT_SETUP_LOG, OPT_COUNT
 };
 struct OptDef {
     const char* name;
@@ -107,6 +108,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"jit_flags", 0, true},                   // extra hiprtc options (part of the cache key)
     {"jit_ilp", 1, false},                    // max-ILP scheduling of one-sample primary+shadow kernels
     {"jit_async", 1, false},                  // compile on a host thread; the generic kernel renders meanwhile
+    {"dev_bins", 1, false},                   // a mesh's primary-ray face bins built on the device
     {"setup_log", 0, false},                  // print the host time of each rtx_camera_set step
 };
 struct OptVal {
@@ -946,7 +948,8 @@ bool lens_bins_disabled() {
 bool primary_bins(const HostScene& H, const rtx_camera_desc* c, const std::vector<DBound>& nodeb,
                   std::vector<int32_t>& start, std::vector<int32_t>& faces, std::vector<float>& zmin,
                   std::vector<uint32_t>& objmask, std::vector<uint32_t>& rootmask, int32_t& bins_x,
-                  int32_t& mesh_bins) {
+                  int32_t& mesh_bins, bool* faces_on_device = nullptr) {
+    if (faces_on_device) *faces_on_device = false;
     if (c->ncols < 2 || c->height < 2) return false;
     const bool pinhole = c->n_dof == 1 && c->n_aa == 1 && c->jitter == RTX_JITTER_OFF &&
                          c->dof_origins[0] == c->position[0] && c->dof_origins[1] == c->position[1] &&
@@ -995,56 +998,23 @@ bool primary_bins(const HostScene& H, const rtx_camera_desc* c, const std::vecto
         const double m = std::max(std::fabs(1.0 - lmin), std::fabs(1.0 - lmax));
         return (lensR1 + m * lensA) * (1.0 + 1e-5) + 1e-5 * (lmax * den_hi + omag + R2 + f);
     };
-    // fractional index of a screen coordinate in the camera's own (fp32) pixel table: the
-    // rays use those very values, so no spacing estimate accumulates error across the image
-    auto table_pos = [](const float* t, int32_t n, double x) {
-        if (x <= (double)t[0]) return (x - (double)t[0]) / ((double)t[1] - (double)t[0]);
-        if (x >= (double)t[n - 1]) return (n - 1) + (x - (double)t[n - 1]) / ((double)t[n - 1] - (double)t[n - 2]);
-        const int32_t k = (int32_t)(std::upper_bound(t, t + n, (float)x) - t);  // t[k-1] <= fl(x) < t[k]
-        const int32_t k1 = std::min(std::max(k, 1), n - 1);
-        return (k1 - 1) + (x - (double)t[k1 - 1]) / ((double)t[k1] - (double)t[k1 - 1]);
-    };
+    // fractional column / row of a point in the camera's own (fp32) pixel tables and the
+    // bin rectangle of a point set (rtx_bins.h: the same arithmetic as the device face pass)
+    BinProj BP;
+    for (int a = 0; a < 3; ++a) {
+        BP.o[a] = o[a];
+        BP.u[a] = c->u[a]; BP.v[a] = c->v[a]; BP.w[a] = c->w[a];
+    }
+    BP.d = c->d;
+    BP.xs = c->xs;
+    BP.ys = c->ys;
+    BP.W = W;
+    BP.H = Hh;
     bins_x = (W + 7) / 8;
     const int32_t bins_y = (Hh + 7) / 8;
     const size_t nb = (size_t)bins_x * bins_y;
-    // pixel coordinates (strip column, image row) and depth of a point; false: grazing/behind
-    auto project = [&](const double p[3], double& col, double& row, double& depth) {
-        double rel[3], len2 = 0.0, pu = 0.0, pv = 0.0, pw = 0.0;
-        for (int a = 0; a < 3; ++a) {
-            rel[a] = p[a] - o[a];
-            len2 += rel[a] * rel[a];
-            pu += rel[a] * c->u[a];
-            pv += rel[a] * c->v[a];
-            pw += rel[a] * c->w[a];
-        }
-        depth = -pw;
-        if (!(depth > 1e-3 * std::sqrt(len2)) || !(depth > 1e-9)) return false;
-        col = table_pos(c->xs, W, c->d * pu / depth);
-        row = (double)(Hh - 1) - table_pos(c->ys, Hh, c->d * pv / depth);
-        return true;
-    };
-    struct Rect { int32_t c0, c1, r0, r1; };
-    // bin range of the points' padded pixel rectangle (c0 > c1: off the strip); false if a
-    // point cannot be projected
-    auto rect_of = [&](const double (*pts)[3], int n, Rect& R, double& zlo) {
-        double cmin = INFINITY, cmax = -INFINITY, rmin = INFINITY, rmax = -INFINITY;
-        zlo = INFINITY;
-        for (int i = 0; i < n; ++i) {
-            double col, row, depth;
-            if (!project(pts[i], col, row, depth)) return false;
-            cmin = std::min(cmin, col); cmax = std::max(cmax, col);
-            rmin = std::min(rmin, row); rmax = std::max(rmax, row);
-            zlo = std::min(zlo, depth);
-        }
-        R = Rect{1, 0, 1, 0};
-        const double c0 = std::floor(cmin) - 2.0, c1 = std::ceil(cmax) + 2.0;
-        const double r0 = std::floor(rmin) - 2.0, r1 = std::ceil(rmax) + 2.0;
-        if (c1 >= 0.0 && c0 <= W - 1 && r1 >= 0.0 && r0 <= Hh - 1) {
-            R.c0 = (int32_t)std::max(0.0, c0) >> 3; R.c1 = (int32_t)std::min((double)(W - 1), c1) >> 3;
-            R.r0 = (int32_t)std::max(0.0, r0) >> 3; R.r1 = (int32_t)std::min((double)(Hh - 1), r1) >> 3;
-        }
-        return true;
-    };
+    using Rect = BinRect;
+    auto rect_of = [&](const double (*pts)[3], int n, Rect& R, double& zlo) { return bins_rect(BP, pts, n, R, zlo); };
     auto mark_in = [&](std::vector<uint32_t>& m, const Rect& R, uint32_t bit) {
         for (int32_t by = R.r0; by <= R.r1; ++by)
             for (int32_t bx = R.c0; bx <= R.c1; ++bx) m[(size_t)by * bins_x + bx] |= bit;
@@ -1150,6 +1120,10 @@ bool primary_bins(const HostScene& H, const rtx_camera_desc* c, const std::vecto
     faces.clear();
     zmin.clear();
     if (H.n_mesh != 1 || !pinhole) return true;
+    if (faces_on_device) {  // the mesh's face bins: rtx_bins.hip (rtx_camera_set)
+        *faces_on_device = true;
+        return true;
+    }
     const DObj& m = H.objs[H.n_plane + H.n_sphere + H.n_box];
     std::vector<Rect> rects(m.tri_count);
     // A hit point P = o + t d (|d| = 1 up to rounding) has depth (P - o).(-w) <= t, and a
@@ -2245,6 +2219,13 @@ struct rtx_scene {
     hipEvent_t split_done = nullptr;     // the last split render's completion (cross-stream order)
     hipStream_t split_stream = nullptr;  // its stream
     bool split_used = false;
+    // the device face bins' scratch (rtx_bins.hip; per camera, reused while large enough):
+    // the pixel tables and stage-1 arrays, then the (bin, rank) pairs
+    char* d_mb = nullptr;
+    size_t mb_cap = 0;
+    char* d_mb2 = nullptr;
+    size_t mb2_cap = 0;
+    MeshBinsDev mbd{};
     // buffers a captured graph may still reference: freed only with the scene
     std::vector<void*> split_retired;
     bool split_captured = false;
@@ -2288,6 +2269,83 @@ int pinned_upload(rtx_scene* s, void* dst, size_t n) {
     return RTX_OK;
 }
 
+// A device buffer of at least n bytes (grown, contents dropped).
+int grow(char** p, size_t* cap, size_t n) {
+    if (*cap >= n) return RTX_OK;
+    (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    RTX_HIP(hipMalloc((void**)p, n + n / 4));
+    *cap = n + n / 4;
+    return RTX_OK;
+}
+
+size_t a256(size_t n) { return (n + 255) & ~(size_t)255; }
+
+// Stage 1 of the device face bins of the scene's one mesh (option dev_bins; rtx_bins.hip):
+// uploads the pixel tables, bins every face, and reads the bins' face counts back (a copy
+// kernel into the mapped pinned buffer: no copy engine) into start (prefix sums, nb + 1).
+// *npairs: the total; mesh_bins 0 when a face cannot be projected (the BVH walk, as on
+// the host). Leaves the faces' order in the scene's scratch for stage 2.
+int mesh_bins_dev1(rtx_scene* s, const rtx_camera_desc* c, int32_t bins_x, std::vector<int32_t>& start,
+                   int32_t* npairs, int32_t* mesh_bins) {
+    const HostScene& H = s->h_bins;
+    const DObj& m = H.objs[H.n_plane + H.n_sphere + H.n_box];
+    const int32_t n = m.tri_count, W = c->ncols, Hh = c->height;
+    const int32_t nb = bins_x * ((Hh + 7) / 8);
+    *npairs = 0;
+    *mesh_bins = 0;
+    start.assign((size_t)nb + 1, 0);
+    const size_t oys = a256(sizeof(float) * W), tb = oys + a256(sizeof(float) * Hh);
+    int rc;
+    if ((rc = grow(&s->d_mb, &s->mb_cap, tb + mesh_bins_bytes1(n, nb)))) return rc;
+    if ((rc = pinned_reserve(s, tb))) return rc;
+    memcpy(s->h_cam, c->xs, sizeof(float) * W);
+    memcpy(s->h_cam + oys, c->ys, sizeof(float) * Hh);
+    if ((rc = pinned_upload(s, s->d_mb, (tb + 15) & ~(size_t)15))) return rc;
+    BinProj P;
+    for (int a = 0; a < 3; ++a) {
+        P.o[a] = c->aa_origins[a];  // (a pinhole: every primary ray leaves aa_o[0])
+        P.u[a] = c->u[a]; P.v[a] = c->v[a]; P.w[a] = c->w[a];
+    }
+    P.d = c->d;
+    P.xs = reinterpret_cast<const float*>(s->d_mb);
+    P.ys = reinterpret_cast<const float*>(s->d_mb + oys);
+    P.W = W;
+    P.H = Hh;
+    const float* tris = reinterpret_cast<const float*>(static_cast<const DTri*>(s->d_tris) + m.tri_begin);
+    RTX_HIP(mesh_bins_stage1(P, tris, (int32_t)(sizeof(DTri) / sizeof(float)), n, bins_x, nb, s->d_mb + tb, s->mbd,
+                             nullptr));
+    // the counts and the flag (the segment after them) to the host
+    const size_t cb = a256(sizeof(int32_t) * ((size_t)nb + 1)) + 16;
+    if ((rc = pinned_reserve(s, cb))) return rc;
+    void* hp = nullptr;
+    RTX_HIP(hipHostGetDevicePointer(&hp, s->h_cam, 0));
+    hipLaunchKernelGGL(k_stage_copy, dim3((unsigned)std::min<size_t>(1024, (cb / 16 + 255) / 256)), dim3(256), 0, nullptr,
+                       (const uint4*)s->mbd.count, (uint4*)hp, (int64_t)(cb / 16));
+    RTX_HIP(hipGetLastError());
+    RTX_HIP(hipStreamSynchronize(nullptr));
+    const int32_t* cnt = reinterpret_cast<const int32_t*>(s->h_cam);
+    if (*reinterpret_cast<const int32_t*>(s->h_cam + cb - 16) != 0) return RTX_OK;  // walk the BVH
+    for (int32_t b = 0; b < nb; ++b) start[b + 1] = start[b] + cnt[b];
+    // the fill cursors of stage 2: the bins' starts
+    memcpy(s->h_cam, start.data(), sizeof(int32_t) * nb);
+    if ((rc = pinned_upload(s, s->mbd.count, (sizeof(int32_t) * nb + 15) & ~(size_t)15))) return rc;
+    *npairs = start[nb];
+    *mesh_bins = 1;
+    return RTX_OK;
+}
+
+// Stage 2: the bins' face lists and depth bounds into the camera buffer.
+int mesh_bins_dev2(rtx_scene* s, int32_t bins_x, int32_t nb, int32_t npairs, int32_t* faces, float* zmin) {
+    const HostScene& H = s->h_bins;
+    const int32_t n = H.objs[H.n_plane + H.n_sphere + H.n_box].tri_count;
+    if (int rc = grow(&s->d_mb2, &s->mb2_cap, mesh_bins_bytes2(n, npairs))) return rc;
+    RTX_HIP(mesh_bins_stage2(s->mbd, n, bins_x, nb, npairs, s->d_mb2, faces, zmin, nullptr));
+    RTX_HIP(hipStreamSynchronize(nullptr));
+    return RTX_OK;
+}
+
 // Forgets the camera (its kernels are specialized on its sample counts); the device
 // buffers stay for the next camera (free_scene frees them).
 void free_camera(rtx_scene* s) {
@@ -2305,6 +2363,8 @@ void free_scene(rtx_scene* s) {
     (void)hipHostFree(s->h_cam);
     (void)hipFree(s->d_dsg_cells);
     (void)hipFree(s->d_scratch);
+    (void)hipFree(s->d_mb);
+    (void)hipFree(s->d_mb2);
     if (s->split_done) (void)hipEventSynchronize(s->split_done);
     (void)hipFree(s->d_split);
     (void)hipFree(s->d_split_count);
@@ -2654,15 +2714,22 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     std::vector<int32_t> bstart, bfaces;
     std::vector<float> bz;
     std::vector<uint32_t> bmask, brmask;
-    int32_t bins_x = 0, mesh_bins = 0;
+    int32_t bins_x = 0, mesh_bins = 0, dev_pairs = 0;
+    bool dev_faces = false;  // the mesh's face bins are built on the device (rtx_bins.hip)
     const bool bins = opt_on(OPT_BINS) &&
-                      primary_bins(s->h_bins, c, s->tr_bounds, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins);
+                      primary_bins(s->h_bins, c, s->tr_bounds, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins,
+                                   opt_on(OPT_DEV_BINS) ? &dev_faces : nullptr);
+    if (bins && dev_faces) {
+        if ((rc = mesh_bins_dev1(s, c, bins_x, bstart, &dev_pairs, &mesh_bins))) return rc;
+        dev_faces = dev_pairs > 0;
+        slog.mark("device face bins (stage 1)");
+    }
     if (bins) {
-        if (bfaces.empty()) { bfaces.push_back(0); bz.push_back(0.0f); }
+        if (bfaces.empty() && !dev_faces) { bfaces.push_back(0); bz.push_back(0.0f); }
         bmask.insert(bmask.end(), brmask.begin(), brmask.end());  // [object masks | root masks]
         o_bstart = st.put(bstart);
-        o_bfaces = st.put(bfaces);
-        o_bz = st.put(bz);
+        o_bfaces = dev_faces ? st.put(nullptr, sizeof(int32_t) * dev_pairs) : st.put(bfaces);
+        o_bz = dev_faces ? st.put(nullptr, sizeof(float) * dev_pairs) : st.put(bz);
         o_bmask = st.put(bmask);
     }
     std::vector<int32_t> bheavy;
@@ -2773,6 +2840,12 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     memcpy(s->h_cam + o_kp, &k, sizeof(KParams));
     if ((rc = pinned_upload(s, D, st.size()))) return rc;
     slog.mark("upload");
+    if (dev_faces) {  // (after the upload, which zero-filled their segments)
+        if ((rc = mesh_bins_dev2(s, bins_x, (int32_t)(bstart.size() - 1), dev_pairs, reinterpret_cast<int32_t*>(D + o_bfaces),
+                                 reinterpret_cast<float*>(D + o_bz))))
+            return rc;
+        slog.mark("device face bins (stage 2)");
+    }
     s->d_kp = reinterpret_cast<KParams*>(D + o_kp);
     s->kp = k;
     s->cam_set = true;

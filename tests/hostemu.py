@@ -14,6 +14,7 @@ DEPS = [SRC, os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_api.h
         os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_fastmath.h"),
         os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_launch.h"),
         os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_split.h"),
+        os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_bins.h"),
         os.path.join(HERE, "..", "python-raytracer_amd", "csrc", "rtx_jit_sources.inc"),
         os.path.join(HERE, "..", "include", "rtx.h")]
 

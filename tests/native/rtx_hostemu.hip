@@ -11,6 +11,13 @@ hipError_t launch_render_ext_m0(int, const RenderLaunch&, const Launch&) { retur
 hipError_t launch_render_ext_m1(int, const RenderLaunch&, const Launch&) { return hipErrorNotSupported; }
 hipError_t launch_split_m0(int, int, const RenderLaunch&, const Launch&, const SplitBuf&) { return hipErrorNotSupported; }
 hipError_t launch_split_m1(int, int, const RenderLaunch&, const Launch&, const SplitBuf&) { return hipErrorNotSupported; }
+size_t mesh_bins_bytes1(int32_t, int32_t) { return 0; }
+size_t mesh_bins_bytes2(int32_t, int32_t) { return 0; }
+hipError_t mesh_bins_stage1(const BinProj&, const float*, int32_t, int32_t, int32_t, int32_t, void*, MeshBinsDev&,
+                            hipStream_t) { return hipErrorNotSupported; }
+hipError_t mesh_bins_stage2(MeshBinsDev&, int32_t, int32_t, int32_t, int32_t, void*, int32_t*, float*, hipStream_t) {
+    return hipErrorNotSupported;
+}
 }  // namespace rtx
 
 #include <omp.h>

@@ -411,6 +411,40 @@ def test_heavy_tiles_equal_walk(tmp_path, monkeypatch):
             assert_parity(img, oracle_render_dict(d), "heavy tiles")
 
 
+def test_device_face_bins_equal_host(tmp_path, monkeypatch):
+    """A mesh's primary-ray face bins built on the device (option dev_bins, rtx_bins.hip:
+    the host's projection arithmetic, rtx_bins.h, then two radix sorts) render the frames
+    of the host-built bins and of no bins at all, bit for bit: the 81,920-face mesh at
+    1920x1080 (heavy tiles included) and at a size that is not a multiple of 8, TorusMesh
+    at 1080p; the small ones also against the oracle. Each camera is set twice, so the
+    scratch is reused, and a camera move re-bins."""
+    from common import oracle_render_dict, product_scene_dict
+    from scenegen import blob_obj, blob_scene
+    from rtx.io import bundled_scene_dict
+    p = str(tmp_path / "blob6.obj")
+    blob_obj(p, level=6)
+    cases = [(blob_scene(p, (1920, 1080)), False), (blob_scene(p, (203, 117)), True),
+             (bundled_scene_dict("TorusMesh", resolution=(1920, 1080)), False),
+             (bundled_scene_dict("TorusMesh", resolution=(97, 61)), True)]
+    for d, small in cases:
+        d = {k: v for k, v in d.items() if k != "__base_dir__"}
+        frames = {}
+        for opt, val in (("dev_bins", "1"), ("dev_bins", "0"), ("bins", "0")):
+            monkeypatch.setattr(OPTS, opt, val)
+            sc = product_scene_dict(d)
+            frames[(opt, val)] = sc.render_device().clone()
+            sc.vc.set_camera(sc.vc.position + np.float32(0.05), [0.0, 0.5, 0.0], [0.0, 1.0, 0.0], 40)
+            frames[(opt, val, "moved")] = sc.render_device().clone()
+            monkeypatch.setattr(OPTS, opt, "1")
+        for key in (("dev_bins", "0"), ("bins", "0")):
+            assert torch.equal(frames[("dev_bins", "1")], frames[key]), key
+            assert torch.equal(frames[("dev_bins", "1", "moved")], frames[key + ("moved",)]), key
+        if small:
+            a = frames[("dev_bins", "1")]
+            img = np.ascontiguousarray(np.transpose(a.cpu().numpy()[::-1], (1, 0, 2))).astype(np.float64)
+            assert_parity(img, oracle_render_dict(d), "device face bins")
+
+
 @pytest.mark.parametrize("name,res,edits", [
     ("TwoSpheresPlane", (160, 90), {}), ("MirrorRefraction", (160, 90), {}), ("TorusMesh", (96, 96), {}),
     ("DepthOfField", (64, 48), {"AA": {"jitter": True, "samples": 2}}),
