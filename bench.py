@@ -317,7 +317,8 @@ def sharded_frame(sc, rank, world, steps, warmup, use_dist, device, sync=cuda_sy
     one graph launch of host time. Frames are stream-ordered: each frame's gather completes
     before the next frame renders. No batching and no overlap across frames: the latency of
     one frame, the reference's one-frame-per-run strip render + glue (render.nu:10-15,
-    provided/glue.py:17-27). Partition: contiguous row blocks for one-sample frames (in
+    provided/glue.py:17-27). The timed loop issues its frames from C, frames_per_graph per
+    graph launch (FrameGraph.run). Partition: contiguous row blocks for one-sample frames (in
     image order when N | H: no reorder), interleaved 8-row groups otherwise.
     Returns (seconds for `steps` frames, max over ranks; rank 0's last frame [H, W, 3];
     the loop's host issue cost)."""
@@ -326,25 +327,30 @@ def sharded_frame(sc, rank, world, steps, warmup, use_dist, device, sync=cuda_sy
                     collective_at_one=collective_at_one)
     for _ in range(warmup):
         fg.step()
+    fg.run(2 * fg.kmax if fg.graph_on else 1, stream)  # (records and warms the multi-frame graph too)
     sync()
-    s = timed(fg.step, steps, use_dist, sync, device)
-    # host issue per frame (outside the timed region): the same loop with the clock stopped
-    # before the device finishes, per step() and as one rtx_graph_launch of all frames
+    # the timed region: `steps` frames, issued from C (rtx_graph_launch, fg.kmax frames per
+    # graph launch; each frame rendered, gathered and reordered before the next starts)
+    s = timed(lambda: fg.run(steps, stream), 1, use_dist, sync, device)
+    # host issue per frame (outside the timed region): the clock stopped before the device
+    # finishes, for run() and for one Python step() per frame
     t0 = time.perf_counter()
-    for _ in range(steps):
-        fg.step()
+    fg.run(steps, stream)
     t1 = time.perf_counter()
     sync()
     t2 = time.perf_counter()
-    fg.run(steps, stream)
+    for _ in range(steps):
+        fg.step()
     t3 = time.perf_counter()
     sync()
     last = fg.frame()
     nrows = [len(r) for r in fg.g.rows]
-    info = {"graph": fg.graph is not None, "rows_per_rank": [min(nrows), max(nrows)], "partition": "interleaved 8-row groups" if fg.interleave else
-            "contiguous row blocks (np.array_split)", "in_order": bool(fg.g.in_order),
+    info = {"graph": fg.graph is not None, "frames_per_graph": fg.kmax if fg.graphk is not None else 1,
+            "rows_per_rank": [min(nrows), max(nrows)],
+            "partition": "interleaved 8-row groups" if fg.interleave else "contiguous row blocks (np.array_split)",
+            "in_order": bool(fg.g.in_order),
             "host_issue_us_per_frame": round((t1 - t0) * 1e6 / steps, 3),
-            "host_issue_c_us_per_frame": round((t3 - t2) * 1e6 / steps, 3)}
+            "host_issue_step_us_per_frame": round((t3 - t2) * 1e6 / steps, 3)}
     return s, (last.clone() if last is not None else None), info
 
 
@@ -413,8 +419,9 @@ def measure_sharded(sc, rank, world, steps, warmup, use_dist, device, sync=cuda_
         "partition": loop["partition"] + (" (rank 0's buffer is the frame)" if loop["in_order"] else
                                           ", reordered on rank 0"),
         "collective": "one torch.distributed.gather (RCCL) of the ranks' uint8 rows to rank 0 per frame, stream-ordered",
-        "frame_loop": dict(loop, note="render + gather + reorder recorded once as a HIP graph (FrameGraph), replayed per "
-                                      "frame; host_issue: Python step() per frame / rtx_graph_launch of all frames"),
+        "frame_loop": dict(loop, note="render + gather + reorder recorded as a HIP graph (FrameGraph): the timed "
+                                      "frames issued from C, frames_per_graph frames per graph launch "
+                                      "(host_issue_us_per_frame); host_issue_step: one Python step() per frame"),
         "throughput": {
             "frame_ms": round(stream_s * 1e3 / steps, 5), "Mrays_s": rate(stream_s),
             "launch": ("one batched launch per group of N frames (rtx_render_groups_frames)" if ex.render_frames

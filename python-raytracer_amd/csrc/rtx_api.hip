@@ -74,7 +74,7 @@ enum Opt {
     OPT_SPLIT, OPT_SPLIT_BYTES, OPT_SPLIT_RATIO, OPT_BINS, OPT_HEAVY_TILES, OPT_LENS_BINS, OPT_LGRID, OPT_DSGRID, OPT_DSGRID_MIN,
     OPT_SELF_SKIP, OPT_TILE_SCHED, OPT_XCD_MAP, OPT_TILE_BLOCK, OPT_PRIM_ORIGIN, OPT_SPP, OPT_SPP_MIN, OPT_JIT, OPT_JIT_BAKE, OPT_JIT_EXT,
     OPT_JIT_DUMP, OPT_JIT_IDLE_BAKED, OPT_JIT_DISK_BAKED, OPT_JIT_CACHE, OPT_JIT_FLAGS, OPT_JIT_ILP, OPT_JIT_ASYNC,
-    OPT_DEV_BINS, OPT_SETUP_LOG, OPT_COUNT
+    OPT_DEV_BINS, OPT_CHUNK_MODE, OPT_SETUP_LOG, OPT_COUNT
 };
 struct OptDef {
     const char* name;
@@ -109,6 +109,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"jit_ilp", 1, false},                    // max-ILP scheduling of one-sample primary+shadow kernels
     {"jit_async", 1, false},                  // compile on a host thread; the generic kernel renders meanwhile
     {"dev_bins", 1, false},                   // a mesh's primary-ray face bins built on the device
+    {"chunk_mode", 3, false},                 // heavy-tile pass: bit 0 LDS-staged faces, bit 1 XCD-aware order
     {"setup_log", 0, false},                  // print the host time of each rtx_camera_set step
 };
 struct OptVal {
@@ -2256,11 +2257,12 @@ int pinned_reserve(rtx_scene* s, size_t n) {
 }
 // The first n bytes of the pinned buffer (whole 16-byte words) to dst (16-byte aligned);
 // blocking, so the buffer can be refilled as soon as it returns.
-int pinned_upload(rtx_scene* s, void* dst, size_t n) {
+int pinned_upload(rtx_scene* s, void* dst, size_t n, size_t off = 0) {  // (bytes [off, off + n) of the buffer)
     if (n == 0) return RTX_OK;
-    if ((n & 15) || (reinterpret_cast<uintptr_t>(dst) & 15)) return fail(RTX_ERR_INVALID, "pinned_upload: unaligned");
+    if ((n & 15) || (off & 15) || (reinterpret_cast<uintptr_t>(dst) & 15))
+        return fail(RTX_ERR_INVALID, "pinned_upload: unaligned");
     void* hp = nullptr;
-    RTX_HIP(hipHostGetDevicePointer(&hp, s->h_cam, 0));
+    RTX_HIP(hipHostGetDevicePointer(&hp, s->h_cam + off, 0));
     const int64_t w = (int64_t)(n / 16);
     hipLaunchKernelGGL(k_stage_copy, dim3((unsigned)std::min<int64_t>(1024, (w + 255) / 256)), dim3(256), 0, nullptr,
                        (const uint4*)hp, (uint4*)dst, w);
@@ -2281,70 +2283,6 @@ int grow(char** p, size_t* cap, size_t n) {
 }
 
 size_t a256(size_t n) { return (n + 255) & ~(size_t)255; }
-
-// Stage 1 of the device face bins of the scene's one mesh (option dev_bins; rtx_bins.hip):
-// uploads the pixel tables, bins every face, and reads the bins' face counts back (a copy
-// kernel into the mapped pinned buffer: no copy engine) into start (prefix sums, nb + 1).
-// *npairs: the total; mesh_bins 0 when a face cannot be projected (the BVH walk, as on
-// the host). Leaves the faces' order in the scene's scratch for stage 2.
-int mesh_bins_dev1(rtx_scene* s, const rtx_camera_desc* c, int32_t bins_x, std::vector<int32_t>& start,
-                   int32_t* npairs, int32_t* mesh_bins) {
-    const HostScene& H = s->h_bins;
-    const DObj& m = H.objs[H.n_plane + H.n_sphere + H.n_box];
-    const int32_t n = m.tri_count, W = c->ncols, Hh = c->height;
-    const int32_t nb = bins_x * ((Hh + 7) / 8);
-    *npairs = 0;
-    *mesh_bins = 0;
-    start.assign((size_t)nb + 1, 0);
-    const size_t oys = a256(sizeof(float) * W), tb = oys + a256(sizeof(float) * Hh);
-    int rc;
-    if ((rc = grow(&s->d_mb, &s->mb_cap, tb + mesh_bins_bytes1(n, nb)))) return rc;
-    if ((rc = pinned_reserve(s, tb))) return rc;
-    memcpy(s->h_cam, c->xs, sizeof(float) * W);
-    memcpy(s->h_cam + oys, c->ys, sizeof(float) * Hh);
-    if ((rc = pinned_upload(s, s->d_mb, (tb + 15) & ~(size_t)15))) return rc;
-    BinProj P;
-    for (int a = 0; a < 3; ++a) {
-        P.o[a] = c->aa_origins[a];  // (a pinhole: every primary ray leaves aa_o[0])
-        P.u[a] = c->u[a]; P.v[a] = c->v[a]; P.w[a] = c->w[a];
-    }
-    P.d = c->d;
-    P.xs = reinterpret_cast<const float*>(s->d_mb);
-    P.ys = reinterpret_cast<const float*>(s->d_mb + oys);
-    P.W = W;
-    P.H = Hh;
-    const float* tris = reinterpret_cast<const float*>(static_cast<const DTri*>(s->d_tris) + m.tri_begin);
-    RTX_HIP(mesh_bins_stage1(P, tris, (int32_t)(sizeof(DTri) / sizeof(float)), n, bins_x, nb, s->d_mb + tb, s->mbd,
-                             nullptr));
-    // the counts and the flag (the segment after them) to the host
-    const size_t cb = a256(sizeof(int32_t) * ((size_t)nb + 1)) + 16;
-    if ((rc = pinned_reserve(s, cb))) return rc;
-    void* hp = nullptr;
-    RTX_HIP(hipHostGetDevicePointer(&hp, s->h_cam, 0));
-    hipLaunchKernelGGL(k_stage_copy, dim3((unsigned)std::min<size_t>(1024, (cb / 16 + 255) / 256)), dim3(256), 0, nullptr,
-                       (const uint4*)s->mbd.count, (uint4*)hp, (int64_t)(cb / 16));
-    RTX_HIP(hipGetLastError());
-    RTX_HIP(hipStreamSynchronize(nullptr));
-    const int32_t* cnt = reinterpret_cast<const int32_t*>(s->h_cam);
-    if (*reinterpret_cast<const int32_t*>(s->h_cam + cb - 16) != 0) return RTX_OK;  // walk the BVH
-    for (int32_t b = 0; b < nb; ++b) start[b + 1] = start[b] + cnt[b];
-    // the fill cursors of stage 2: the bins' starts
-    memcpy(s->h_cam, start.data(), sizeof(int32_t) * nb);
-    if ((rc = pinned_upload(s, s->mbd.count, (sizeof(int32_t) * nb + 15) & ~(size_t)15))) return rc;
-    *npairs = start[nb];
-    *mesh_bins = 1;
-    return RTX_OK;
-}
-
-// Stage 2: the bins' face lists and depth bounds into the camera buffer.
-int mesh_bins_dev2(rtx_scene* s, int32_t bins_x, int32_t nb, int32_t npairs, int32_t* faces, float* zmin) {
-    const HostScene& H = s->h_bins;
-    const int32_t n = H.objs[H.n_plane + H.n_sphere + H.n_box].tri_count;
-    if (int rc = grow(&s->d_mb2, &s->mb2_cap, mesh_bins_bytes2(n, npairs))) return rc;
-    RTX_HIP(mesh_bins_stage2(s->mbd, n, bins_x, nb, npairs, s->d_mb2, faces, zmin, nullptr));
-    RTX_HIP(hipStreamSynchronize(nullptr));
-    return RTX_OK;
-}
 
 // Forgets the camera (its kernels are specialized on its sample counts); the device
 // buffers stay for the next camera (free_scene frees them).
@@ -2420,12 +2358,13 @@ struct CamStage {
         size_t off;
         const void* p;
         size_t n;
+        bool dev;  // filled on the device after the upload: not written (nor uploaded)
     };
     std::vector<Seg> segs;
     size_t bytes = 0;
-    size_t put(const void* p, size_t n) {
+    size_t put(const void* p, size_t n, bool dev = false) {
         const size_t off = (bytes + 255) & ~(size_t)255;
-        segs.push_back(Seg{off, p, n});
+        segs.push_back(Seg{off, p, n, dev});
         bytes = off + std::max<size_t>(n, 4);
         return off;
     }
@@ -2435,10 +2374,82 @@ struct CamStage {
     void write(char* h) const {
         for (const Seg& g : segs) {
             if (g.p) memcpy(h + g.off, g.p, g.n);
-            else memset(h + g.off, 0, std::max<size_t>(g.n, 4));
+            else if (!g.dev) memset(h + g.off, 0, std::max<size_t>(g.n, 4));
         }
     }
 };
+
+}  // namespace
+
+namespace {
+// Stage 1 of the device face bins of the scene's one mesh (option dev_bins; rtx_bins.hip):
+// uploads the pixel tables, bins every face, and reads the bins' face counts back (a copy
+// kernel into the mapped pinned buffer: no copy engine) into start (prefix sums, nb + 1).
+// *npairs: the total; mesh_bins 0 when a face cannot be projected (the BVH walk, as on
+// the host). Leaves the faces' order in the scene's scratch for stage 2.
+int mesh_bins_dev1(rtx_scene* s, const rtx_camera_desc* c, int32_t bins_x, std::vector<int32_t>& start,
+                   int32_t* npairs, int32_t* mesh_bins, SetupLog& slog) {
+    const HostScene& H = s->h_bins;
+    const DObj& m = H.objs[H.n_plane + H.n_sphere + H.n_box];
+    const int32_t n = m.tri_count, W = c->ncols, Hh = c->height;
+    const int32_t nb = bins_x * ((Hh + 7) / 8);
+    *npairs = 0;
+    *mesh_bins = 0;
+    start.assign((size_t)nb + 1, 0);
+    const size_t oys = a256(sizeof(float) * W), tb = oys + a256(sizeof(float) * Hh);
+    int rc;
+    if ((rc = grow(&s->d_mb, &s->mb_cap, tb + mesh_bins_bytes1(n, nb)))) return rc;
+    if ((rc = pinned_reserve(s, tb))) return rc;
+    memcpy(s->h_cam, c->xs, sizeof(float) * W);
+    memcpy(s->h_cam + oys, c->ys, sizeof(float) * Hh);
+    if ((rc = pinned_upload(s, s->d_mb, (tb + 15) & ~(size_t)15))) return rc;
+    slog.mark("face bins: scratch + tables");
+    BinProj P;
+    for (int a = 0; a < 3; ++a) {
+        P.o[a] = c->aa_origins[a];  // (a pinhole: every primary ray leaves aa_o[0])
+        P.u[a] = c->u[a]; P.v[a] = c->v[a]; P.w[a] = c->w[a];
+    }
+    P.d = c->d;
+    P.xs = reinterpret_cast<const float*>(s->d_mb);
+    P.ys = reinterpret_cast<const float*>(s->d_mb + oys);
+    P.W = W;
+    P.H = Hh;
+    const float* tris = reinterpret_cast<const float*>(static_cast<const DTri*>(s->d_tris) + m.tri_begin);
+    RTX_HIP(mesh_bins_stage1(P, tris, (int32_t)(sizeof(DTri) / sizeof(float)), n, bins_x, nb, s->d_mb + tb, s->mbd,
+                             nullptr));
+    if (opt_on(OPT_SETUP_LOG)) {
+        RTX_HIP(hipStreamSynchronize(nullptr));
+        slog.mark("face bins: rects + sort");
+    }
+    // the counts and the flag (the segment after them) to the host
+    const size_t cb = a256(sizeof(int32_t) * ((size_t)nb + 1)) + 16;
+    if ((rc = pinned_reserve(s, cb))) return rc;
+    void* hp = nullptr;
+    RTX_HIP(hipHostGetDevicePointer(&hp, s->h_cam, 0));
+    hipLaunchKernelGGL(k_stage_copy, dim3((unsigned)std::min<size_t>(1024, (cb / 16 + 255) / 256)), dim3(256), 0, nullptr,
+                       (const uint4*)s->mbd.count, (uint4*)hp, (int64_t)(cb / 16));
+    RTX_HIP(hipGetLastError());
+    RTX_HIP(hipStreamSynchronize(nullptr));
+    const int32_t* cnt = reinterpret_cast<const int32_t*>(s->h_cam);
+    if (*reinterpret_cast<const int32_t*>(s->h_cam + cb - 16) != 0) return RTX_OK;  // walk the BVH
+    for (int32_t b = 0; b < nb; ++b) start[b + 1] = start[b] + cnt[b];
+    // the fill cursors of stage 2: the bins' starts
+    memcpy(s->h_cam, start.data(), sizeof(int32_t) * nb);
+    if ((rc = pinned_upload(s, s->mbd.count, (sizeof(int32_t) * nb + 15) & ~(size_t)15))) return rc;
+    *npairs = start[nb];
+    *mesh_bins = 1;
+    return RTX_OK;
+}
+
+// Stage 2: the bins' face lists and depth bounds into the camera buffer.
+int mesh_bins_dev2(rtx_scene* s, int32_t bins_x, int32_t nb, int32_t npairs, int32_t* faces, float* zmin) {
+    const HostScene& H = s->h_bins;
+    const int32_t n = H.objs[H.n_plane + H.n_sphere + H.n_box].tri_count;
+    if (int rc = grow(&s->d_mb2, &s->mb2_cap, mesh_bins_bytes2(n, npairs))) return rc;
+    RTX_HIP(mesh_bins_stage2(s->mbd, n, bins_x, nb, npairs, s->d_mb2, faces, zmin, nullptr));
+    RTX_HIP(hipStreamSynchronize(nullptr));
+    return RTX_OK;
+}
 
 }  // namespace
 
@@ -2720,16 +2731,16 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
                       primary_bins(s->h_bins, c, s->tr_bounds, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins,
                                    opt_on(OPT_DEV_BINS) ? &dev_faces : nullptr);
     if (bins && dev_faces) {
-        if ((rc = mesh_bins_dev1(s, c, bins_x, bstart, &dev_pairs, &mesh_bins))) return rc;
+        if ((rc = mesh_bins_dev1(s, c, bins_x, bstart, &dev_pairs, &mesh_bins, slog))) return rc;
         dev_faces = dev_pairs > 0;
-        slog.mark("device face bins (stage 1)");
+        slog.mark("face bins: counts read back");
     }
     if (bins) {
         if (bfaces.empty() && !dev_faces) { bfaces.push_back(0); bz.push_back(0.0f); }
         bmask.insert(bmask.end(), brmask.begin(), brmask.end());  // [object masks | root masks]
         o_bstart = st.put(bstart);
-        o_bfaces = dev_faces ? st.put(nullptr, sizeof(int32_t) * dev_pairs) : st.put(bfaces);
-        o_bz = dev_faces ? st.put(nullptr, sizeof(float) * dev_pairs) : st.put(bz);
+        o_bfaces = dev_faces ? st.put(nullptr, sizeof(int32_t) * dev_pairs, true) : st.put(bfaces);
+        o_bz = dev_faces ? st.put(nullptr, sizeof(float) * dev_pairs, true) : st.put(bz);
         o_bmask = st.put(bmask);
     }
     std::vector<int32_t> bheavy;
@@ -2838,9 +2849,14 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     if ((rc = pinned_reserve(s, st.size()))) return rc;
     st.write(s->h_cam);
     memcpy(s->h_cam + o_kp, &k, sizeof(KParams));
-    if ((rc = pinned_upload(s, D, st.size()))) return rc;
+    if (dev_faces) {  // (the device fills the face lists: the upload skips their segments)
+        const size_t cut0 = o_bfaces, cut1 = a256(o_bz + sizeof(float) * dev_pairs);
+        if ((rc = pinned_upload(s, D, cut0)) || (rc = pinned_upload(s, D + cut1, st.size() - cut1, cut1))) return rc;
+    } else if ((rc = pinned_upload(s, D, st.size()))) {
+        return rc;
+    }
     slog.mark("upload");
-    if (dev_faces) {  // (after the upload, which zero-filled their segments)
+    if (dev_faces) {
         if ((rc = mesh_bins_dev2(s, bins_x, (int32_t)(bstart.size() - 1), dev_pairs, reinterpret_cast<int32_t*>(D + o_bfaces),
                                  reinterpret_cast<float*>(D + o_bz))))
             return rc;
@@ -3210,7 +3226,7 @@ int render_launch(rtx_scene* s, Launch L, uint64_t* counters_dev, void* stream, 
     auto heavy_pass = [&](bool tiles) -> int {
         if (s->heavy_n <= 0 || !tiles || s->has_ext) return RTX_OK;
         hipLaunchKernelGGL(k_mesh_chunks, dim3((unsigned)s->heavy_n), dim3(64), 0, st, kp, L,  // (a wave per chunk)
-                           s->d_heavy_items, s->heavy_n, s->d_mesh_hits);
+                           s->d_heavy_items, s->heavy_n, s->d_mesh_hits, (int32_t)opt(OPT_CHUNK_MODE));
         RTX_HIP(hipGetLastError());
         return RTX_OK;
     };

@@ -325,6 +325,62 @@ RTX_HD uint2 mesh_chunk(const KParams& P, int32_t bin, int32_t c, int lane) {
     return make_uint2(__builtin_bit_cast(uint32_t, h.t32), h.obj >= 0 ? (uint32_t)h.sub : 0xFFFFFFFFu);
 }
 
+// mesh_chunk with the chunk's face records staged in LDS first (k_mesh_chunks mode bit 0,
+// device only): one round of coalesced loads -- every lane fetches 16-byte words of the
+// chunk's face records (its 32 face indices, then 96 B of triangle and 32 B of face box
+// per face) -- instead of 2-3 dependent scalar loads per face inside the loop (the pass
+// waited on memory 0.63 of its wave cycles, profiles/pmc_blob1080.json). The same tests,
+// in the same order, as mesh_chunk.
+#if defined(__HIP_DEVICE_COMPILE__)
+struct ChunkLds {
+    DTri tri[kHeavyChunk];
+    DFaceBox box[kHeavyChunk];
+    int32_t face[kHeavyChunk];
+    float zmin[kHeavyChunk];
+};
+__device__ __forceinline__ uint2 mesh_chunk_lds(const KParams& P, int32_t bin, int32_t c, int lane, ChunkLds& sh) {
+    const SceneView& S = P.S;
+    const int32_t ty = bin / S.bins_x, tx = bin - ty * S.bins_x;
+    const int32_t row = ty * 8 + (lane >> 3), cc = tx * 8 + (lane & 7);
+    const bool active = row < P.height && cc < P.ncols;
+    const int32_t oi = S.n_plane + S.n_sphere + S.n_box;  // the scene's one top-level mesh
+    const DObj ob = S.objs[oi];
+    const int32_t q0 = S.bin_start[bin] + c * kHeavyChunk;
+    const int32_t n = min(S.bin_start[bin + 1], q0 + kHeavyChunk) - q0;
+    if (lane < n) {
+        sh.face[lane] = S.bin_faces[q0 + lane];
+        sh.zmin[lane] = S.bin_zmin[q0 + lane];
+    }
+    __syncthreads();  // (one wave per block)
+    constexpr int kTriW = (int)(sizeof(DTri) / 16), kBoxW = (int)(sizeof(DFaceBox) / 16), kW = kTriW + kBoxW;
+    for (int w = lane; w < n * kW; w += 64) {
+        const int i = w / kW, k = w - i * kW;
+        const int64_t f = ob.tri_begin + sh.face[i];
+        if (k < kTriW)
+            reinterpret_cast<uint4*>(&sh.tri[i])[k] = reinterpret_cast<const uint4 RTX_CONST*>(&S.tris[f])[k];
+        else
+            reinterpret_cast<uint4*>(&sh.box[i])[k - kTriW] = reinterpret_cast<const uint4 RTX_CONST*>(&S.fboxes[f])[k - kTriW];
+    }
+    __syncthreads();
+    const int j = P.height - 1 - (active ? row : 0);
+    const f3 d = normalize(sub(pixel_focal(P, active ? cc : 0, j), ld3(P.dof_o)));  // scene.py:58
+    const f3 o = ld3(P.aa_o);  // scene.py:60-61 (one sample, no jitter)
+    const float time = P.times[0];
+    const RayInv ri = ray_inv(o, d);
+    Hit h{INFINITY, -1, 0};
+    for (int i = 0; i < n; ++i) {
+        if (RTX_ALL(!active || h.t32 < sh.zmin[i])) break;  // nearest first (closest_hit's exit)
+        const DFaceBox B = sh.box[i];
+        const bool fmaybe = active && leaf_maybe_hit(B, o, ri, ob.cmax, h.t32);
+        if (!RTX_ANY(fmaybe)) continue;
+        float t32;
+        const bool valid = tri_hit(sh.tri[i], o, d, fmaybe, t32);
+        offer(S, h, valid, t32, oi, sh.face[i], o, d, time);
+    }
+    return make_uint2(__builtin_bit_cast(uint32_t, h.t32), h.obj >= 0 ? (uint32_t)h.sub : 0xFFFFFFFFu);
+}
+#endif
+
 // Blocks of a split chunk to render again in the one-kernel form (rtx_split.h): n == nullptr
 // for every other launch. A listed block's flag is set; the launch that renders it clears it.
 struct RedoList {
@@ -739,10 +795,19 @@ __global__ __launch_bounds__(256) void k_occluded(SceneView S, int64_t n, const 
 #if !defined(RTX_EXT_TU)  // defined once, in rtx_api.hip
 // The heavy tiles' chunks (one wave per chunk, launched as one-wave blocks), before the
 // render kernel: items (bin, chunk). A launch of rows (row0, nrows) or 8-row groups
-// (gphase + k gstride) runs only the chunks of its tiles.
-__global__ __launch_bounds__(256) void k_mesh_chunks(const KParams* __restrict__ Pp, const Launch L,
-                                                     const int2* __restrict__ items, int32_t n, uint2* __restrict__ out) {
-    const int32_t w = __builtin_amdgcn_readfirstlane((int32_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+// (gphase + k gstride) runs only the chunks of its tiles. mode (option chunk_mode):
+// bit 0 stages each chunk's face records in LDS first (mesh_chunk_lds); bit 1 hands the
+// items to the XCDs in runs of 16 consecutive chunks (xcd_block: the dispatcher deals
+// blocks round-robin to the 8 XCDs, so neighbouring chunks -- which share faces -- would
+// otherwise pull the same records into all eight L2s).
+__global__ __launch_bounds__(64) void k_mesh_chunks(const KParams* __restrict__ Pp, const Launch L,
+                                                    const int2* __restrict__ items, int32_t n, uint2* __restrict__ out,
+                                                    int32_t mode) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __shared__ ChunkLds sh;
+#endif
+    const uint32_t b = (mode & 2) ? xcd_block(blockIdx.x, gridDim.x, 1) : blockIdx.x;
+    const int32_t w = __builtin_amdgcn_readfirstlane((int32_t)b);
     if (w >= n) return;
     const int2 it = items[w];
     const int32_t ty = it.x / Pp->S.bins_x;  // the tile's 8-row group
@@ -751,6 +816,12 @@ __global__ __launch_bounds__(256) void k_mesh_chunks(const KParams* __restrict__
     if (!mine) return;
     const int lane = threadIdx.x & 63;
     const int64_t slot = Pp->S.bin_heavy[it.x];
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (mode & 1) {
+        out[(slot + it.y) * 64 + lane] = mesh_chunk_lds(*Pp, it.x, it.y, lane, sh);
+        return;
+    }
+#endif
     out[(slot + it.y) * 64 + lane] = mesh_chunk(*Pp, it.x, it.y, lane);
 }
 // (v * 255.0) truncated to uint8, four values per thread: one 16-byte load and one 4-byte

@@ -144,8 +144,11 @@ class FrameGraph:
     render.nu:10-15, provided/glue.py:17-27), issued without per-frame Python: this rank's
     render of its rows (uint8, main.py:33's conversion fused), the RCCL gather
     (FrameGather) and, on ``dst``, the reorder into image order are recorded ONCE as a HIP
-    graph and replayed per frame -- ``step()`` is one graph launch, ``run(n)`` launches n
-    frames from C (rtx_graph_launch: one hipGraphLaunch of host time per frame).
+    graph and replayed per frame -- ``step()`` is one graph launch; ``run(n)`` launches n
+    frames from C (rtx_graph_launch), ``frames_per_graph`` of them per graph: a second graph
+    records that many frames one after the other (each still rendered, gathered and
+    reordered in stream order before the next), so a frame costs 1 / frames_per_graph of
+    a hipGraphLaunch of host time (~4.6 us per launch on the MI355X box, profiles/r06/s2).
 
     Partition: contiguous np.array_split row blocks for one-sample frames (``interleave``
     None and samples_per_pixel == 1): with N | H they arrive in image order and the gathered
@@ -162,7 +165,7 @@ class FrameGraph:
     inject the host emulation."""
 
     def __init__(self, scene, rank, world, dst=0, group=None, device=None, interleave=None, render_block=None,
-                 graph=True, collective_at_one=False):
+                 graph=True, collective_at_one=False, frames_per_graph=8):
         H, W = scene.vc.height, scene.vc.width
         device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         if interleave is None:
@@ -185,7 +188,9 @@ class FrameGraph:
                     scene.render_device(row0=r0, nrows=n, out=out)
         self.render_block = render_block
         self.graph_on = graph and device.type == "cuda"
-        self.graph = None
+        self.kmax = max(1, int(frames_per_graph))
+        self.graph = None   # one frame
+        self.graphk = None  # kmax frames
         self._state = None
 
     def _issue(self):
@@ -227,8 +232,14 @@ class FrameGraph:
         gr = torch.cuda.CUDAGraph()
         with torch.cuda.graph(gr, capture_error_mode="thread_local"):
             self._issue()
+        gk = None
+        if self.kmax > 1:
+            gk = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gk, capture_error_mode="thread_local"):
+                for _ in range(self.kmax):
+                    self._issue()
         torch.cuda.synchronize()
-        self.graph = gr
+        self.graph, self.graphk = gr, gk
 
     def step(self):
         """Issue one frame (asynchronous; frames are stream-ordered, so each one's gather is
@@ -244,8 +255,9 @@ class FrameGraph:
         self.graph.replay()
 
     def run(self, n, stream=None):
-        """Issue n frames: one rtx_graph_launch call (n hipGraphLaunch from C) when the frame
-        is a graph, else n eager frames."""
+        """Issue n frames: rtx_graph_launch calls (n / frames_per_graph launches of the
+        multi-frame graph, then the rest one frame each) when the frame is a graph, else n
+        eager frames."""
         if n <= 0:
             return
         if self.graph_on and (self.graph is None or self._scene_state() != self._state):
@@ -255,9 +267,12 @@ class FrameGraph:
                 self._issue()
             return
         from . import _native as N
-        st = stream if stream is not None else torch.cuda.current_stream()
-        N.call("rtx_graph_launch", ctypes.c_void_p(self.graph.raw_cuda_graph_exec()), int(n),
-               ctypes.c_void_p(st.cuda_stream))
+        st = ctypes.c_void_p((stream if stream is not None else torch.cuda.current_stream()).cuda_stream)
+        q, r = divmod(int(n), self.kmax) if self.graphk is not None else (0, int(n))
+        if q:
+            N.call("rtx_graph_launch", ctypes.c_void_p(self.graphk.raw_cuda_graph_exec()), q, st)
+        if r:
+            N.call("rtx_graph_launch", ctypes.c_void_p(self.graph.raw_cuda_graph_exec()), r, st)
 
     def frame(self):
         """The last frame on ``dst`` ([H, W, 3] uint8, valid until the next step), None

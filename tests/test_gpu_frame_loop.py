@@ -95,7 +95,8 @@ def test_frame_exchange_graph_mode_recaptures_after_camera_change(pg):
         assert np.array_equal(f.cpu().numpy(), want_a if k < 2 else want_b), k
 
 
-@pytest.mark.parametrize("name,interleave", [("TwoSpheresPlane", None), ("MirrorRefraction", True)])
+@pytest.mark.parametrize("name,interleave", [("TwoSpheresPlane", None), ("MirrorRefraction", None),
+                                             ("MirrorRefraction", True)])
 def test_frame_graph_replays_render_and_gather(pg, name, interleave):
     """bench.py's N > 1 value loop (rtx.distributed.FrameGraph): this rank's render, the RCCL
     gather (issued even at world 1: collective_at_one) and -- for interleaved rows -- rank
@@ -106,16 +107,22 @@ def test_frame_graph_replays_render_and_gather(pg, name, interleave):
     sc = product_scene(name)
     want = _png(name)
     fg = FrameGraph(sc, 0, 1, interleave=interleave, collective_at_one=True)
-    assert fg.interleave == (interleave is True)  # one-sample frames: contiguous blocks by default
+    # by default one-sample frames (MirrorRefraction) in contiguous blocks, multi-sample ones
+    # (the published TwoSpheresPlane: 3 samples) in interleaved groups, reordered in the graph
+    assert fg.interleave == (interleave is True or sc.samples_per_pixel > 1)
     for _ in range(3):
         fg.step()
     torch.cuda.synchronize()
     assert fg.graph is not None, sc.last_kernel
     assert np.array_equal(fg.frame().cpu().numpy(), want)
-    fg.g.recv.zero_()
-    fg.run(4)
-    torch.cuda.synchronize()
-    assert np.array_equal(fg.frame().cpu().numpy(), want)
+    for n in (4, 11):  # one-frame launches; one 8-frame graph launch + 3 one-frame ones
+        fg.g.recv.zero_()
+        if fg.out is not None:
+            fg.out.zero_()
+        fg.run(n)
+        torch.cuda.synchronize()
+        assert np.array_equal(fg.frame().cpu().numpy(), want), n
+    assert fg.graphk is not None and fg.kmax == 8
     first = fg.graph
     # a camera change uploads new tables: the next step records a new graph
     sc.vc.set_camera([1.0, 2.5, 6.0], [0.0, 0.5, 0.0], [0.0, 1.0, 0.0], 40)
