@@ -2371,6 +2371,20 @@ struct CamStage {
     template <class T>
     size_t put(const std::vector<T>& v) { return put(v.empty() ? nullptr : v.data(), sizeof(T) * v.size()); }
     size_t size() const { return (bytes + 15) & ~(size_t)15; }  // (whole 16-byte words)
+    // the byte ranges to upload: the segments not filled on the device, merged, in whole
+    // 16-byte words (a segment's next neighbour starts 256-aligned, so the rounding stays
+    // short of it)
+    std::vector<std::pair<size_t, size_t>> runs() const {
+        std::vector<std::pair<size_t, size_t>> r;
+        for (const Seg& g : segs) {
+            if (g.dev) continue;
+            const size_t end = (g.off + std::max<size_t>(g.n, 4) + 15) & ~(size_t)15;
+            if (!r.empty() && r.back().second == g.off) r.back().second = end;
+            else if (!r.empty() && ((r.back().second + 255) & ~(size_t)255) == g.off) r.back().second = end;
+            else r.emplace_back(g.off, end);
+        }
+        return r;
+    }
     void write(char* h) const {
         for (const Seg& g : segs) {
             if (g.p) memcpy(h + g.off, g.p, g.n);
@@ -2625,6 +2639,10 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
             hipLaunchKernelGGL(k_stage_copy, dim3(1), dim3(64), 0, nullptr, nullptr, nullptr, (int64_t)0);
             (void)hipGetLastError();
         });
+        // a scene whose one mesh gets device face bins: the sorts' one-time setup (once per
+        // process), here rather than in the first camera upload
+        static std::once_flag sorts;
+        if (H.n_mesh == 1 && opt_on(OPT_DEV_BINS)) std::call_once(sorts, [] { mesh_bins_warm(); });
     }
     *out = s;
     return RTX_OK;
@@ -2750,7 +2768,7 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     if (heavy) {
         o_bheavy = st.put(bheavy);
         o_hitems = st.put(hitems);
-        o_mhits = st.put(nullptr, sizeof(uint2) * 64 * hitems.size());
+        o_mhits = st.put(nullptr, sizeof(uint2) * 64 * hitems.size(), true);  // (the chunk pass writes it)
     }
     slog.mark("bins", st.size());
     // the measured tile schedule (tile_schedule): identity order until measured
@@ -2763,7 +2781,7 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
         ident.resize((size_t)nw);
         std::iota(ident.begin(), ident.end(), 0);
         o_tperm = st.put(ident);
-        o_ttime = st.put(nullptr, sizeof(uint32_t) * nw);
+        o_ttime = st.put(nullptr, sizeof(uint32_t) * nw, true);  // (a measured frame writes it before it is read)
     }
     const size_t o_kp = st.put(nullptr, sizeof(KParams));
     slog.mark("tile schedule", st.size());
@@ -2849,12 +2867,8 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     if ((rc = pinned_reserve(s, st.size()))) return rc;
     st.write(s->h_cam);
     memcpy(s->h_cam + o_kp, &k, sizeof(KParams));
-    if (dev_faces) {  // (the device fills the face lists: the upload skips their segments)
-        const size_t cut0 = o_bfaces, cut1 = a256(o_bz + sizeof(float) * dev_pairs);
-        if ((rc = pinned_upload(s, D, cut0)) || (rc = pinned_upload(s, D + cut1, st.size() - cut1, cut1))) return rc;
-    } else if ((rc = pinned_upload(s, D, st.size()))) {
-        return rc;
-    }
+    for (const auto& r : st.runs())  // (the segments the device fills are not uploaded)
+        if ((rc = pinned_upload(s, D + r.first, r.second - r.first, r.first))) return rc;
     slog.mark("upload");
     if (dev_faces) {
         if ((rc = mesh_bins_dev2(s, bins_x, (int32_t)(bstart.size() - 1), dev_pairs, reinterpret_cast<int32_t*>(D + o_bfaces),

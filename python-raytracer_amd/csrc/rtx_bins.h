@@ -117,6 +117,9 @@ struct MeshBinsDev {
     void* tmp;         // hipcub scratch
     size_t tmp_bytes;
 };
+// the sorts' one-time setup (rtx_scene_create of a scene with one mesh, so that the first
+// camera upload does not pay it)
+void mesh_bins_warm();
 // device bytes of the first stage (faces n) and of the second (npairs), incl. scratch
 size_t mesh_bins_bytes1(int32_t n, int32_t nb);
 size_t mesh_bins_bytes2(int32_t n, int32_t npairs);

@@ -90,6 +90,13 @@ size_t sort_keys_tmp(int32_t n) {
 
 }  // namespace
 
+void mesh_bins_warm() {
+    // rocPRIM picks its sort configuration from the device's arch, read once per process
+    // with hipGetDeviceProperties (~8 ms the first time, profiles/r06/s3/setup_blob.err)
+    (void)sort_pairs_tmp(1 << 16);
+    (void)sort_keys_tmp(1 << 16);
+}
+
 size_t mesh_bins_bytes1(int32_t n, int32_t nb) {
     return align256(sizeof(int4) * n) + align256(sizeof(double) * n) + align256(sizeof(int32_t) * (nb + 1)) +
            align256(sizeof(int32_t)) + 2 * align256(sizeof(uint64_t) * n) + 2 * align256(sizeof(int32_t) * n) +

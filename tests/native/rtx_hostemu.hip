@@ -11,6 +11,7 @@ hipError_t launch_render_ext_m0(int, const RenderLaunch&, const Launch&) { retur
 hipError_t launch_render_ext_m1(int, const RenderLaunch&, const Launch&) { return hipErrorNotSupported; }
 hipError_t launch_split_m0(int, int, const RenderLaunch&, const Launch&, const SplitBuf&) { return hipErrorNotSupported; }
 hipError_t launch_split_m1(int, int, const RenderLaunch&, const Launch&, const SplitBuf&) { return hipErrorNotSupported; }
+void mesh_bins_warm() {}
 size_t mesh_bins_bytes1(int32_t, int32_t) { return 0; }
 size_t mesh_bins_bytes2(int32_t, int32_t) { return 0; }
 hipError_t mesh_bins_stage1(const BinProj&, const float*, int32_t, int32_t, int32_t, int32_t, void*, MeshBinsDev&,
