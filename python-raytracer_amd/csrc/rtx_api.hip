@@ -74,7 +74,7 @@ enum Opt {
     OPT_SPLIT, OPT_SPLIT_BYTES, OPT_SPLIT_RATIO, OPT_BINS, OPT_HEAVY_TILES, OPT_LENS_BINS, OPT_LGRID, OPT_DSGRID, OPT_DSGRID_MIN,
     OPT_SELF_SKIP, OPT_TILE_SCHED, OPT_XCD_MAP, OPT_TILE_BLOCK, OPT_PRIM_ORIGIN, OPT_SPP, OPT_SPP_MIN, OPT_JIT, OPT_JIT_BAKE, OPT_JIT_EXT,
     OPT_JIT_DUMP, OPT_JIT_IDLE_BAKED, OPT_JIT_DISK_BAKED, OPT_JIT_CACHE, OPT_JIT_FLAGS, OPT_JIT_ILP, OPT_JIT_ASYNC,
-    OPT_DEV_BINS, OPT_CHUNK_MODE, OPT_SETUP_LOG, OPT_COUNT
+    OPT_DEV_BINS, OPT_CHUNK_MODE, OPT_BIN_LDS, OPT_SETUP_LOG, OPT_COUNT
 };
 struct OptDef {
     const char* name;
@@ -110,6 +110,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"jit_async", 1, false},                  // compile on a host thread; the generic kernel renders meanwhile
     {"dev_bins", 1, false},                   // a mesh's primary-ray face bins built on the device
     {"chunk_mode", 3, false},                 // heavy-tile pass: bit 0 LDS-staged faces, bit 1 XCD-aware order
+    {"bin_lds", 0, false},                    // primary-ray face lists staged in LDS (specialized mesh kernels)
     {"setup_log", 0, false},                  // print the host time of each rtx_camera_set step
 };
 struct OptVal {
@@ -1879,6 +1880,8 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
         opts.push_back("-DRTX_LB_WAVES(MESH,SEC)=7");
     }
     opts.push_back(std::string("-DRTX_PRIMARY_BINS=") + (kp.S.bins_on ? "1" : "0"));
+    // a mesh's face bins read through LDS (rtx_trace.h BinLds; option bin_lds)
+    if (mesh && !ext && kp.S.bins_on && kp.S.mesh_bins && opt_on(OPT_BIN_LDS)) opts.push_back("-DRTX_BIN_LDS=1");
     opts.push_back(std::string("-DRTX_LIGHT_GRIDS=") + (v.lgrid_on ? "1" : "0"));
     opts.push_back(std::string("-DRTX_DIR_GRIDS=") + (kp.S.dsg_on ? "1" : "0"));
     // (records and mesh data staged in LDS -- RTX_LDS_OBJS / RTX_LDS_TRIS kernels -- measured

@@ -91,10 +91,26 @@ size_t sort_keys_tmp(int32_t n) {
 }  // namespace
 
 void mesh_bins_warm() {
-    // rocPRIM picks its sort configuration from the device's arch, read once per process
-    // with hipGetDeviceProperties (~8 ms the first time, profiles/r06/s3/setup_blob.err)
-    (void)sort_pairs_tmp(1 << 16);
-    (void)sort_keys_tmp(1 << 16);
+    // The first sort of a process costs ~8 ms (profiles/r06/s3/setup_blob.err: rocPRIM
+    // reads the device's properties with hipGetDeviceProperties and clears its scan state
+    // with hipMemsetAsync, whose blit kernels the runtime loads on first use): one tiny
+    // sort of each kind, here, so that the first camera upload does not pay it.
+    constexpr int32_t n = 256;
+    const size_t tp = sort_pairs_tmp(n), tk = sort_keys_tmp(n);
+    const size_t bytes = 4 * align256(sizeof(uint64_t) * n) + align256(tp) + align256(tk);
+    char* p = nullptr;
+    if (hipMalloc((void**)&p, bytes) != hipSuccess) return;
+    uint64_t* k0 = reinterpret_cast<uint64_t*>(p);
+    uint64_t* k1 = reinterpret_cast<uint64_t*>(p + align256(sizeof(uint64_t) * n));
+    int32_t* v0 = reinterpret_cast<int32_t*>(p + 2 * align256(sizeof(uint64_t) * n));
+    int32_t* v1 = reinterpret_cast<int32_t*>(p + 3 * align256(sizeof(uint64_t) * n));
+    char* t = p + 4 * align256(sizeof(uint64_t) * n);
+    size_t tpb = tp, tkb = tk;
+    if (hipMemsetAsync(p, 0, 4 * align256(sizeof(uint64_t) * n), nullptr) == hipSuccess &&
+        hipcub::DeviceRadixSort::SortPairs(t, tpb, k0, k1, v0, v1, n, 0, 64, nullptr) == hipSuccess)
+        (void)hipcub::DeviceRadixSort::SortKeys(t + align256(tp), tkb, k0, k1, n, 0, 64, nullptr);
+    (void)hipStreamSynchronize(nullptr);
+    (void)hipFree(p);
 }
 
 size_t mesh_bins_bytes1(int32_t n, int32_t nb) {

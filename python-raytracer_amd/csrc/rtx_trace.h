@@ -382,6 +382,31 @@ __shared__ DLeaf g_lds_leaves[RTX_LDS_LEAVES];
 #define RTX_LEAF(S, i) ((S).leaves[i])
 #endif
 
+// A primary-ray tile's face list staged in LDS (RTX_BIN_LDS, scene-specialized mesh
+// kernels; option bin_lds): kHeavyChunk faces at a time, their indices, depth bounds and
+// records fetched by the wave's active lanes with coalesced 16-byte loads, then read from
+// LDS by the closest-hit loop -- one round of memory latency per 32 faces instead of two
+// or three dependent scalar loads per face. One slot per wave of the block.
+#if defined(RTX_BIN_LDS) && RTX_BIN_LDS && defined(__HIP_DEVICE_COMPILE__)
+struct BinLds {
+    DTri tri[kHeavyChunk];
+    DFaceBox box[kHeavyChunk];
+    int32_t face[kHeavyChunk];
+    float zmin[kHeavyChunk];
+};
+#ifdef RTX_BLOCK_FLAT
+__shared__ BinLds g_bin_lds[RTX_BLOCK_FLAT / 64];
+#else
+__shared__ BinLds g_bin_lds[4];  // (256-thread blocks, rtx_kernels.h kBlock)
+#endif
+// rocPRIM's wave_barrier: LDS written by some lanes is read by others of the same wave
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+#endif
+
 // Object and material records fetched with a per-lane index (the hit object of each lane,
 // its material): scene-specialized kernels built with RTX_LDS_OBJS / RTX_LDS_MATS (the
 // scene's record counts) copy both tables into LDS once per block (render_body), so these
@@ -1944,12 +1969,56 @@ RTX_HD Hit closest_hit(const SceneView& S, f3 o, f3 d, float time, Tally& tl, co
                     }
                     continue;
                 }
+#if defined(RTX_BIN_LDS) && RTX_BIN_LDS && defined(__HIP_DEVICE_COMPILE__)
+                {
+                    BinLds& sh = g_bin_lds[threadIdx.x >> 6];
+                    const uint64_t act = __builtin_amdgcn_ballot_w64(true);  // (the lanes tracing here)
+                    const int na = __builtin_popcountll(act);
+                    const int rk = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+                    constexpr int kTriW = (int)(sizeof(DTri) / 16), kW = kTriW + (int)(sizeof(DFaceBox) / 16);
+                    bool done = false;
+                    for (int32_t qb = S.bin_start[ub]; qb < q1 && !done; qb += kHeavyChunk) {
+                        if (RTX_ALL(h.t32 < S.bin_zmin[qb])) break;  // (the loop below's first exit test)
+                        const int n = min(q1 - qb, kHeavyChunk);
+                        wave_lds_sync();  // (the previous block's reads are done)
+                        for (int i = rk; i < n; i += na) {
+                            sh.face[i] = S.bin_faces[qb + i];
+                            sh.zmin[i] = S.bin_zmin[qb + i];
+                        }
+                        wave_lds_sync();
+                        for (int w = rk; w < n * kW; w += na) {
+                            const int i = w / kW, k = w - i * kW;
+                            const int64_t f = ob.tri_begin + sh.face[i];
+                            if (k < kTriW)
+                                reinterpret_cast<uint4*>(&sh.tri[i])[k] = reinterpret_cast<const uint4 RTX_CONST*>(&S.tris[f])[k];
+                            else
+                                reinterpret_cast<uint4*>(&sh.box[i])[k - kTriW] =
+                                    reinterpret_cast<const uint4 RTX_CONST*>(&S.fboxes[f])[k - kTriW];
+                        }
+                        wave_lds_sync();
+                        for (int i = 0; i < n; ++i) {
+                            // faces come nearest first: once every lane's best hit precedes a
+                            // face's nearest possible t, no later face can win (or tie)
+                            if (RTX_ALL(h.t32 < sh.zmin[i])) { done = true; break; }
+                            const DFaceBox B = sh.box[i];
+                            const bool fmaybe = leaf_maybe_hit(B, o, ri, ob.cmax, h.t32);
+                            if (!RTX_ANY(fmaybe)) continue;
+                            tally_inc<COUNT>(tl, &Tally::tri);
+                            float t32;
+                            const bool valid = tri_hit(sh.tri[i], o, d, fmaybe, t32);
+                            offer(S, h, valid, t32, oi, sh.face[i], o, d, time);
+                        }
+                    }
+                }
+#else
                 for (int32_t q = S.bin_start[ub]; q < q1; ++q) {
                     // faces come nearest first: once every lane's best hit precedes a
                     // face's nearest possible t, no later face can win (or tie)
                     if (RTX_ALL(h.t32 < S.bin_zmin[q])) break;
                     test_face(S.bin_faces[q], true, true);
                 }
+#endif
                 continue;
             }
             for (int li = 0; li < ob.leaf_count;) {  // stackless wave-uniform BVH walk

@@ -529,8 +529,10 @@ extern "C" int64_t rtx_hostemu_jit_spec(const rtx_scene_desc* sd, const rtx_came
     int32_t bins_x = 0, mesh_bins = 0;
     std::vector<DBound> nodeb;
     if (!H.nodes.empty()) nodeb = compute_bounds(H.nodes, H.objs, H.tris, *tmm.first, *tmm.second);
-    if (opt_on(OPT_BINS) && primary_bins(H, cd, nodeb, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins))
+    if (opt_on(OPT_BINS) && primary_bins(H, cd, nodeb, bstart, bfaces, bz, bmask, brmask, bins_x, mesh_bins)) {
         k.S.bins_on = 1;
+        k.S.mesh_bins = mesh_bins;
+    }
     const int spp = k.n_dof * k.n_aa * k.n_times;
     const bool spp_mode = use_spp_mode(spp, H.has_ext);
     JitSpec sp;
