@@ -229,17 +229,60 @@ class FrameGraph:
             self.graph_on = False
             self.graph = None
             return
-        gr = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(gr, capture_error_mode="thread_local"):
-            self._issue()
-        gk = None
-        if self.kmax > 1:
-            gk = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gk, capture_error_mode="thread_local"):
-                for _ in range(self.kmax):
-                    self._issue()
-        torch.cuda.synchronize()
+        ref = self.frame().clone() if self.rank == self.dst else None
+        gr = gk = None
+        ok, why = True, ""
+        try:
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr, capture_error_mode="thread_local"):
+                self._issue()
+            if self.kmax > 1:
+                gk = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gk, capture_error_mode="thread_local"):
+                    for _ in range(self.kmax):
+                        self._issue()
+            torch.cuda.synchronize()
+        except Exception as e:  # noqa: BLE001 -- a backend that cannot record its collective
+            ok, why = False, "capture failed on rank %d: %r" % (self.rank, e)
+        ok = self._agree(ok)  # (every rank records, or none: the frame loop stays eager)
+        if ok:
+            # one replay of each graph, which must finish and deliver the eager frame's bytes
+            for g in (gr, gk):
+                if g is not None:
+                    self._replay_checked(g)
+            same = True if ref is None else bool(torch.equal(self.frame(), ref))
+            ok = self._agree(same)
+            if not ok:
+                why = "a replayed frame differs from the eager frame"
+        if not ok:
+            import warnings
+            warnings.warn("FrameGraph: issuing frames eagerly (%s)" % (why or "another rank could not record"))
+            self.graph_on = False
+            self.graph = self.graphk = None
+            return
         self.graph, self.graphk = gr, gk
+
+    def _agree(self, ok):
+        """Whether every rank's ok holds (an all_reduce, outside any capture)."""
+        if not (self.collective and dist.is_available() and dist.is_initialized()):
+            return ok
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.g.send.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.g.group)
+        return bool(t.item())
+
+    @staticmethod
+    def _replay_checked(g, timeout_s=60.0):
+        """Replay g once and wait for it, bounded: a collective that never completes inside
+        a graph raises instead of hanging the frame loop."""
+        import time
+        ev = torch.cuda.Event()
+        g.replay()
+        ev.record()
+        t0 = time.perf_counter()
+        while not ev.query():
+            if time.perf_counter() - t0 > timeout_s:
+                raise RuntimeError("FrameGraph: a replayed frame did not complete in %.0f s" % timeout_s)
+            time.sleep(1e-4)
 
     def step(self):
         """Issue one frame (asynchronous; frames are stream-ordered, so each one's gather is

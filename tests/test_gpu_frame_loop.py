@@ -132,3 +132,26 @@ def test_frame_graph_replays_render_and_gather(pg, name, interleave):
     moved = product_scene(name)
     moved.vc.set_camera([1.0, 2.5, 6.0], [0.0, 0.5, 0.0], [0.0, 1.0, 0.0], 40)
     assert np.array_equal(fg.frame().cpu().numpy(), moved.render_rgb8())
+
+
+def test_frame_graph_falls_back_to_eager_when_recording_fails(pg, monkeypatch):
+    """A backend that cannot record its collective into a graph: every rank agrees (an
+    all_reduce outside the capture) to issue the frames eagerly, with a warning, and the
+    frames are still the published PNG."""
+    import contextlib
+    from rtx.distributed import FrameGraph
+
+    @contextlib.contextmanager
+    def refuses(*a, **k):
+        raise RuntimeError("operation not permitted when stream is capturing (simulated)")
+        yield
+    sc = product_scene("MirrorRefraction")
+    want = _png("MirrorRefraction")
+    fg = FrameGraph(sc, 0, 1, collective_at_one=True)
+    monkeypatch.setattr(torch.cuda, "graph", refuses)
+    with pytest.warns(UserWarning, match="eagerly"):
+        fg.step()
+    assert not fg.graph_on and fg.graph is None
+    fg.run(3)
+    torch.cuda.synchronize()
+    assert np.array_equal(fg.frame().cpu().numpy(), want)
