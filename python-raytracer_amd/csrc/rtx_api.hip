@@ -2760,8 +2760,10 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
         if (bfaces.empty() && !dev_faces) { bfaces.push_back(0); bz.push_back(0.0f); }
         bmask.insert(bmask.end(), brmask.begin(), brmask.end());  // [object masks | root masks]
         o_bstart = st.put(bstart);
-        o_bfaces = dev_faces ? st.put(nullptr, sizeof(int32_t) * dev_pairs, true) : st.put(bfaces);
-        o_bz = dev_faces ? st.put(nullptr, sizeof(float) * dev_pairs, true) : st.put(bz);
+        if (!dev_faces) {  // (the device-filled lists go last: below)
+            o_bfaces = st.put(bfaces);
+            o_bz = st.put(bz);
+        }
         o_bmask = st.put(bmask);
     }
     std::vector<int32_t> bheavy;
@@ -2771,7 +2773,7 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
     if (heavy) {
         o_bheavy = st.put(bheavy);
         o_hitems = st.put(hitems);
-        o_mhits = st.put(nullptr, sizeof(uint2) * 64 * hitems.size(), true);  // (the chunk pass writes it)
+        // (o_mhits: below, device-filled)
     }
     slog.mark("bins", st.size());
     // the measured tile schedule (tile_schedule): identity order until measured
@@ -2784,9 +2786,22 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
         ident.resize((size_t)nw);
         std::iota(ident.begin(), ident.end(), 0);
         o_tperm = st.put(ident);
-        o_ttime = st.put(nullptr, sizeof(uint32_t) * nw, true);  // (a measured frame writes it before it is read)
+        // (o_ttime: below, device-filled)
     }
     const size_t o_kp = st.put(nullptr, sizeof(KParams));
+    // the segments the device fills, last: the host stages (and uploads) only what precedes
+    // them -- the face lists of device bins, the heavy tiles' per-frame hits (the chunk pass
+    // writes them) and the tile times (a measured frame writes them before they are read)
+    const size_t host_bytes = st.size();
+    if (dev_faces) {
+        o_bfaces = st.put(nullptr, sizeof(int32_t) * dev_pairs, true);
+        o_bz = st.put(nullptr, sizeof(float) * dev_pairs, true);
+    }
+    if (heavy) o_mhits = st.put(nullptr, sizeof(uint2) * 64 * hitems.size(), true);
+    if (tsched) {
+        const int64_t nw = (tiles + kBlock<false> / 64 - 1) / (kBlock<false> / 64) * (kBlock<false> / 64);
+        o_ttime = st.put(nullptr, sizeof(uint32_t) * nw, true);
+    }
     slog.mark("tile schedule", st.size());
     // one device buffer for all of it, reused while large enough; its old contents may still
     // be read by frames of the previous camera
@@ -2867,7 +2882,7 @@ int rtx_camera_set(rtx_scene* s, const rtx_camera_desc* c) {
         s->d_tile_time = D + o_ttime;
         s->tile_sched = 1;
     }
-    if ((rc = pinned_reserve(s, st.size()))) return rc;
+    if ((rc = pinned_reserve(s, host_bytes))) return rc;
     st.write(s->h_cam);
     memcpy(s->h_cam + o_kp, &k, sizeof(KParams));
     for (const auto& r : st.runs())  // (the segments the device fills are not uploaded)
