@@ -308,23 +308,54 @@ def timed(fn, steps, use_dist, sync=cuda_sync, device="cuda"):
     return max_over_ranks(t1 - t0, use_dist, device)
 
 
+def root_shares(world):
+    """Candidate shares of the frame's rows for rank 0 in the value loop's uneven blocks
+    (rtx.distributed.BlockGather): from an even split up to 0.9 -- every rank keeps rows."""
+    c = [1.0 / world, 1.5 / world, 2.0 / world, 3.0 / world, 0.5, 0.6, 0.7, 0.8, 0.9]
+    return sorted(set(round(x, 4) for x in c if 1.0 / world - 1e-9 <= x <= 0.9))
+
+
 def sharded_frame(sc, rank, world, steps, warmup, use_dist, device, sync=cuda_sync, stream=None, render_rows=None,
-                  graph=True, collective_at_one=False):
+                  graph=True, collective_at_one=False, tune=True):
     """ONE frame sharded over the ranks per step (the N > 1 value; rtx.distributed.FrameGraph):
     every step renders this rank's rows of the frame straight to uint8 (fused, one launch),
-    gathers them to rank 0 (one RCCL gather) and, for interleaved rows, puts them in image
-    order on rank 0 -- recorded once as a HIP graph and replayed per frame, so a frame costs
-    one graph launch of host time. Frames are stream-ordered: each frame's gather completes
-    before the next frame renders. No batching and no overlap across frames: the latency of
-    one frame, the reference's one-frame-per-run strip render + glue (render.nu:10-15,
-    provided/glue.py:17-27). The timed loop issues its frames from C, frames_per_graph per
-    graph launch (FrameGraph.run). Partition: contiguous row blocks for one-sample frames (in
-    image order when N | H: no reorder), interleaved 8-row groups otherwise.
+    gathers them to rank 0 (one RCCL collective) and, for interleaved rows, puts them in
+    image order on rank 0 -- recorded once as a HIP graph and replayed per frame, so a frame
+    costs one graph launch of host time. Frames are stream-ordered: each frame's gather
+    completes before the next frame renders. No batching and no overlap across frames: the
+    latency of one frame, the reference's one-frame-per-run strip render + glue
+    (render.nu:10-15, provided/glue.py:17-27). The timed loop issues its frames from C,
+    frames_per_graph per graph launch (FrameGraph.run).
+    Partition: one-sample frames in contiguous row blocks, rank 0's share TUNED before the
+    timed region (tune, N > 1): rank 0's own rows cross no link while every other row is
+    carried into rank 0 by the collective, so the frame is fastest when rank 0 renders more
+    than 1/N of it; each candidate share (root_shares) is timed over
+    the same loop (max over ranks, so every rank picks the same one). Multi-sample frames
+    (render-bound): interleaved 8-row groups, one gather, reordered on rank 0.
     Returns (seconds for `steps` frames, max over ranks; rank 0's last frame [H, W, 3];
-    the loop's host issue cost)."""
+    the loop's description)."""
     from rtx.distributed import FrameGraph
-    fg = FrameGraph(sc, rank, world, dst=0, device=device, render_block=render_rows, graph=graph,
-                    collective_at_one=collective_at_one)
+    H = sc.vc.height
+    blocks = sc.samples_per_pixel == 1
+    tuning, root_rows = [], None
+
+    def build(x):
+        return FrameGraph(sc, rank, world, dst=0, device=device, render_block=render_rows, graph=graph,
+                          collective_at_one=collective_at_one, root_rows=x)
+    if tune and blocks and world > 1:
+        m = max(4, min(steps, 100))
+        for share in root_shares(world):
+            x = min(max(int(round(share * H)), 1), H - (world - 1))
+            fg = build(x)
+            for _ in range(max(1, min(warmup, 3))):
+                fg.step()
+            fg.run(2 * fg.kmax if fg.graph_on else 1, stream)
+            sync()
+            t = timed(lambda: fg.run(m, stream), 1, use_dist, sync, device) / m
+            tuning.append({"root_rows": x, "share": share, "frame_us": round(t * 1e6, 3)})
+            del fg
+        root_rows = min(tuning, key=lambda e: e["frame_us"])["root_rows"]
+    fg = build(root_rows)
     for _ in range(warmup):
         fg.step()
     fg.run(2 * fg.kmax if fg.graph_on else 1, stream)  # (records and warms the multi-frame graph too)
@@ -345,12 +376,21 @@ def sharded_frame(sc, rank, world, steps, warmup, use_dist, device, sync=cuda_sy
     sync()
     last = fg.frame()
     nrows = [len(r) for r in fg.g.rows]
+    if fg.interleave:
+        part = "interleaved 8-row groups, one gather to rank 0, reordered there"
+    elif fg.root_rows is not None:
+        part = ("contiguous row blocks, rank 0 renders rows 0-%d itself (its share tuned over %d candidates), "
+                "the others np.array_split the rest; one all_to_all_single with uneven splits brings them to rank 0 "
+                "in image order" % (fg.root_rows - 1, len(tuning)))
+    else:
+        part = "contiguous row blocks (np.array_split), one gather to rank 0"
     info = {"graph": fg.graph is not None, "frames_per_graph": fg.kmax if fg.graphk is not None else 1,
-            "rows_per_rank": [min(nrows), max(nrows)],
-            "partition": "interleaved 8-row groups" if fg.interleave else "contiguous row blocks (np.array_split)",
-            "in_order": bool(fg.g.in_order),
+            "rows_per_rank": nrows if len(nrows) <= 16 else [min(nrows), max(nrows)],
+            "partition": part, "in_order": bool(fg.g.in_order),
             "host_issue_us_per_frame": round((t1 - t0) * 1e6 / steps, 3),
             "host_issue_step_us_per_frame": round((t3 - t2) * 1e6 / steps, 3)}
+    if tuning:
+        info["root_share_tuning"] = tuning
     return s, (last.clone() if last is not None else None), info
 
 
@@ -416,9 +456,8 @@ def measure_sharded(sc, rank, world, steps, warmup, use_dist, device, sync=cuda_
         "frame_s": frame_s,
         "frame_ms": round(frame_s * 1e3 / steps, 5),
         "rows_per_rank": loop["rows_per_rank"],
-        "partition": loop["partition"] + (" (rank 0's buffer is the frame)" if loop["in_order"] else
-                                          ", reordered on rank 0"),
-        "collective": "one torch.distributed.gather (RCCL) of the ranks' uint8 rows to rank 0 per frame, stream-ordered",
+        "partition": loop["partition"],
+        "collective": "one RCCL collective per frame bringing the ranks' uint8 rows to rank 0, stream-ordered",
         "frame_loop": dict(loop, note="render + gather + reorder recorded as a HIP graph (FrameGraph): the timed "
                                       "frames issued from C, frames_per_graph frames per graph launch "
                                       "(host_issue_us_per_frame); host_issue_step: one Python step() per frame"),

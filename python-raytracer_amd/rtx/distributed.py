@@ -138,6 +138,44 @@ def render_frame(scene, rank, world, render_rows=None, dtype=torch.float32, dst=
     return gather_rows(block, H, world, rank, dst=dst, group=group, interleave=interleave)
 
 
+class BlockGather:
+    """A frame gathered to rank 0 from uneven contiguous row blocks: rank 0 renders rows
+    [0, root_rows) in place, the other ranks split the rest with np.array_split and send
+    their blocks to rank 0 in ONE all_to_all_single with uneven splits (each rank's rows
+    straight to rank 0, nothing elsewhere), landing in image order -- rank 0's buffer IS
+    the frame. Rank 0's own rows cross no link, so giving it more of them balances the
+    render against the other ranks' transfer into rank 0 (FrameGraph ``root_rows``;
+    bench.py tunes the share)."""
+
+    def __init__(self, height, width, world, rank, device, root_rows, group=None):
+        x = int(root_rows)
+        if world < 2 or not 0 < x < height:
+            raise ValueError("root_rows must leave rows to every rank: 0 < %d < %d, world >= 2" % (x, height))
+        self.world, self.rank, self.dst, self.group = world, rank, 0, group
+        rest = [x + b for b in np.array_split(np.arange(height - x), world - 1)]
+        self.rows = [np.arange(0, x)] + rest
+        self.nrows = len(self.rows[rank])
+        self.height, self.in_order = height, True
+        if rank == 0:
+            self.frame_buf = torch.zeros((height, width, 3), dtype=torch.uint8, device=device)
+            self.block = self.frame_buf[:x]
+            self.send = self.frame_buf[:0]
+            self.recv = self.frame_buf[x:]
+            self.in_splits, self.out_splits = [0] * world, [0] + [len(r) for r in rest]
+        else:
+            self.send = torch.zeros((self.nrows, width, 3), dtype=torch.uint8, device=device)
+            self.block = self.send
+            self.recv = torch.empty((0, width, 3), dtype=torch.uint8, device=device)
+            self.in_splits, self.out_splits = [self.nrows if j == 0 else 0 for j in range(world)], [0] * world
+
+    def start(self, async_op=False):
+        return dist.all_to_all_single(self.recv, self.send, output_split_sizes=self.out_splits,
+                                      input_split_sizes=self.in_splits, group=self.group, async_op=async_op)
+
+    def frame(self):
+        return self.frame_buf
+
+
 class FrameGraph:
     """ONE frame sharded over the ranks per step, gathered to ``dst`` and awaited before the
     next step (bench.py's N > 1 value; the reference's strip renders + glue,
@@ -154,6 +192,8 @@ class FrameGraph:
     None and samples_per_pixel == 1): with N | H they arrive in image order and the gathered
     buffer IS the frame; interleaved 8-row groups otherwise (render-bound multi-sample
     frames balance better), put in order by an index_select recorded into the graph.
+    ``root_rows`` (blocks, N > 1, dst 0): rank 0 renders that many rows itself and the
+    others split the rest (BlockGather: one all_to_all_single with uneven splits).
 
     The graph bakes in the scene's device buffers: it is recorded again when the scene's
     upload generation changes (a camera upload or an edit re-upload, checked per ``step``;
@@ -161,17 +201,22 @@ class FrameGraph:
     emulation) issues the same three steps eagerly. ``collective_at_one``: issue the
     (one-rank) gather even at world 1, so a one-rank group records RCCL's calls too
     (tests/test_gpu_frame_loop.py); otherwise world 1 has no collective at all.
-    ``render_block(out)`` fills this rank's rows (uint8 [nrows, W, 3]) -- the CPU tests
-    inject the host emulation."""
+    ``render_block(out, rows)`` fills this rank's rows (uint8 [len(rows), W, 3], image rows
+    ``rows``) -- the CPU tests inject the host emulation."""
 
     def __init__(self, scene, rank, world, dst=0, group=None, device=None, interleave=None, render_block=None,
-                 graph=True, collective_at_one=False, frames_per_graph=8):
+                 graph=True, collective_at_one=False, frames_per_graph=8, root_rows=None):
         H, W = scene.vc.height, scene.vc.width
         device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         if interleave is None:
             interleave = scene.samples_per_pixel > 1
         self.scene, self.rank, self.world, self.dst, self.interleave = scene, rank, world, dst, interleave
-        self.g = FrameGather(H, W, 3, world, rank, torch.uint8, device, interleave=interleave, dst=dst, group=group)
+        self.root_rows = None
+        if root_rows is not None and not interleave and world > 1 and dst == 0:
+            self.root_rows = int(root_rows)
+            self.g = BlockGather(H, W, world, rank, device, self.root_rows, group=group)
+        else:
+            self.g = FrameGather(H, W, 3, world, rank, torch.uint8, device, interleave=interleave, dst=dst, group=group)
         self.rows = self.g.rows[rank]
         self.collective = world > 1 or collective_at_one
         self.out = None
@@ -179,13 +224,11 @@ class FrameGraph:
             self.out = torch.empty((H, W, 3), dtype=torch.uint8, device=device)
         if render_block is None:
             if interleave:
-                def render_block(out):
+                def render_block(out, rows):
                     scene.render_device(groups=(rank, world), out=out)
             else:
-                r0, n = row_block(H, world, rank)
-
-                def render_block(out):
-                    scene.render_device(row0=r0, nrows=n, out=out)
+                def render_block(out, rows):
+                    scene.render_device(row0=int(rows[0]), nrows=len(rows), out=out)
         self.render_block = render_block
         self.graph_on = graph and device.type == "cuda"
         self.kmax = max(1, int(frames_per_graph))
@@ -197,8 +240,10 @@ class FrameGraph:
         """The frame's three steps, in stream order on the current stream."""
         g = self.g
         if g.nrows:
-            self.render_block(g.block)
-        if self.collective:
+            self.render_block(g.block, self.rows)
+        if isinstance(g, BlockGather):
+            g.start()
+        elif self.collective:
             if self.rank != self.dst:
                 dist.gather(g.send, dst=self.dst, group=g.group)
             else:

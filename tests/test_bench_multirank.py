@@ -33,7 +33,7 @@ def _worker(rank, world, port, res, steps, out_q):
     import bench
     import hostemu
     from common import product_scene
-    from rtx.distributed import rank_rows, to_rgb8
+    from rtx.distributed import to_rgb8
     sc = product_scene("MirrorRefraction", res)
     cache = {}
     calls = [0]
@@ -45,11 +45,8 @@ def _worker(rank, world, port, res, steps, out_q):
         calls[0] += 1
         return cache[key]
 
-    # the value loop (rtx.distributed.FrameGraph): one-sample frames in contiguous row blocks
-    mine = rank_rows(res[1], world, rank, sc.samples_per_pixel > 1)
-
-    def render_rows(out):  # the value loop: this rank's rows
-        out.copy_(rows_u8(mine))
+    def render_rows(out, rows):  # the value loop (rtx.distributed.FrameGraph): this rank's rows
+        out.copy_(rows_u8(rows))
 
     def render_block(out, rows):  # FramePipeline
         out.copy_(rows_u8(rows))
@@ -65,6 +62,14 @@ def _worker(rank, world, port, res, steps, out_q):
     out_q.put((rank, mg, None if frame is None else frame.clone().numpy(), calls[0]))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def bench_root_shares(world):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.dirname(here))
+    import bench
+    return bench.root_shares(world)
 
 
 @pytest.mark.parametrize("world,res", [(2, (40, 23)), (3, (33, 26))])
@@ -93,10 +98,17 @@ def test_bench_sharded_frame_loop(world, res):
     assert mg0["frame_s"] > 0 and mg0["frame_ms"] == round(mg0["frame_s"] * 1e3 / steps, 5)
     W, H = res
     assert mg0["throughput"]["Mrays_s"] > 0 and mg0["gather_to_rank0"]["Mrays_s"] > 0
-    blocks = [len(b) for b in np.array_split(np.arange(H), world)]
-    assert mg0["rows_per_rank"] == [min(blocks), max(blocks)]
+    # one-sample frames: contiguous blocks, rank 0's share tuned over the candidate shares
+    # (every rank agrees: the timings are maxima over ranks); every row rendered once
     loop = mg0["frame_loop"]
     assert loop["partition"].startswith("contiguous") and not loop["graph"]  # (gloo: eager)
+    tuned = loop["root_share_tuning"]
+    assert [e["share"] for e in tuned] == bench_root_shares(world)
+    x = min(tuned, key=lambda e: e["frame_us"])["root_rows"]
+    assert mg0["rows_per_rank"][0] == x and sum(mg0["rows_per_rank"]) == H
+    assert all(n > 0 for n in mg0["rows_per_rank"])
+    for r in range(1, world):
+        assert got[r][0]["frame_loop"]["root_share_tuning"] == tuned
     # the fields the 1 -> N comparison needs: the scaling config's sharded frame at N > 1 ...
     sc_f = mg0["scaling_config"]
     assert sc_f["config"] == "dof4k" and sc_f["frame_ms"] > 0 and sc_f["Mrays_s"] > 0
