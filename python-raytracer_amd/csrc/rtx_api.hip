@@ -1751,6 +1751,7 @@ const char* const kLibMacros[] = {
     "-DRTX_TOOLS_BUILD",
 #endif
     "-DRTX_HIER_INLINE=" RTX_STR(RTX_HIER_INLINE),
+    "-DRTX_HEAVY_CHUNK=" RTX_STR(RTX_HEAVY_CHUNK),
 #ifdef RTX_PAD
     "-DRTX_PAD=" RTX_STR(RTX_PAD),
 #endif

@@ -37,7 +37,10 @@ using __hip_internal::uint64_t;
 namespace rtx {
 
 constexpr int kMaxDepth = 10;  // cast_ray(max_recursion=10) (scene.py:81)
-constexpr int kHeavyChunk = 32;  // faces per chunk of a heavy tile's primary-ray list (SceneView::bin_heavy)
+#ifndef RTX_HEAVY_CHUNK  // (a library build knob, forwarded to the hiprtc kernels)
+#define RTX_HEAVY_CHUNK 32
+#endif
+constexpr int kHeavyChunk = RTX_HEAVY_CHUNK;  // faces per chunk of a heavy tile's primary-ray list (SceneView::bin_heavy)
 
 // Cost probes (tools/ablate.sh, tools/ab_jitflags.sh): a tools build of the library
 // (-DRTX_TOOLS_BUILD, tools/build_lib_variant.sh) compiles kernels with -DRTX_ABLATE=n that
