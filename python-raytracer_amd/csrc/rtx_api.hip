@@ -1341,6 +1341,13 @@ bool light_grids(const HostScene& H, std::vector<DLGrid>& grids, std::vector<int
 // Measured on the 81,920-face mesh at 1080p: the silhouette tiles' lists (up to ~770 faces,
 // where lanes that miss the mesh keep the early exit from firing) were tested one face at
 // a time by one wave and set the frame's length. Returns false when no bin is heavy.
+// Lists of at most kHeavyMin faces stay in the render kernel's walk (build knob
+// RTX_HEAVY_MIN, default 32: TorusMesh's lists of 17-32 faces measured 45.9 -> 57.7 us as
+// chunks of 16, profiles/r06/s7/).
+#ifndef RTX_HEAVY_MIN
+#define RTX_HEAVY_MIN 32
+#endif
+constexpr int32_t kHeavyMin = RTX_HEAVY_MIN;
 bool heavy_chunks(const std::vector<int32_t>& bstart, std::vector<int32_t>& bheavy, std::vector<int2>& items) {
     bheavy.clear();
     items.clear();
@@ -1349,7 +1356,7 @@ bool heavy_chunks(const std::vector<int32_t>& bstart, std::vector<int32_t>& bhea
     bheavy.assign(nb, -1);
     for (size_t b = 0; b < nb; ++b) {
         const int32_t len = bstart[b + 1] - bstart[b];
-        if (len <= kHeavyChunk) continue;
+        if (len <= kHeavyMin) continue;
         bheavy[b] = (int32_t)items.size();  // (items in bin order: a bin's chunks are consecutive)
         for (int32_t c = 0; c * kHeavyChunk < len; ++c) items.push_back(make_int2((int32_t)b, c));
     }
