@@ -1342,10 +1342,11 @@ bool light_grids(const HostScene& H, std::vector<DLGrid>& grids, std::vector<int
 // where lanes that miss the mesh keep the early exit from firing) were tested one face at
 // a time by one wave and set the frame's length. Returns false when no bin is heavy.
 // Lists of at most kHeavyMin faces stay in the render kernel's walk (build knob
-// RTX_HEAVY_MIN, default 32: TorusMesh's lists of 17-32 faces measured 45.9 -> 57.7 us as
-// chunks of 16, profiles/r06/s7/).
+// RTX_HEAVY_MIN): with every list longer than 16 chunked, TorusMesh's lists of 17-32 faces
+// measured 45.9 -> 57.7 us (profiles/r06/s7/); from 25 faces on, it is unchanged (45.9 us)
+// and the 81,920-face mesh gains 4 % (0.1560 -> 0.1498 ms, profiles/r06/s8/).
 #ifndef RTX_HEAVY_MIN
-#define RTX_HEAVY_MIN 32
+#define RTX_HEAVY_MIN 24
 #endif
 constexpr int32_t kHeavyMin = RTX_HEAVY_MIN;
 bool heavy_chunks(const std::vector<int32_t>& bstart, std::vector<int32_t>& bheavy, std::vector<int2>& items) {

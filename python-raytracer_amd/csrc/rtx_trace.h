@@ -37,8 +37,11 @@ using __hip_internal::uint64_t;
 namespace rtx {
 
 constexpr int kMaxDepth = 10;  // cast_ray(max_recursion=10) (scene.py:81)
-#ifndef RTX_HEAVY_CHUNK  // (a library build knob, forwarded to the hiprtc kernels)
-#define RTX_HEAVY_CHUNK 32
+// (a library build knob, forwarded to the hiprtc kernels): chunks of 16 faces measured
+// 3-4 % faster than 32 on the 81,920-face mesh (0.1560 -> 0.1498 ms, three rounds on one
+// box, profiles/r06/s8/), 64 slower (0.173 ms, profiles/r06/s6/)
+#ifndef RTX_HEAVY_CHUNK
+#define RTX_HEAVY_CHUNK 16
 #endif
 constexpr int kHeavyChunk = RTX_HEAVY_CHUNK;  // faces per chunk of a heavy tile's primary-ray list (SceneView::bin_heavy)
 
