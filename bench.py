@@ -581,7 +581,7 @@ def main():
     sc.render_device(out=fb)
     torch.cuda.synchronize()
     t6 = time.perf_counter()
-    if first_kernel.startswith("rtx_jit_render_"):
+    if first_kernel.startswith(("rtx_jit_render_", "rtx_jit_split_")):
         how = "specialized kernel, compiled (hiprtc)" if n_cached() > cached0 else \
             "specialized kernel, code object from the disk cache"
     else:

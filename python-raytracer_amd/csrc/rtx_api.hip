@@ -74,7 +74,7 @@ enum Opt {
     OPT_SPLIT, OPT_SPLIT_BYTES, OPT_SPLIT_RATIO, OPT_BINS, OPT_HEAVY_TILES, OPT_LENS_BINS, OPT_LGRID, OPT_DSGRID, OPT_DSGRID_MIN,
     OPT_SELF_SKIP, OPT_TILE_SCHED, OPT_XCD_MAP, OPT_TILE_BLOCK, OPT_PRIM_ORIGIN, OPT_SPP, OPT_SPP_MIN, OPT_JIT, OPT_JIT_BAKE, OPT_JIT_EXT,
     OPT_JIT_DUMP, OPT_JIT_IDLE_BAKED, OPT_JIT_DISK_BAKED, OPT_JIT_CACHE, OPT_JIT_FLAGS, OPT_JIT_ILP, OPT_JIT_ASYNC,
-    OPT_DEV_BINS, OPT_CHUNK_MODE, OPT_BIN_LDS, OPT_SETUP_LOG, OPT_COUNT
+    OPT_DEV_BINS, OPT_CHUNK_MODE, OPT_BIN_LDS, OPT_JIT_CSG, OPT_SETUP_LOG, OPT_COUNT
 };
 struct OptDef {
     const char* name;
@@ -111,6 +111,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"dev_bins", 1, false},                   // a mesh's primary-ray face bins built on the device
     {"chunk_mode", 3, false},                 // heavy-tile pass: bit 0 LDS-staged faces, bit 1 XCD-aware order
     {"bin_lds", 0, false},                    // primary-ray face lists staged in LDS (specialized mesh kernels)
+    {"jit_csg", 1, false},                    // split hierarchy passes specialized on the scene's CSG trees
     {"setup_log", 0, false},                  // print the host time of each rtx_camera_set step
 };
 struct OptVal {
@@ -1963,6 +1964,121 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
     return true;
 }
 
+// A hierarchy scene's node table as the compile-time constants of the specialized split
+// passes (rtx_trace.h namespace csg: the traversals unrolled over the trees, node fields and
+// matrices as literals). "" when the scene does not qualify: a difference with fewer than
+// two children, a non-finite matrix, or trees whose unrolled traversals would be large
+// (csg_cost: node visits of the unrolled code, a deep tree's walk-ups repeat its siblings).
+constexpr int64_t kCsgMaxNodes = 512, kCsgMaxCost = 6000;
+int64_t csg_cost(const std::vector<DNode>& N) {
+    auto kids = [&](int x, const std::function<void(int)>& f) {
+        for (int j = x + 1; j < N[x].end; j = N[j].end) f(j);
+    };
+    std::function<int64_t(int)> inside = [&](int x) -> int64_t {
+        int64_t c = 1;
+        if (N[x].kind != HN_LEAF && N[x].kind != HN_OTHER) kids(x, [&](int j) { c += inside(j); });
+        return c;
+    };
+    std::function<int64_t(int)> material = [&](int x) -> int64_t {
+        int64_t c = 1;
+        if (N[x].kind != HN_LEAF) kids(x, [&](int j) { c += inside(j) + material(j); });
+        return c;
+    };
+    auto walk = [&](int cur, int stop) {
+        int64_t c = 0;
+        for (; cur != stop; cur = N[cur].parent) {
+            const int a = N[cur].parent;
+            if (N[a].kind == HN_INTER || N[a].kind == HN_DIFF) {
+                kids(a, [&](int j) { if (j != cur) c += inside(j); });
+                if (N[a].kind == HN_DIFF && N[cur].cidx != 0) c += material(a + 1);
+            }
+            ++c;
+        }
+        return c;
+    };
+    std::function<int64_t(int, int)> enumerate = [&](int x, int root) -> int64_t {
+        if (N[x].kind == HN_LEAF) return 1 + walk(x, root);
+        int64_t c = 1;
+        kids(x, [&](int j) { c += enumerate(j, root); });
+        return c;
+    };
+    int64_t total = (int64_t)N.size();  // (the shadow walk)
+    for (int r = 0; r < (int)N.size(); r = N[r].end) total += enumerate(r, r);
+    for (int i = 0; i < (int)N.size(); ++i)
+        if (N[i].kind == HN_DIFF) {
+            const int c0 = i + 1, c1 = N[c0].end;
+            total += enumerate(c0, c0) + enumerate(c1, c1) + inside(c0) + inside(c1);
+        }
+    return total;
+}
+std::string jit_csg_tables(const std::vector<DNode>& N) {
+    if (N.empty() || (int64_t)N.size() > kCsgMaxNodes) return "";
+    for (size_t i = 0; i < N.size(); ++i) {
+        const DNode& d = N[i];
+        if (d.kind == HN_DIFF && (i + 1 >= (size_t)d.end || N[i + 1].end >= d.end)) return "";
+        for (int k = 0; k < 16; ++k)
+            if (!std::isfinite(d.M[k]) || !std::isfinite(d.Minv[k])) return "";
+    }
+    if (csg_cost(N) > kCsgMaxCost) return "";
+    std::string s = "namespace rtx_csg {\nstruct CNode {\n    int kind, parent, cidx, depth, end, pkind, obj, mat0, oid;\n};\n";
+    s += "constexpr int kCount = " + std::to_string(N.size()) + ";\nconstexpr CNode kNode[] = {";
+    char buf[160];
+    for (const DNode& d : N) {
+        snprintf(buf, sizeof(buf), "{%d,%d,%d,%d,%d,%d,%d,%d,%d},", d.kind, d.parent, d.cidx, d.depth, d.end, d.pkind,
+                 d.obj, d.mat0, d.oid);
+        s += buf;
+    }
+    auto mats = [&](const char* name, bool inv) {  // hexadecimal float literals: exact
+        s += std::string("};\nconstexpr float ") + name + "[][16] = {";
+        for (const DNode& d : N) {
+            s += "{";
+            for (int k = 0; k < 16; ++k) {
+                snprintf(buf, sizeof(buf), "%af,", (double)(inv ? d.Minv[k] : d.M[k]));
+                s += buf;
+            }
+            s += "},";
+        }
+    };
+    mats("kM", false);
+    mats("kMinv", true);
+    return s + "};\n}  // namespace rtx_csg\n#define RTX_CSG_STATIC 1\n";
+}
+
+// The split pass kernel specialized on a node table (rtx_split.h split_trace / split_shadow,
+// with the static traversals): the library's own kernel build otherwise.
+JitSpec jit_split_spec(const std::string& arch, const std::string& tables, bool mesh, bool sec, bool cnt, bool jit,
+                       int pass) {
+    JitSpec sp;
+    sp.opts = {"--offload-arch=" + arch, "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize"};
+    for (const char* m : kLibMacros) sp.opts.push_back(m);
+    {
+        std::istringstream is(opt_str(OPT_JIT_FLAGS));
+        for (std::string o; is >> o;) sp.opts.push_back(o);
+    }
+    auto b = [](bool x) { return x ? "true" : "false"; };
+    std::string args = std::string("<") + b(mesh);
+    if (pass == 0) {
+        sp.name = "rtx_jit_split_trace_";
+        for (bool f : {mesh, sec, cnt, jit}) sp.name += f ? '1' : '0';
+        args += std::string(", ") + b(sec) + ", " + b(cnt) + ", " + b(jit) + ">";
+    } else {
+        sp.name = "rtx_jit_split_shadow_";
+        for (bool f : {mesh, cnt}) sp.name += f ? '1' : '0';
+        args += std::string(", ") + b(cnt) + ">";
+    }
+#if defined(RTX_TOOLS_BUILD)
+    const std::string tools_guard;
+#else
+    const std::string tools_guard = "#undef RTX_TOOLS_BUILD\n";
+#endif
+    sp.src = tools_guard + tables + "#include \"rtx_split.h\"\nextern \"C\" __global__ __launch_bounds__(rtx::kBlock<true>, " +
+             (pass == 0 ? "RTX_LB_SPLIT_A" : "RTX_LB_SPLIT_B") + ") void " + sp.name +
+             "(const rtx::KParams* __restrict__ Pp, const rtx::Launch L, rtx::SplitBuf sb) {\n  rtx::" +
+             (pass == 0 ? "split_trace" : "split_shadow") + args + "(Pp, L, sb);\n}\n";
+    sp.baked = true;  // (the scene's own kernel: pruned from memory and disk as the baked ones)
+    return sp;
+}
+
 // Scene-specialized kernels compiled on a host thread (option jit_async, the default): a
 // scene's first frames render with the precompiled generic kernel -- the same bytes
 // (tests/test_gpu_parity.py test_scene_specialized_kernel_equals_generic) -- while hiprtc
@@ -2055,6 +2171,7 @@ namespace {
 // Resolves slot r: the specialized kernel from memory or the disk cache, or a compile --
 // started on a host thread (jit_async: r.pending, the generic kernel renders meanwhile) or
 // waited for. r.fn == nullptr and !r.pending: the generic kernel.
+void jit_start(int device, const JitSpec& sp, JitSlot& r);
 void jit_render_kernel(int device, const SceneView& v, const KParams& kp, const SceneTraits& tr, bool mesh, bool sec,
                        bool ext, bool cnt, bool jit, bool spp, bool out8, const std::string& baked, JitSlot& r) {
     r.fn = nullptr;
@@ -2064,6 +2181,24 @@ void jit_render_kernel(int device, const SceneView& v, const KParams& kp, const 
     if (arch.empty()) return;
     JitSpec sp;
     if (!jit_spec(arch, v, kp, tr, mesh, sec, ext, cnt, jit, spp, out8, baked, sp)) return;
+    jit_start(device, sp, r);
+}
+
+// The specialized split pass (pass 0 trace, 1 shadow) of a hierarchy scene whose node table
+// is `tables` (jit_csg_tables; "" or option jit_csg 0: the precompiled passes run).
+void jit_split_kernel(int device, const std::string& tables, bool mesh, bool sec, bool cnt, bool jit, int pass,
+                      JitSlot& r) {
+    r.fn = nullptr;
+    r.pending = false;
+    if (!jit_enabled() || !opt_on(OPT_JIT_CSG) || tables.empty()) return;
+    const std::string arch = device_arch(device);
+    if (arch.empty()) return;
+    jit_start(device, jit_split_spec(arch, tables, mesh, sec, cnt, jit, pass), r);
+}
+
+// Resolves slot r for spec sp: the kernel from memory or the disk cache, or a compile on a
+// host thread (r.pending).
+void jit_start(int device, const JitSpec& sp, JitSlot& r) {
     std::string key = sp.src;
     for (const auto& o : sp.opts) key += "\n" + o;
     r.name = sp.name;
@@ -2193,10 +2328,12 @@ struct rtx_scene {
     void* d_dsg_cells = nullptr;
     // the kernel resolved for each (counters, jitter, sample-parallel) variant of the
     // current camera: looked up (and compiled) once per camera, not per frame; nullptr
-    // after a lookup means the generic kernel
-    JitSlot resolved[16];
+    // after a lookup means the generic kernel; 16-23: the split hierarchy passes
+    // (16 + 4 pass + 2 counters + jitter, jit_split_kernel)
+    JitSlot resolved[24];
     std::string last_kernel;  // name of the kernel the last render call launched
     std::string jit_baked;    // the scene records as constant arrays (jit_baked_records)
+    std::string csg_tables;   // the hierarchy node table (jit_csg_tables)
     // fp32 staging of the rgb8 entry points when no scene-specialized kernel is available
     float* d_scratch = nullptr;
     size_t scratch_floats = 0;
@@ -2591,6 +2728,7 @@ int rtx_scene_create(const rtx_scene_desc* desc, rtx_scene** out) {
     }
     if (!H.nodes.empty()) {
         s->h_nodes = H.nodes;
+        s->csg_tables = jit_csg_tables(H.nodes);
         s->h_objs = H.objs;
         s->h_tris = H.tris;
         if ((rc = upload(&s->d_bounds_abi, std::vector<DBox>(3 * H.nodes.size())))) {
@@ -3170,7 +3308,34 @@ int render_split(rtx_scene* s, Launch L, const KParams* kp, size_t hbytes, hipSt
     // one scene's renders share these buffers: a render on another stream waits for the last one
     if (!capturing && s->split_used && s->split_stream != st)
         RTX_HIP(hipStreamWaitEvent(st, s->split_done, 0));
+    // the trace and shadow passes specialized on the scene's CSG trees, when compiled
+    // (jit_split_kernel; the precompiled passes render meanwhile: the same bytes)
+    JitSlot* sk[2];
+    for (int pass = 0; pass < 2; ++pass) {
+        JitSlot& r = s->resolved[16 + 4 * pass + (cnt ? 2 : 0) + ((sel & 1) ? 1 : 0)];
+        if (!r.done) {
+            r.block = B;
+            jit_split_kernel(s->device, s->csg_tables, s->has_mesh, s->has_secondary, cnt, (sel & 1) != 0, pass, r);
+            if (r.pending && !opt_on(OPT_JIT_ASYNC) && !capturing) jit_poll(r, true);
+            r.done = true;
+        } else if (r.pending && !capturing) {
+            jit_poll(r, false);
+        }
+        sk[pass] = &r;
+    }
+    if (sk[0]->fn && sk[1]->fn && jit_enabled()) {
+        s->last_kernel = "rtx_jit_split_";
+        for (bool f : {s->has_mesh, s->has_secondary, cnt, (sel & 1) != 0}) s->last_kernel += f ? '1' : '0';
+    }
     auto launch = [&](int pass, const RenderLaunch& r, const Launch& Lc, const SplitBuf& sb) {
+        if (pass < 2 && sk[pass]->fn && jit_enabled()) {
+            const KParams* kpp = r.kp;
+            Launch La = Lc;
+            SplitBuf sbb = sb;
+            void* args[] = {(void*)&kpp, (void*)&La, (void*)&sbb};
+            return hipModuleLaunchKernel(sk[pass]->fn, r.nblocks, 1, 1, B, 1, 1, (unsigned)r.lds_bytes, r.stream, args,
+                                         nullptr);
+        }
         return s->has_mesh ? launch_split_m1(sel, pass, r, Lc, sb) : launch_split_m0(sel, pass, r, Lc, sb);
     };
     char* base = reinterpret_cast<char*>(L.fb);

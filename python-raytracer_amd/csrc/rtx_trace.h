@@ -14,6 +14,7 @@
 using __hip_internal::int32_t;
 using __hip_internal::int64_t;
 using __hip_internal::uint8_t;
+using __hip_internal::uint16_t;
 using __hip_internal::uint32_t;
 using __hip_internal::uint64_t;
 #ifndef INFINITY
@@ -1493,6 +1494,296 @@ RTX_HD bool diff_shadow(const SceneView& S, const HStack& hs, int x, float time)
     return found;
 }
 
+// Best hierarchy hit: the surface the walk-up produced (world frame).
+constexpr int32_t kHierHit = -2;  // Hit.obj of a hierarchy hit; Hit.sub then holds the root's oid
+struct HHit {
+    double t64;
+    f3 pos, n;
+    int32_t mat, gobj;  // gobj: the leaf DObj (Plane/AABB get_diffuse), -1 otherwise
+};
+
+#if defined(RTX_CSG_STATIC)
+// ---- Hierarchies with their shape as compile-time constants (the scene-specialized split
+// passes, rtx_api.hip jit_csg_tables): the traversals above -- the same tests in the same
+// order, the same wave votes, the same arithmetic -- unrolled over the scene's node table
+// (rtx_csg::kNode, kM, kMinv in the kernel's source), so node fields and matrices are
+// literals and no traversal step waits on a node record. Points descend by value; rays
+// keep the LDS stack (HStack) at constant levels. Only the boxes (per motion time) and the
+// leaves' DObj records are read from memory, at constant offsets.
+namespace csg {
+using rtx_csg::kNode;
+RTX_HD bool fold(bool a, int32_t pk, int32_t cidx, bool v) {  // hfold for one node's value
+    return pk == HN_UNION ? (a || v) : pk == HN_INTER ? (a && v) : (cidx == 0 ? v : (cidx == 1 ? (a && !v) : a));
+}
+RTX_HD bool decided(bool a, int32_t k, int32_t nc) {  // hdecided
+    if (k == HN_UNION) return RTX_ALL(a);
+    if (k == HN_INTER || (k == HN_DIFF && nc >= 1)) return RTX_ALL(!a);
+    return false;
+}
+
+// is_inside: the value of X's children (X inner, q in their frame), no box test
+// (is_inside's loop tests the box of the node it is called on only)
+template <int X>
+RTX_HD bool inside_body(const SceneView& S, f3 p, float time);
+template <int X, int C>
+RTX_HD bool inside_kids(const SceneView& S, f3 q, float time, bool acc) {
+    constexpr rtx_csg::CNode x = kNode[X];
+    if constexpr (C >= x.end) {
+        return acc;
+    } else {
+        constexpr rtx_csg::CNode c = kNode[C];
+        if constexpr (x.kind == HN_DIFF && c.cidx >= 2) {
+            return acc;
+        } else {
+            if (decided(acc, x.kind, c.cidx)) return acc;
+            bool v = false;
+            if constexpr (c.kind == HN_LEAF) v = leaf_inside(S.objs[c.obj], q, time);
+            else if constexpr (c.kind != HN_OTHER) v = inside_body<C>(S, q, time);
+            return inside_kids<X, c.end>(S, q, time, fold(acc, x.kind, c.cidx, v));
+        }
+    }
+}
+template <int X>
+RTX_HD bool inside_body(const SceneView& S, f3 p, float time) {
+    return inside_kids<X, X + 1>(S, xform(rtx_csg::kMinv[X], p, 1.0f), time, kNode[X].kind == HN_INTER);
+}
+// is_inside(X, p)
+template <int X>
+RTX_HD bool inside(const SceneView& S, f3 p, float time) {
+    if (!pt_in(S.ibox[X].lo, S.ibox[X].hi, p)) return false;
+    constexpr rtx_csg::CNode x = kNode[X];
+    if constexpr (x.kind == HN_LEAF) return leaf_inside(S.objs[x.obj], p, time);
+    else if constexpr (x.kind == HN_OTHER) return false;
+    else return inside_body<X>(S, p, time);
+}
+
+// get_material(X, p)
+template <int X, int J>
+RTX_HD int32_t material_kids(const SceneView& S, f3 q, float time);
+template <int X>
+RTX_HD int32_t material(const SceneView& S, f3 p, float time) {
+    constexpr rtx_csg::CNode x = kNode[X];
+    if constexpr (x.kind == HN_LEAF) {
+        cref<DObj> ob = S.objs[x.obj];
+        return ob.type == OBJ_PLANE ? plane_material(ob, p, time) : ob.mat0;
+    } else {
+        return material_kids<X, X + 1>(S, xform(rtx_csg::kMinv[X], p, 1.0f), time);
+    }
+}
+template <int X, int J>
+RTX_HD int32_t material_kids(const SceneView& S, f3 q, float time) {
+    if constexpr (J >= kNode[X].end) {
+        return -1;
+    } else {
+        if (inside<J>(S, q, time)) return material<J>(S, q, time);
+        return material_kids<X, kNode[J].end>(S, q, time);
+    }
+}
+
+// walk_up's filter at parent A of CUR: the siblings from J on must contain the hit (KEEP)
+// or not; a difference tests one
+template <int A, int CUR, int J, bool INTER, bool KEEP>
+RTX_HD bool walk_filter(const SceneView& S, float time, f3 pos) {
+    if constexpr (J >= kNode[A].end) {
+        return true;
+    } else if constexpr (J == CUR) {
+        return walk_filter<A, CUR, kNode[J].end, INTER, KEEP>(S, time, pos);
+    } else {
+        if (inside<J>(S, pos, time) != KEEP) return false;
+        if constexpr (!INTER) return true;
+        else return walk_filter<A, CUR, kNode[J].end, INTER, KEEP>(S, time, pos);
+    }
+}
+// walk_up(CUR -> STOP)
+template <int CUR, int STOP, bool SURF>
+RTX_HD bool walk(const SceneView& S, float time, f3& pos, f3& n, int32_t& mat) {
+    if constexpr (CUR == STOP) {
+        return true;
+    } else {
+        constexpr rtx_csg::CNode c = kNode[CUR];
+        constexpr int A = c.parent;
+        constexpr rtx_csg::CNode a = kNode[A];
+        if constexpr (a.kind == HN_INTER || a.kind == HN_DIFF) {
+            constexpr bool inter = a.kind == HN_INTER;
+            constexpr int c0 = A + 1;
+            constexpr int j0 = inter ? c0 : (c.cidx == 0 ? kNode[c0].end : c0);
+            if (!walk_filter<A, CUR, j0, inter, inter || c.cidx != 0>(S, time, pos)) return false;
+            if constexpr (SURF && !inter && c.cidx != 0) {
+                mat = material<c0>(S, pos, time);
+                n = neg(n);
+            }
+        }
+        if (SURF && mat < 0) mat = a.mat0 < 0 ? 0 : a.mat0;
+        pos = xform(rtx_csg::kM[A], pos, 1.0f);
+        if (SURF) n = normal_xform(rtx_csg::kMinv[A], n);
+        return walk<A, STOP, SURF>(S, time, pos, n, mat);
+    }
+}
+
+// hier_enum(ROOT): node I of ROOT's subtree in preorder
+template <int X, int C, int ROOT, bool MESH, bool SURF, class Want, class Take, class Cap>
+RTX_HD void enum_kids(const SceneView& S, const HStack& hs, float time, Want& want, Take& take, Cap& cap);
+template <int I, int ROOT, bool MESH, bool SURF, class Want, class Take, class Cap>
+RTX_HD void enum_node(const SceneView& S, const HStack& hs, float time, Want& want, Take& take, Cap& cap) {
+    constexpr rtx_csg::CNode c = kNode[I];
+    if constexpr (I != ROOT && c.pkind == HN_DIFF && c.cidx >= 2) {
+        return;  // difference reads children 0, 1
+    } else {
+        f3 ro, rd;
+        hs.get_ray(c.depth, ro, rd);
+        if constexpr (I != ROOT)  // (the caller tested the root's box)
+            if (!RTX_ANY(ray_meets(S.hbox[I].lo, S.hbox[I].hi, ro, rd, cap()))) return;
+        if constexpr (c.kind == HN_LEAF) {
+            auto emit = [&](double t, f3 pos, f3 n, int32_t mat) {
+                if (!want(t)) return;
+                if (walk<I, ROOT, SURF>(S, time, pos, n, mat)) take(t, pos, n, mat, c.obj);
+            };
+            leaf_hits<MESH, cref<DObj>, decltype(emit)&, SURF>(S, S.objs[c.obj], ro, rd, time, emit);
+        } else if constexpr (c.kind != HN_OTHER) {
+            hs.put_ray(c.depth + 1, xform(rtx_csg::kMinv[I], ro, 1.0f), xform(rtx_csg::kMinv[I], rd, 0.0f));
+            enum_kids<I, I + 1, ROOT, MESH, SURF>(S, hs, time, want, take, cap);
+        }
+    }
+}
+template <int X, int C, int ROOT, bool MESH, bool SURF, class Want, class Take, class Cap>
+RTX_HD void enum_kids(const SceneView& S, const HStack& hs, float time, Want& want, Take& take, Cap& cap) {
+    if constexpr (C < kNode[X].end) {
+        enum_node<C, ROOT, MESH, SURF>(S, hs, time, want, take, cap);
+        enum_kids<X, kNode[C].end, ROOT, MESH, SURF>(S, hs, time, want, take, cap);
+    }
+}
+template <int ROOT, bool MESH, bool SURF, class Want, class Take, class Cap>
+RTX_HD void enum_root(const SceneView& S, const HStack& hs, float time, Want& want, Take& take, Cap& cap) {
+    {
+        f3 ro, rd;
+        hs.get_ray(kNode[ROOT].depth, ro, rd);
+        if (!RTX_ANY(ray_meets(S.hbox[ROOT].lo, S.hbox[ROOT].hi, ro, rd, cap()))) return;
+    }
+    enum_node<ROOT, ROOT, MESH, SURF>(S, hs, time, want, take, cap);
+}
+
+// diff_shadow(X)
+template <int X, bool MESH>
+RTX_HD bool diff_shadow(const SceneView& S, const HStack& hs, float time) {
+    constexpr rtx_csg::CNode x = kNode[X];
+    {
+        f3 ro, rd;
+        hs.get_ray(x.depth, ro, rd);
+        hs.put_ray(x.depth + 1, xform(rtx_csg::kMinv[X], ro, 1.0f), xform(rtx_csg::kMinv[X], rd, 0.0f));
+    }
+    constexpr int c0 = X + 1, c1 = kNode[c0].end;
+    static_assert(c1 < x.end, "a difference has two children (rtx_api.hip jit_csg_tables)");
+    bool found = false;
+    auto want = [&](double t) { return !found && t > 1e-4; };
+    auto cap = [&]() { return found ? -1.0f : INFINITY; };
+    {
+        auto take = [&](double, f3 pos, f3, int32_t, int32_t) { found = inside<c1>(S, pos, time) == false; };
+        enum_root<c0, MESH, false>(S, hs, time, want, take, cap);
+    }
+    {
+        auto take = [&](double, f3 pos, f3, int32_t, int32_t) { found = inside<c0>(S, pos, time) == true; };
+        enum_root<c1, MESH, false>(S, hs, time, want, take, cap);
+    }
+    return found;
+}
+
+// hier_shadow: the children of the open node X (value acc so far)
+template <int X, int C, bool MESH>
+RTX_HD bool shadow_kids(const SceneView& S, const HStack& hs, double t_max, float time, bool acc) {
+    constexpr rtx_csg::CNode x = kNode[X];
+    if constexpr (C >= x.end) {
+        return acc;
+    } else {
+        constexpr rtx_csg::CNode c = kNode[C];
+        if (decided(acc, x.kind, c.cidx)) return acc;
+        bool live;
+        {
+            f3 ro, rd;
+            hs.get_ray(c.depth, ro, rd);
+            live = ray_meets(S.sbox[C].lo, S.sbox[C].hi, ro, rd, INFINITY);
+        }
+        bool v = false;
+        if (RTX_ANY(live)) {
+            if constexpr (c.kind == HN_LEAF) {
+                f3 lo, ld;
+                hs.get_ray(c.depth, lo, ld);
+                v = live && leaf_shadow<MESH>(S, S.objs[c.obj], lo, ld, t_max, time);
+            } else if constexpr (c.kind == HN_DIFF) {
+                if (live) v = diff_shadow<C, MESH>(S, hs, time);
+            } else if constexpr (c.kind != HN_OTHER) {
+                f3 ro, rd;
+                hs.get_ray(c.depth, ro, rd);
+                hs.put_ray(c.depth + 1, xform(rtx_csg::kMinv[C], ro, 1.0f), xform(rtx_csg::kMinv[C], rd, 0.0f));
+                v = shadow_kids<C, C + 1, MESH>(S, hs, t_max, time, c.kind == HN_INTER);
+            }
+        }
+        return shadow_kids<X, c.end, MESH>(S, hs, t_max, time, fold(acc, x.kind, c.cidx, v));
+    }
+}
+// hier_shadow(R)
+template <int R, bool MESH>
+RTX_HD bool shadow_root(const SceneView& S, const HStack& hs, f3 o, f3 d, double t_max, float time) {
+    hs.put_ray(0, o, d);
+    if (!RTX_ANY(ray_meets(S.sbox[R].lo, S.sbox[R].hi, o, d, INFINITY))) return false;
+    constexpr rtx_csg::CNode r = kNode[R];
+    if constexpr (r.kind == HN_OTHER) {
+        return false;
+    } else if constexpr (r.kind == HN_DIFF) {
+        return diff_shadow<R, MESH>(S, hs, time);
+    } else {
+        hs.put_ray(1, xform(rtx_csg::kMinv[R], o, 1.0f), xform(rtx_csg::kMinv[R], d, 0.0f));
+        return shadow_kids<R, R + 1, MESH>(S, hs, t_max, time, r.kind == HN_INTER);
+    }
+}
+// hier_occluded: roots R, R' = end(R), ... (Q: R's ordinal)
+template <bool MESH, int R, int Q>
+RTX_HD bool occluded_roots(const SceneView& S, const HStack& hs, f3 o, f3 d, double t_max, float time, bool occ,
+                           uint32_t rmask) {
+    if constexpr (R >= rtx_csg::kCount) {
+        return occ;
+    } else {
+        if (RTX_ALL(occ)) return occ;
+        const bool live = !occ && (Q >= 32 || ((rmask >> Q) & 1u) != 0u);
+        if (RTX_ANY(live)) {
+            if (live) occ = shadow_root<R, MESH>(S, hs, o, d, t_max, time);
+        }
+        return occluded_roots<MESH, kNode[R].end, Q + 1>(S, hs, o, d, t_max, time, occ, rmask);
+    }
+}
+// hier_closest: roots R, R' = end(R), ... (Q: R's ordinal)
+template <bool MESH, int R, int Q>
+RTX_HD void closest_roots(const SceneView& S, const HStack& hs, f3 o, f3 d, float time, Hit& h, HHit& hh,
+                          uint32_t rmask) {
+    if constexpr (R < rtx_csg::kCount) {
+        if (!(Q < 32 && !((rmask >> Q) & 1u))) {  // (else the tile's rays miss its hit box)
+            constexpr int32_t oid = kNode[R].oid;
+            auto want = [&](double t) {
+                const float t32 = (float)t;
+                if (t32 < h.t32) return true;
+                if (!(t32 == h.t32)) return false;
+                if (h.obj == -1) return t < INFINITY;
+                double bt;
+                int32_t bo;
+                if (h.obj == kHierHit) { bt = hh.t64; bo = h.sub; }
+                else { bt = hit_t64(S, h.obj, h.sub, o, d, time); bo = S.objs[h.obj].oid; }
+                return t < bt || (t == bt && oid < bo);
+            };
+            auto take = [&](double t, f3 pos, f3 n, int32_t mat, int32_t leaf) {
+                const int32_t ty = S.objs[leaf].type;
+                h.t32 = (float)t;
+                h.obj = kHierHit;
+                h.sub = oid;
+                hh = HHit{t, pos, n, mat, (ty == OBJ_PLANE || ty == OBJ_BOX) ? leaf : -1};
+            };
+            auto cap = [&]() { return h.t32; };
+            enum_root<R, MESH, true>(S, hs, time, want, take, cap);
+        }
+        closest_roots<MESH, kNode[R].end, Q + 1>(S, hs, o, d, time, h, hh, rmask);
+    }
+}
+}  // namespace csg
+#endif
+
 // Hierarchy.shadow_intersect of root r for the world ray (o, d): union = any child,
 // intersection = every child (each tested on its own), difference = diff_shadow.
 #if RTX_HIER_INLINE >= 1
@@ -1585,6 +1876,9 @@ RTX_HY bool hier_shadow(const SceneView& S, const HStack& hs, int r, f3 o, f3 d,
 template <bool MESH>
 RTX_HD bool hier_occluded(const SceneView& S, const HStack& hs, f3 o, f3 d, double t_max, float time, bool occ,
                           uint32_t rmask = ~0u) {
+#if defined(RTX_CSG_STATIC)
+    return csg::occluded_roots<MESH, 0, 0>(S, hs, o, d, t_max, time, occ, rmask);
+#endif
     int q = 0;
     for (int r = 0; r < S.n_nodes; r = S.nodes[r].end, ++q) {
         if (RTX_ALL(occ)) break;
@@ -1594,14 +1888,6 @@ RTX_HD bool hier_occluded(const SceneView& S, const HStack& hs, f3 o, f3 d, doub
     }
     return occ;
 }
-
-// Best hierarchy hit: the surface the walk-up produced (world frame).
-constexpr int32_t kHierHit = -2;  // Hit.obj of a hierarchy hit; Hit.sub then holds the root's oid
-struct HHit {
-    double t64;
-    f3 pos, n;
-    int32_t mat, gobj;  // gobj: the leaf DObj (Plane/AABB get_diffuse), -1 otherwise
-};
 
 // Closest hit over the hierarchies, merged into h (flat objects done): a candidate wins
 // with a smaller t, or an equal t and an earlier top-level object (scene.py:94).
@@ -1613,6 +1899,10 @@ template <bool MESH>
 RTX_HY void hier_closest(const SceneView& S, const HStack& hs, f3 o, f3 d, float time, Hit& h, HHit& hh,
                          uint32_t rmask = ~0u) {
     hs.put_ray(0, o, d);
+#if defined(RTX_CSG_STATIC)
+    csg::closest_roots<MESH, 0, 0>(S, hs, o, d, time, h, hh, rmask);
+    return;
+#endif
     // The root whose hit box the wave's first ray enters first goes first: its hit then
     // caps the others' culling. Candidates compare by (t, top-level position), so the
     // order of the roots does not change the result (the order inside a root does, on

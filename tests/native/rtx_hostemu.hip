@@ -550,6 +550,28 @@ extern "C" int64_t rtx_hostemu_jit_spec(const rtx_scene_desc* sd, const rtx_came
     return (int64_t)s.size();
 }
 
+// The specialized split pass (rtx_api.hip jit_split_spec: pass 0 trace, 1 shadow) librtx.so
+// would build for this scene on gfx950, as rtx_hostemu_jit_spec's text; -1: the scene's
+// trees do not qualify (jit_csg_tables). *cost: csg_cost of its trees (-1 without any).
+extern "C" int64_t rtx_hostemu_jit_split(const rtx_scene_desc* sd, int32_t pass, int32_t cnt, int32_t jit, char* out,
+                                         int64_t cap, int64_t* cost) {
+    HostScene H;
+    if (convert_scene(sd, H)) return -2;
+    if (cost) *cost = H.nodes.empty() ? -1 : csg_cost(H.nodes);
+    const std::string tables = jit_csg_tables(H.nodes);
+    if (tables.empty()) return -1;
+    const JitSpec sp = jit_split_spec("gfx950", tables, H.has_mesh, H.has_secondary, cnt != 0, jit != 0, pass);
+    std::string s = sp.name + "\n";
+    for (const auto& o : sp.opts) s += o + "\n";
+    s += "\n" + sp.src;
+    if (out && cap > 0) {
+        const size_t n = std::min((size_t)cap - 1, s.size());
+        memcpy(out, s.data(), n);
+        out[n] = '\0';
+    }
+    return (int64_t)s.size();
+}
+
 // The split hierarchy passes (rtx_split.h trace_sample / shadow_mask / shade_sample) on
 // the host, chunked like rtx_api.hip render_split (split_plan with `budget` bytes and
 // `ratio` deeper records per sample), over image rows [row0, row0 + nrows). Deeper records

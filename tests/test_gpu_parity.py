@@ -489,9 +489,10 @@ def test_codegen_options_render_the_default_bytes(name, opt, value, monkeypatch)
 
 def test_default_flat_scenes_run_the_specialized_kernel():
     """The production path for flat scenes is the scene-specialized kernel (bench.py reports
-    its name); hierarchy/texture scenes run the split passes (csrc/rtx_split.h)."""
+    its name); hierarchy/texture scenes run the split passes (csrc/rtx_split.h) specialized
+    on their CSG trees (option jit_csg)."""
     for name, prefix in (("TwoSpheresPlane", "rtx_jit_render_00000"), ("TorusMesh", "rtx_jit_render_10000"),
-                         ("MirrorRefraction", "rtx_jit_render_01000"), ("NovelScene1", "k_split_")):
+                         ("MirrorRefraction", "rtx_jit_render_01000"), ("NovelScene1", "rtx_jit_split_")):
         sc = product_scene(name, (64, 32))
         sc.render_device()
         assert sc.last_kernel.startswith(prefix), (name, sc.last_kernel)

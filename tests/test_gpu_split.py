@@ -1,7 +1,9 @@
 """The hierarchy/texture scenes rendered by the three split passes on the MI355X
 (csrc/rtx_split.h, RTX_SPLIT=1): chains of closest hits -> shade-point records, shadow
 rays per record -> occlusion masks, lighting + unwinding + the ordered mean. Bit-identical
-to the oracle (with its ray tallies) and to the one-kernel form."""
+to the oracle (with its ray tallies) and to the one-kernel form. The trace and shadow passes
+run specialized on the scene's CSG trees (option jit_csg, rtx_trace.h namespace csg) where
+the scene qualifies, the precompiled passes otherwise: both are the split path."""
 import numpy as np
 import pytest
 import torch
@@ -19,6 +21,9 @@ CASES = [
 ]
 
 
+SPLIT = ("k_split_", "rtx_jit_split_")  # the split passes: precompiled, or specialized on the trees
+
+
 @pytest.fixture
 def split(monkeypatch):
     monkeypatch.setattr(OPTS, "split", "1")
@@ -28,7 +33,7 @@ def split(monkeypatch):
 def test_split_matches_oracle(name, res, edits, split):
     sc = product_scene(name, res, **edits)
     img = sc.render()
-    assert sc.last_kernel.startswith("k_split_"), sc.last_kernel
+    assert sc.last_kernel.startswith(SPLIT), sc.last_kernel
     assert_parity(img, oracle_render(name, res, **edits), name)
 
 
@@ -38,7 +43,7 @@ def test_split_random_hierarchy_scenes(seed, split):
     d = random_hier_scene(seed, res=(64, 48), mesh=(seed % 4 == 0))
     sc = product_scene_dict(d)
     assert_parity(sc.render(), oracle_render_dict(d), "hier seed %d" % seed)
-    assert sc.last_kernel.startswith("k_split_"), sc.last_kernel
+    assert sc.last_kernel.startswith(SPLIT), sc.last_kernel
 
 
 def test_split_tallies_match_oracle(split):
@@ -83,7 +88,7 @@ def test_split_equals_one_kernel_full_novel_scene1(monkeypatch):
     monkeypatch.setattr(OPTS, "split", "1")
     sc.render_device(out=b)
     torch.cuda.synchronize()
-    assert one.startswith("k_render_ext") and sc.last_kernel.startswith("k_split_"), (one, sc.last_kernel)
+    assert one.startswith("k_render_ext") and sc.last_kernel.startswith(SPLIT), (one, sc.last_kernel)
     assert torch.equal(a, b), float((a != b).float().mean())
 
 
@@ -97,7 +102,7 @@ def test_split_many_roots_bins_and_grids(seed, split, monkeypatch):
     d = many_roots_scene(seed, res=(96, 64))
     sc = product_scene_dict(d)
     a = sc.render_device().clone()
-    assert sc.last_kernel.startswith("k_split_"), sc.last_kernel
+    assert sc.last_kernel.startswith(SPLIT), sc.last_kernel
     monkeypatch.setattr(OPTS, "bins", "0")
     monkeypatch.setattr(OPTS, "dsgrid", "0")
     b = product_scene_dict(d).render_device().clone()
@@ -122,7 +127,7 @@ def test_split_pool_overflow_redo(ratio, budget, split, monkeypatch):
                           for i, m in enumerate(d["materials"])]
         sc = product_scene_dict(d)
         img = sc.render()
-        assert sc.last_kernel.startswith("k_split_"), sc.last_kernel
+        assert sc.last_kernel.startswith(SPLIT), sc.last_kernel
         assert_parity(img, oracle_render_dict(d), "pool overflow %s seed %d" % (ratio, seed))
 
 
@@ -182,3 +187,32 @@ def test_split_capture_needs_a_first_render(split):
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("case", ["ns1", "ns1_full", "ns2", "random", "many_roots"])
+def test_split_csg_specialized_equals_precompiled(case, split, monkeypatch):
+    """The trace and shadow passes specialized on the scene's CSG trees (node fields and
+    matrices as literals, the traversals unrolled: rtx_api.hip jit_csg_tables) give the
+    precompiled passes' bytes: NovelScene1/2 (NovelScene1 also at its full 2048x1024 AA32
+    Philox config), random hierarchy scenes with and without a mesh, 40 roots."""
+    from scenegen import many_roots_scene, random_hier_scene
+    if case == "random":
+        ds = [random_hier_scene(seed, res=(64, 48), mesh=(seed % 2 == 0)) for seed in (1, 2, 9, 12)]
+        make = [lambda d=d: product_scene_dict(d) for d in ds]
+    elif case == "many_roots":
+        make = [lambda: product_scene_dict(many_roots_scene(1, res=(96, 64)))]
+    elif case == "ns1_full":
+        make = [lambda: product_scene("NovelScene1")]
+    else:
+        name = "NovelScene1" if case == "ns1" else "NovelScene2"
+        make = [lambda: product_scene(name, (128, 64), AA={"jitter": True, "samples": 4})]
+    for mk in make:
+        frames, kernels = [], []
+        for on in ("1", "0"):
+            monkeypatch.setattr(OPTS, "jit_csg", on)
+            sc = mk()
+            frames.append(sc.render_device().clone())
+            kernels.append(sc.last_kernel)
+        torch.cuda.synchronize()
+        assert kernels[0].startswith("rtx_jit_split_") and kernels[1].startswith("k_split_"), kernels
+        assert torch.equal(frames[0], frames[1]), float((frames[0] != frames[1]).float().mean())

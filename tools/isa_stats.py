@@ -5,7 +5,7 @@ from collections import Counter
 
 s = open(sys.argv[1]).read()
 pat = sys.argv[2] if len(sys.argv) > 2 else "k_render"
-for m in re.finditer(r"^(_Z\w+):\s*(?:;.*)?$", s, re.M):
+for m in re.finditer(r"^(_Z\w+|rtx_jit\w+):\s*(?:;.*)?$", s, re.M):
     name = m.group(1)
     if pat not in name:
         continue

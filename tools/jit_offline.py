@@ -5,6 +5,8 @@ rtx_api.hip's jit_spec (tests/native/librtx_hostemu.so) for a bench.py config.
 
 usage: python tools/jit_offline.py LOG KERNEL OUT.s [extra hipcc flags...]
        python tools/jit_offline.py --config tsp1080 [--rgb8] OUT.s [extra hipcc flags...]
+       python tools/jit_offline.py --split ns1 PASS OUT.s [...]  (a hierarchy config's specialized
+           split pass: 0 trace, 1 shadow; rtx_api.hip jit_split_spec)
 Environment variables that change the specialization (RTX_JIT_FLAGS, RTX_BINS, ...)
 apply in the --config form as they would on the box."""
 import ctypes as C
@@ -57,9 +59,36 @@ def from_config(cfg, rgb8):
     return opts, src
 
 
+def from_split(cfg, pas):
+    sys.path[:0] = [repo, os.path.join(repo, "python-raytracer_amd"), os.path.join(repo, "tests")]
+    import bench
+    import hostemu
+    sc = bench.make_scene(cfg)
+    sd = sc.scene_desc()
+    cd, _tables = sc.camera_desc()
+    f = hostemu.lib().rtx_hostemu_jit_split
+    f.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_char_p, C.c_int64, C.POINTER(C.c_int64)]
+    f.restype = C.c_int64
+    cost = C.c_int64()
+    jit = 1 if cd.jitter else 0
+    n = f(C.addressof(sd), pas, 0, jit, None, 0, C.byref(cost))
+    print("csg_cost", cost.value)
+    if n < 0:
+        sys.exit("config %s runs the precompiled split passes (%d)" % (cfg, n))
+    buf = C.create_string_buffer(int(n) + 1)
+    f(C.addressof(sd), pas, 0, jit, buf, n + 1, C.byref(cost))
+    head, src = buf.value.decode().split("\n\n", 1)
+    name, *opts = head.split("\n")
+    print("kernel", name)
+    return opts, src
+
+
 def main():
     a = sys.argv[1:]
-    if a[0] == "--config":
+    if a[0] == "--split":
+        opts, src = from_split(a[1], int(a[2]))
+        out, extra = a[3], a[4:]
+    elif a[0] == "--config":
         cfg = a[1]
         rgb8 = len(a) > 2 and a[2] == "--rgb8"
         a = a[3 if rgb8 else 2:]

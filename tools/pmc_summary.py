@@ -19,7 +19,7 @@ import sys
 
 d, cfg = sys.argv[1], sys.argv[2]
 frames = int(sys.argv[3]) if len(sys.argv) > 3 else 5  # tools/prof_driver.py --iters in pmc_session.sh
-RENDER = ("k_render", "rtx_jit_render", "k_split_", "k_mesh_chunks")
+RENDER = ("k_render", "rtx_jit_render", "k_split_", "rtx_jit_split_", "k_mesh_chunks")
 per = {}  # kernel -> counter -> [values per dispatch]
 for f in sorted(glob.glob(os.path.join(d, "p*", "*counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
