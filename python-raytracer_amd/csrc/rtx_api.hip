@@ -111,7 +111,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"dev_bins", 1, false},                   // a mesh's primary-ray face bins built on the device
     {"chunk_mode", 3, false},                 // heavy-tile pass: bit 0 LDS-staged faces, bit 1 XCD-aware order
     {"bin_lds", 0, false},                    // primary-ray face lists staged in LDS (specialized mesh kernels)
-    {"jit_csg", 1, false},                    // split hierarchy passes specialized on the scene's CSG trees
+    {"jit_csg", 1, false},                    // split hierarchy passes specialized on the CSG trees (2: + boxes, 3: + objects)
     {"setup_log", 0, false},                  // print the host time of each rtx_camera_set step
 };
 struct OptVal {
@@ -1761,6 +1761,7 @@ const char* const kLibMacros[] = {
 #endif
     "-DRTX_HIER_INLINE=" RTX_STR(RTX_HIER_INLINE),
     "-DRTX_HEAVY_CHUNK=" RTX_STR(RTX_HEAVY_CHUNK),
+    "-DRTX_CSG_RAYREG=" RTX_STR(RTX_CSG_RAYREG),  // (the host sizes the split passes' LDS from it)
 #ifdef RTX_PAD
     "-DRTX_PAD=" RTX_STR(RTX_PAD),
 #endif
@@ -2044,6 +2045,17 @@ std::string jit_csg_tables(const std::vector<DNode>& N) {
     return s + "};\n}  // namespace rtx_csg\n#define RTX_CSG_STATIC 1\n";
 }
 
+// The camera's node boxes (option jit_csg 2) and the scene's object records (3) for the
+// specialized split passes (rtx_trace.h csg::hbox / obj, RTX_CSG_BAKED 2 / 3): the bytes
+// the camera and scene uploads hold. Measured slower: with both, NovelScene1 11.4 -> 48.7 ms
+// (the literals' live ranges spill 429 VGPRs, profiles/r06/s14/).
+std::string jit_csg_baked(const std::vector<DBound>& bounds, const std::vector<DObj>& objs, int level) {
+    std::string s = "namespace rtx_csg {\n";
+    baked_array(s, "kBoxes", split_bounds(bounds));
+    if (level >= 3) baked_array(s, "kObjs", objs);
+    return s + "}  // namespace rtx_csg\n#define RTX_CSG_BAKED " + std::to_string(level) + "\n";
+}
+
 // The split pass kernel specialized on a node table (rtx_split.h split_trace / split_shadow,
 // with the static traversals): the library's own kernel build otherwise.
 JitSpec jit_split_spec(const std::string& arch, const std::string& tables, bool mesh, bool sec, bool cnt, bool jit,
@@ -2051,6 +2063,13 @@ JitSpec jit_split_spec(const std::string& arch, const std::string& tables, bool 
     JitSpec sp;
     sp.opts = {"--offload-arch=" + arch, "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize"};
     for (const char* m : kLibMacros) sp.opts.push_back(m);
+    // the shadow pass with its rays in registers: at most 128 VGPRs (4 waves/SIMD), which its
+    // precompiled form's LDS stack had imposed (1 wave bound: 129 VGPRs, NovelScene1 13.35 ms
+    // against 11.36 bounded, profiles/r06/s13/)
+    if (pass == 1 && RTX_CSG_RAYREG) {
+        sp.opts.push_back("-URTX_LB_SPLIT_B");
+        sp.opts.push_back("-DRTX_LB_SPLIT_B=4");
+    }
     {
         std::istringstream is(opt_str(OPT_JIT_FLAGS));
         for (std::string o; is >> o;) sp.opts.push_back(o);
@@ -3315,7 +3334,12 @@ int render_split(rtx_scene* s, Launch L, const KParams* kp, size_t hbytes, hipSt
         JitSlot& r = s->resolved[16 + 4 * pass + (cnt ? 2 : 0) + ((sel & 1) ? 1 : 0)];
         if (!r.done) {
             r.block = B;
-            jit_split_kernel(s->device, s->csg_tables, s->has_mesh, s->has_secondary, cnt, (sel & 1) != 0, pass, r);
+            // option jit_csg 2 / 3: the camera's boxes / and the object records as literals too
+            const int bake = opt(OPT_JIT_CSG) >= 3.0 ? 3 : opt(OPT_JIT_CSG) >= 2.0 ? 2 : 0;
+            const bool can = !s->csg_tables.empty() && s->tr_valid && s->tr_bounds.size() == s->h_nodes.size();
+            jit_split_kernel(s->device,
+                             bake && can ? s->csg_tables + jit_csg_baked(s->tr_bounds, s->h_objs, bake) : s->csg_tables,
+                             s->has_mesh, s->has_secondary, cnt, (sel & 1) != 0, pass, r);
             if (r.pending && !opt_on(OPT_JIT_ASYNC) && !capturing) jit_poll(r, true);
             r.done = true;
         } else if (r.pending && !capturing) {
@@ -3333,8 +3357,9 @@ int render_split(rtx_scene* s, Launch L, const KParams* kp, size_t hbytes, hipSt
             Launch La = Lc;
             SplitBuf sbb = sb;
             void* args[] = {(void*)&kpp, (void*)&La, (void*)&sbb};
-            return hipModuleLaunchKernel(sk[pass]->fn, r.nblocks, 1, 1, B, 1, 1, (unsigned)r.lds_bytes, r.stream, args,
-                                         nullptr);
+            // (rays in registers: the specialized passes use no LDS stack, RTX_CSG_RAYREG)
+            const unsigned lds = RTX_CSG_RAYREG ? 0u : (unsigned)r.lds_bytes;
+            return hipModuleLaunchKernel(sk[pass]->fn, r.nblocks, 1, 1, B, 1, 1, lds, r.stream, args, nullptr);
         }
         return s->has_mesh ? launch_split_m1(sel, pass, r, Lc, sb) : launch_split_m0(sel, pass, r, Lc, sb);
     };

@@ -1502,16 +1502,40 @@ struct HHit {
     int32_t mat, gobj;  // gobj: the leaf DObj (Plane/AABB get_diffuse), -1 otherwise
 };
 
+// (library build knob of the CSG-specialized split passes, below; the host sizes their LDS
+// from it)
+#ifndef RTX_CSG_RAYREG
+#define RTX_CSG_RAYREG 1
+#endif
 #if defined(RTX_CSG_STATIC)
 // ---- Hierarchies with their shape as compile-time constants (the scene-specialized split
 // passes, rtx_api.hip jit_csg_tables): the traversals above -- the same tests in the same
 // order, the same wave votes, the same arithmetic -- unrolled over the scene's node table
 // (rtx_csg::kNode, kM, kMinv in the kernel's source), so node fields and matrices are
-// literals and no traversal step waits on a node record. Points descend by value; rays
-// keep the LDS stack (HStack) at constant levels. Only the boxes (per motion time) and the
-// leaves' DObj records are read from memory, at constant offsets.
+// literals and no traversal step waits on a node record. Points and rays descend by value
+// (RTX_CSG_RAYREG 0: rays through the LDS stack at constant levels, as the loop form). Only
+// the boxes (per motion time) and the leaves' DObj records are read from memory, at
+// constant offsets.
 namespace csg {
 using rtx_csg::kNode;
+// The boxes of node I (hit, inside, shadow) and the leaves' object records: the uploaded
+// arrays, or (RTX_CSG_BAKED 2: the boxes, 3: also the records; option jit_csg) the camera's
+// values baked into the source with the tables -- the same bytes, reads at constant offsets
+// folding to literals. (Measured slower: rtx_api.hip jit_csg_baked.)
+#if defined(RTX_CSG_BAKED)
+template <int I> RTX_HD cref<DBox> hbox(const SceneView&) { return ((cptr<DBox>)rtx_csg::kBoxes)[I]; }
+template <int I> RTX_HD cref<DBox> ibox(const SceneView&) { return ((cptr<DBox>)rtx_csg::kBoxes)[rtx_csg::kCount + I]; }
+template <int I> RTX_HD cref<DBox> sbox(const SceneView&) { return ((cptr<DBox>)rtx_csg::kBoxes)[2 * rtx_csg::kCount + I]; }
+#else
+template <int I> RTX_HD cref<DBox> hbox(const SceneView& S) { return S.hbox[I]; }
+template <int I> RTX_HD cref<DBox> ibox(const SceneView& S) { return S.ibox[I]; }
+template <int I> RTX_HD cref<DBox> sbox(const SceneView& S) { return S.sbox[I]; }
+#endif
+#if defined(RTX_CSG_BAKED) && RTX_CSG_BAKED >= 3
+template <int O> RTX_HD cref<DObj> obj(const SceneView&) { return ((cptr<DObj>)rtx_csg::kObjs)[O]; }
+#else
+template <int O> RTX_HD cref<DObj> obj(const SceneView& S) { return S.objs[O]; }
+#endif
 RTX_HD bool fold(bool a, int32_t pk, int32_t cidx, bool v) {  // hfold for one node's value
     return pk == HN_UNION ? (a || v) : pk == HN_INTER ? (a && v) : (cidx == 0 ? v : (cidx == 1 ? (a && !v) : a));
 }
@@ -1537,7 +1561,7 @@ RTX_HD bool inside_kids(const SceneView& S, f3 q, float time, bool acc) {
         } else {
             if (decided(acc, x.kind, c.cidx)) return acc;
             bool v = false;
-            if constexpr (c.kind == HN_LEAF) v = leaf_inside(S.objs[c.obj], q, time);
+            if constexpr (c.kind == HN_LEAF) v = leaf_inside(obj<c.obj>(S), q, time);
             else if constexpr (c.kind != HN_OTHER) v = inside_body<C>(S, q, time);
             return inside_kids<X, c.end>(S, q, time, fold(acc, x.kind, c.cidx, v));
         }
@@ -1550,9 +1574,9 @@ RTX_HD bool inside_body(const SceneView& S, f3 p, float time) {
 // is_inside(X, p)
 template <int X>
 RTX_HD bool inside(const SceneView& S, f3 p, float time) {
-    if (!pt_in(S.ibox[X].lo, S.ibox[X].hi, p)) return false;
+    if (!pt_in(ibox<X>(S).lo, ibox<X>(S).hi, p)) return false;
     constexpr rtx_csg::CNode x = kNode[X];
-    if constexpr (x.kind == HN_LEAF) return leaf_inside(S.objs[x.obj], p, time);
+    if constexpr (x.kind == HN_LEAF) return leaf_inside(obj<x.obj>(S), p, time);
     else if constexpr (x.kind == HN_OTHER) return false;
     else return inside_body<X>(S, p, time);
 }
@@ -1564,7 +1588,7 @@ template <int X>
 RTX_HD int32_t material(const SceneView& S, f3 p, float time) {
     constexpr rtx_csg::CNode x = kNode[X];
     if constexpr (x.kind == HN_LEAF) {
-        cref<DObj> ob = S.objs[x.obj];
+        cref<DObj> ob = obj<x.obj>(S);
         return ob.type == OBJ_PLANE ? plane_material(ob, p, time) : ob.mat0;
     } else {
         return material_kids<X, X + 1>(S, xform(rtx_csg::kMinv[X], p, 1.0f), time);
@@ -1620,57 +1644,71 @@ RTX_HD bool walk(const SceneView& S, float time, f3& pos, f3& n, int32_t& mat) {
     }
 }
 
-// hier_enum(ROOT): node I of ROOT's subtree in preorder
+// Rays descend by value (RTX_CSG_RAYREG 1: registers) or, as the loop form, through the
+// LDS stack at constant levels (0): at_depth / to_depth are the two forms' reads and writes.
+template <int DEPTH>
+RTX_HD void at_depth(const HStack& hs, f3& ro, f3& rd) {
+#if !RTX_CSG_RAYREG
+    hs.get_ray(DEPTH, ro, rd);
+#else
+    (void)hs, (void)ro, (void)rd;
+#endif
+}
+template <int DEPTH>
+RTX_HD void to_depth(const HStack& hs, f3 ro, f3 rd) {
+#if !RTX_CSG_RAYREG
+    hs.put_ray(DEPTH, ro, rd);
+#else
+    (void)hs, (void)ro, (void)rd;
+#endif
+}
+
+// hier_enum(ROOT): node I of ROOT's subtree in preorder, (ro, rd) the ray of its depth
 template <int X, int C, int ROOT, bool MESH, bool SURF, class Want, class Take, class Cap>
-RTX_HD void enum_kids(const SceneView& S, const HStack& hs, float time, Want& want, Take& take, Cap& cap);
+RTX_HD void enum_kids(const SceneView& S, const HStack& hs, f3 ro, f3 rd, float time, Want& want, Take& take, Cap& cap);
 template <int I, int ROOT, bool MESH, bool SURF, class Want, class Take, class Cap>
-RTX_HD void enum_node(const SceneView& S, const HStack& hs, float time, Want& want, Take& take, Cap& cap) {
+RTX_HD void enum_node(const SceneView& S, const HStack& hs, f3 ro, f3 rd, float time, Want& want, Take& take, Cap& cap) {
     constexpr rtx_csg::CNode c = kNode[I];
     if constexpr (I != ROOT && c.pkind == HN_DIFF && c.cidx >= 2) {
         return;  // difference reads children 0, 1
     } else {
-        f3 ro, rd;
-        hs.get_ray(c.depth, ro, rd);
+        at_depth<c.depth>(hs, ro, rd);
         if constexpr (I != ROOT)  // (the caller tested the root's box)
-            if (!RTX_ANY(ray_meets(S.hbox[I].lo, S.hbox[I].hi, ro, rd, cap()))) return;
+            if (!RTX_ANY(ray_meets(hbox<I>(S).lo, hbox<I>(S).hi, ro, rd, cap()))) return;
         if constexpr (c.kind == HN_LEAF) {
             auto emit = [&](double t, f3 pos, f3 n, int32_t mat) {
                 if (!want(t)) return;
                 if (walk<I, ROOT, SURF>(S, time, pos, n, mat)) take(t, pos, n, mat, c.obj);
             };
-            leaf_hits<MESH, cref<DObj>, decltype(emit)&, SURF>(S, S.objs[c.obj], ro, rd, time, emit);
+            leaf_hits<MESH, cref<DObj>, decltype(emit)&, SURF>(S, obj<c.obj>(S), ro, rd, time, emit);
         } else if constexpr (c.kind != HN_OTHER) {
-            hs.put_ray(c.depth + 1, xform(rtx_csg::kMinv[I], ro, 1.0f), xform(rtx_csg::kMinv[I], rd, 0.0f));
-            enum_kids<I, I + 1, ROOT, MESH, SURF>(S, hs, time, want, take, cap);
+            const f3 co = xform(rtx_csg::kMinv[I], ro, 1.0f), cd = xform(rtx_csg::kMinv[I], rd, 0.0f);
+            to_depth<c.depth + 1>(hs, co, cd);
+            enum_kids<I, I + 1, ROOT, MESH, SURF>(S, hs, co, cd, time, want, take, cap);
         }
     }
 }
 template <int X, int C, int ROOT, bool MESH, bool SURF, class Want, class Take, class Cap>
-RTX_HD void enum_kids(const SceneView& S, const HStack& hs, float time, Want& want, Take& take, Cap& cap) {
+RTX_HD void enum_kids(const SceneView& S, const HStack& hs, f3 ro, f3 rd, float time, Want& want, Take& take, Cap& cap) {
     if constexpr (C < kNode[X].end) {
-        enum_node<C, ROOT, MESH, SURF>(S, hs, time, want, take, cap);
-        enum_kids<X, kNode[C].end, ROOT, MESH, SURF>(S, hs, time, want, take, cap);
+        enum_node<C, ROOT, MESH, SURF>(S, hs, ro, rd, time, want, take, cap);
+        enum_kids<X, kNode[C].end, ROOT, MESH, SURF>(S, hs, ro, rd, time, want, take, cap);
     }
 }
 template <int ROOT, bool MESH, bool SURF, class Want, class Take, class Cap>
-RTX_HD void enum_root(const SceneView& S, const HStack& hs, float time, Want& want, Take& take, Cap& cap) {
-    {
-        f3 ro, rd;
-        hs.get_ray(kNode[ROOT].depth, ro, rd);
-        if (!RTX_ANY(ray_meets(S.hbox[ROOT].lo, S.hbox[ROOT].hi, ro, rd, cap()))) return;
-    }
-    enum_node<ROOT, ROOT, MESH, SURF>(S, hs, time, want, take, cap);
+RTX_HD void enum_root(const SceneView& S, const HStack& hs, f3 ro, f3 rd, float time, Want& want, Take& take, Cap& cap) {
+    at_depth<kNode[ROOT].depth>(hs, ro, rd);
+    if (!RTX_ANY(ray_meets(hbox<ROOT>(S).lo, hbox<ROOT>(S).hi, ro, rd, cap()))) return;
+    enum_node<ROOT, ROOT, MESH, SURF>(S, hs, ro, rd, time, want, take, cap);
 }
 
-// diff_shadow(X)
+// diff_shadow(X), (ro, rd) the ray of X's depth
 template <int X, bool MESH>
-RTX_HD bool diff_shadow(const SceneView& S, const HStack& hs, float time) {
+RTX_HD bool diff_shadow(const SceneView& S, const HStack& hs, f3 ro, f3 rd, float time) {
     constexpr rtx_csg::CNode x = kNode[X];
-    {
-        f3 ro, rd;
-        hs.get_ray(x.depth, ro, rd);
-        hs.put_ray(x.depth + 1, xform(rtx_csg::kMinv[X], ro, 1.0f), xform(rtx_csg::kMinv[X], rd, 0.0f));
-    }
+    at_depth<x.depth>(hs, ro, rd);
+    const f3 co = xform(rtx_csg::kMinv[X], ro, 1.0f), cd = xform(rtx_csg::kMinv[X], rd, 0.0f);
+    to_depth<x.depth + 1>(hs, co, cd);
     constexpr int c0 = X + 1, c1 = kNode[c0].end;
     static_assert(c1 < x.end, "a difference has two children (rtx_api.hip jit_csg_tables)");
     bool found = false;
@@ -1678,61 +1716,55 @@ RTX_HD bool diff_shadow(const SceneView& S, const HStack& hs, float time) {
     auto cap = [&]() { return found ? -1.0f : INFINITY; };
     {
         auto take = [&](double, f3 pos, f3, int32_t, int32_t) { found = inside<c1>(S, pos, time) == false; };
-        enum_root<c0, MESH, false>(S, hs, time, want, take, cap);
+        enum_root<c0, MESH, false>(S, hs, co, cd, time, want, take, cap);
     }
     {
         auto take = [&](double, f3 pos, f3, int32_t, int32_t) { found = inside<c0>(S, pos, time) == true; };
-        enum_root<c1, MESH, false>(S, hs, time, want, take, cap);
+        enum_root<c1, MESH, false>(S, hs, co, cd, time, want, take, cap);
     }
     return found;
 }
 
-// hier_shadow: the children of the open node X (value acc so far)
+// hier_shadow: the children of the open node X (value acc so far), (ro, rd) their ray
 template <int X, int C, bool MESH>
-RTX_HD bool shadow_kids(const SceneView& S, const HStack& hs, double t_max, float time, bool acc) {
+RTX_HD bool shadow_kids(const SceneView& S, const HStack& hs, f3 ro, f3 rd, double t_max, float time, bool acc) {
     constexpr rtx_csg::CNode x = kNode[X];
     if constexpr (C >= x.end) {
         return acc;
     } else {
         constexpr rtx_csg::CNode c = kNode[C];
         if (decided(acc, x.kind, c.cidx)) return acc;
-        bool live;
-        {
-            f3 ro, rd;
-            hs.get_ray(c.depth, ro, rd);
-            live = ray_meets(S.sbox[C].lo, S.sbox[C].hi, ro, rd, INFINITY);
-        }
+        at_depth<c.depth>(hs, ro, rd);
+        const bool live = ray_meets(sbox<C>(S).lo, sbox<C>(S).hi, ro, rd, INFINITY);
         bool v = false;
         if (RTX_ANY(live)) {
             if constexpr (c.kind == HN_LEAF) {
-                f3 lo, ld;
-                hs.get_ray(c.depth, lo, ld);
-                v = live && leaf_shadow<MESH>(S, S.objs[c.obj], lo, ld, t_max, time);
+                v = live && leaf_shadow<MESH>(S, obj<c.obj>(S), ro, rd, t_max, time);
             } else if constexpr (c.kind == HN_DIFF) {
-                if (live) v = diff_shadow<C, MESH>(S, hs, time);
+                if (live) v = diff_shadow<C, MESH>(S, hs, ro, rd, time);
             } else if constexpr (c.kind != HN_OTHER) {
-                f3 ro, rd;
-                hs.get_ray(c.depth, ro, rd);
-                hs.put_ray(c.depth + 1, xform(rtx_csg::kMinv[C], ro, 1.0f), xform(rtx_csg::kMinv[C], rd, 0.0f));
-                v = shadow_kids<C, C + 1, MESH>(S, hs, t_max, time, c.kind == HN_INTER);
+                const f3 co = xform(rtx_csg::kMinv[C], ro, 1.0f), cd = xform(rtx_csg::kMinv[C], rd, 0.0f);
+                to_depth<c.depth + 1>(hs, co, cd);
+                v = shadow_kids<C, C + 1, MESH>(S, hs, co, cd, t_max, time, c.kind == HN_INTER);
             }
         }
-        return shadow_kids<X, c.end, MESH>(S, hs, t_max, time, fold(acc, x.kind, c.cidx, v));
+        return shadow_kids<X, c.end, MESH>(S, hs, ro, rd, t_max, time, fold(acc, x.kind, c.cidx, v));
     }
 }
 // hier_shadow(R)
 template <int R, bool MESH>
 RTX_HD bool shadow_root(const SceneView& S, const HStack& hs, f3 o, f3 d, double t_max, float time) {
-    hs.put_ray(0, o, d);
-    if (!RTX_ANY(ray_meets(S.sbox[R].lo, S.sbox[R].hi, o, d, INFINITY))) return false;
+    to_depth<0>(hs, o, d);
+    if (!RTX_ANY(ray_meets(sbox<R>(S).lo, sbox<R>(S).hi, o, d, INFINITY))) return false;
     constexpr rtx_csg::CNode r = kNode[R];
     if constexpr (r.kind == HN_OTHER) {
         return false;
     } else if constexpr (r.kind == HN_DIFF) {
-        return diff_shadow<R, MESH>(S, hs, time);
+        return diff_shadow<R, MESH>(S, hs, o, d, time);
     } else {
-        hs.put_ray(1, xform(rtx_csg::kMinv[R], o, 1.0f), xform(rtx_csg::kMinv[R], d, 0.0f));
-        return shadow_kids<R, R + 1, MESH>(S, hs, t_max, time, r.kind == HN_INTER);
+        const f3 co = xform(rtx_csg::kMinv[R], o, 1.0f), cd = xform(rtx_csg::kMinv[R], d, 0.0f);
+        to_depth<1>(hs, co, cd);
+        return shadow_kids<R, R + 1, MESH>(S, hs, co, cd, t_max, time, r.kind == HN_INTER);
     }
 }
 // hier_occluded: roots R, R' = end(R), ... (Q: R's ordinal)
@@ -1776,7 +1808,7 @@ RTX_HD void closest_roots(const SceneView& S, const HStack& hs, f3 o, f3 d, floa
                 hh = HHit{t, pos, n, mat, (ty == OBJ_PLANE || ty == OBJ_BOX) ? leaf : -1};
             };
             auto cap = [&]() { return h.t32; };
-            enum_root<R, MESH, true>(S, hs, time, want, take, cap);
+            enum_root<R, MESH, true>(S, hs, o, d, time, want, take, cap);
         }
         closest_roots<MESH, kNode[R].end, Q + 1>(S, hs, o, d, time, h, hh, rmask);
     }
@@ -1898,11 +1930,12 @@ RTX_HD bool hier_occluded(const SceneView& S, const HStack& hs, f3 o, f3 d, doub
 template <bool MESH>
 RTX_HY void hier_closest(const SceneView& S, const HStack& hs, f3 o, f3 d, float time, Hit& h, HHit& hh,
                          uint32_t rmask = ~0u) {
-    hs.put_ray(0, o, d);
 #if defined(RTX_CSG_STATIC)
+    csg::to_depth<0>(hs, o, d);
     csg::closest_roots<MESH, 0, 0>(S, hs, o, d, time, h, hh, rmask);
     return;
 #endif
+    hs.put_ray(0, o, d);
     // The root whose hit box the wave's first ray enters first goes first: its hit then
     // caps the others' culling. Candidates compare by (t, top-level position), so the
     // order of the roots does not change the result (the order inside a root does, on

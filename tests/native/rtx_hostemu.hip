@@ -558,8 +558,10 @@ extern "C" int64_t rtx_hostemu_jit_split(const rtx_scene_desc* sd, int32_t pass,
     HostScene H;
     if (convert_scene(sd, H)) return -2;
     if (cost) *cost = H.nodes.empty() ? -1 : csg_cost(H.nodes);
-    const std::string tables = jit_csg_tables(H.nodes);
+    std::string tables = jit_csg_tables(H.nodes);
     if (tables.empty()) return -1;
+    if (opt(OPT_JIT_CSG) >= 2.0)  // (the boxes of motion time 0)
+        tables += jit_csg_baked(compute_bounds(H.nodes, H.objs, H.tris, 0.0, 0.0), H.objs, opt(OPT_JIT_CSG) >= 3.0 ? 3 : 2);
     const JitSpec sp = jit_split_spec("gfx950", tables, H.has_mesh, H.has_secondary, cnt != 0, jit != 0, pass);
     std::string s = sp.name + "\n";
     for (const auto& o : sp.opts) s += o + "\n";
