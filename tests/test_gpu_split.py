@@ -38,12 +38,15 @@ def test_split_matches_oracle(name, res, edits, split):
 
 
 @pytest.mark.parametrize("seed", range(24))
-def test_split_random_hierarchy_scenes(seed, split):
+def test_split_random_hierarchy_scenes(seed, split, monkeypatch):
+    """Random hierarchy scenes (every fourth with a mesh): every third seed with the passes
+    specialized on its trees (a compile each), the others with the precompiled passes."""
     from scenegen import random_hier_scene
+    monkeypatch.setattr(OPTS, "jit_csg", "1" if seed % 3 == 0 else "0")
     d = random_hier_scene(seed, res=(64, 48), mesh=(seed % 4 == 0))
     sc = product_scene_dict(d)
     assert_parity(sc.render(), oracle_render_dict(d), "hier seed %d" % seed)
-    assert sc.last_kernel.startswith(SPLIT), sc.last_kernel
+    assert sc.last_kernel.startswith("rtx_jit_split_" if seed % 3 == 0 else "k_split_"), sc.last_kernel
 
 
 def test_split_tallies_match_oracle(split):

@@ -9,7 +9,8 @@ sum the kernels' per-dispatch averages times their dispatches per frame, and "ke
 breaks them down. bench.py reads counters_per_dispatch (= per frame) and
 hbm_bytes_per_launch (= per frame).
 
-usage: python tools/pmc_summary.py gpurun_out/<tag> <config> [frames=5] > profiles/rNN/pmc_<config>.json
+usage: python tools/pmc_summary.py gpurun_out/<tag> <config> [frames=6] > profiles/rNN/pmc_<config>.json
+(frames: tools/prof_driver.py renders --iters + 1, all with the specialized kernels)
 """
 import csv
 import glob
@@ -18,7 +19,7 @@ import os
 import sys
 
 d, cfg = sys.argv[1], sys.argv[2]
-frames = int(sys.argv[3]) if len(sys.argv) > 3 else 5  # tools/prof_driver.py --iters in pmc_session.sh
+frames = int(sys.argv[3]) if len(sys.argv) > 3 else 6  # tools/prof_driver.py --iters 5 (pmc_session.sh) + 1
 RENDER = ("k_render", "rtx_jit_render", "k_split_", "rtx_jit_split_", "k_mesh_chunks")
 per = {}  # kernel -> counter -> [values per dispatch]
 for f in sorted(glob.glob(os.path.join(d, "p*", "*counter_collection.csv"))):

@@ -1,7 +1,11 @@
-"""Minimal render loop for rocprofv3 runs: N frames of a bench config on cuda:0."""
+"""Minimal render loop for rocprofv3 runs: N + 1 frames of a bench config on cuda:0, every
+one with the product's (scene-specialized) kernels: compiles wait inside the first render
+(RTX_JIT_ASYNC=0), so no generic-kernel frame mixes into the counters."""
 import argparse
 import os
 import sys
+
+os.environ.setdefault("RTX_JIT_ASYNC", "0")  # (read when librtx.so loads)
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "python-raytracer_amd"))
@@ -19,7 +23,7 @@ torch.cuda.set_device(0)
 sc = bench.make_scene(a.config)
 fb = torch.empty((sc.vc.height, sc.vc.width, 3), dtype=torch.float32, device="cuda")
 sc.render_device(out=fb)
-sc.jit_wait()  # (the specialized kernel: the profiled frames are the product's)
+assert sc.jit_wait() == 0  # (the specialized kernels: the profiled frames are the product's)
 for _ in range(a.iters):
     sc.render_device(out=fb)
 torch.cuda.synchronize()

@@ -36,7 +36,7 @@ for s in ${STEPS:-tests smoke bench rocprof}; do
   case $s in
     tests)
       if [ -n "${KEXPR:-}" ]; then kx=(-k "$KEXPR"); else kx=(); fi
-      step pytest_gpu 900 python -u -m pytest ${TESTS:-tests} "${kx[@]}" -m gpu -x -q -p no:cacheprovider \
+      step pytest_gpu ${TESTS_TIMEOUT:-900} python -u -m pytest ${TESTS:-tests} "${kx[@]}" -m gpu -x -q -p no:cacheprovider \
         --timeout 120 --timeout-method thread
       rc=$?; [ $rc -eq 0 ] || [ "${KEEP_GOING:-0}" = 1 -a $rc -eq 1 ] || exit 1 ;;
     smoke)
@@ -61,7 +61,7 @@ for s in ${STEPS:-tests smoke bench rocprof}; do
     pmc)
       for c in $CFGS; do
         CFG=$c TAG="${OUT#gpurun_out/}/pmc_$c" bash tools/pmc_session.sh > "$OUT/pmc_$c.log" 2>&1 || { tail "$OUT/pmc_$c.log"; exit 1; }
-        python tools/pmc_summary.py "$OUT/pmc_$c" $c > "$OUT/pmc_$c.json" || exit 1
+        python tools/pmc_summary.py "$OUT/pmc_$c" $c 6 > "$OUT/pmc_$c.json" || exit 1
         python -c "import json;d=json.load(open('$OUT/pmc_$c.json'));c=d['counters_per_dispatch'];print('$c', d['kernel'], 'WRITE_KiB', c.get('WRITE_SIZE'), 'FETCH_KiB', c.get('FETCH_SIZE'), 'hbm_B', d.get('hbm_bytes_per_launch'), 'valu/wave', d.get('valu_insts_per_wave'))"
       done ;;
     rocprof)
