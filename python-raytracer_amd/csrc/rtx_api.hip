@@ -74,7 +74,7 @@ enum Opt {
     OPT_SPLIT, OPT_SPLIT_BYTES, OPT_SPLIT_RATIO, OPT_BINS, OPT_HEAVY_TILES, OPT_LENS_BINS, OPT_LGRID, OPT_DSGRID, OPT_DSGRID_MIN,
     OPT_SELF_SKIP, OPT_TILE_SCHED, OPT_XCD_MAP, OPT_TILE_BLOCK, OPT_PRIM_ORIGIN, OPT_SPP, OPT_SPP_MIN, OPT_JIT, OPT_JIT_BAKE, OPT_JIT_EXT,
     OPT_JIT_DUMP, OPT_JIT_IDLE_BAKED, OPT_JIT_DISK_BAKED, OPT_JIT_CACHE, OPT_JIT_FLAGS, OPT_JIT_ILP, OPT_JIT_ASYNC,
-    OPT_DEV_BINS, OPT_CHUNK_MODE, OPT_BIN_LDS, OPT_JIT_CSG, OPT_SETUP_LOG, OPT_COUNT
+    OPT_DEV_BINS, OPT_CHUNK_MODE, OPT_BIN_LDS, OPT_JIT_CSG, OPT_CSG_RAYS, OPT_SETUP_LOG, OPT_COUNT
 };
 struct OptDef {
     const char* name;
@@ -112,6 +112,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"chunk_mode", 3, false},                 // heavy-tile pass: bit 0 LDS-staged faces, bit 1 XCD-aware order
     {"bin_lds", 0, false},                    // primary-ray face lists staged in LDS (specialized mesh kernels)
     {"jit_csg", 1, false},                    // split hierarchy passes specialized on the CSG trees (2: + boxes, 3: + objects)
+    {"csg_rays", 3, false},                   // their rays in registers (bit 0: trace, bit 1: shadow), else the LDS stack
     {"setup_log", 0, false},                  // print the host time of each rtx_camera_set step
 };
 struct OptVal {
@@ -1761,7 +1762,6 @@ const char* const kLibMacros[] = {
 #endif
     "-DRTX_HIER_INLINE=" RTX_STR(RTX_HIER_INLINE),
     "-DRTX_HEAVY_CHUNK=" RTX_STR(RTX_HEAVY_CHUNK),
-    "-DRTX_CSG_RAYREG=" RTX_STR(RTX_CSG_RAYREG),  // (the host sizes the split passes' LDS from it)
 #ifdef RTX_PAD
     "-DRTX_PAD=" RTX_STR(RTX_PAD),
 #endif
@@ -2059,14 +2059,16 @@ std::string jit_csg_baked(const std::vector<DBound>& bounds, const std::vector<D
 // The split pass kernel specialized on a node table (rtx_split.h split_trace / split_shadow,
 // with the static traversals): the library's own kernel build otherwise.
 JitSpec jit_split_spec(const std::string& arch, const std::string& tables, bool mesh, bool sec, bool cnt, bool jit,
-                       int pass) {
+                       int pass, bool rayreg) {
     JitSpec sp;
     sp.opts = {"--offload-arch=" + arch, "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize"};
     for (const char* m : kLibMacros) sp.opts.push_back(m);
+    // rays in registers, or the LDS stack (option csg_rays; the launch sizes the LDS from it)
+    sp.opts.push_back(rayreg ? "-DRTX_CSG_RAYREG=1" : "-DRTX_CSG_RAYREG=0");
     // the shadow pass with its rays in registers: at most 128 VGPRs (4 waves/SIMD), which its
     // precompiled form's LDS stack had imposed (1 wave bound: 129 VGPRs, NovelScene1 13.35 ms
     // against 11.36 bounded, profiles/r06/s13/)
-    if (pass == 1 && RTX_CSG_RAYREG) {
+    if (pass == 1 && rayreg) {
         sp.opts.push_back("-URTX_LB_SPLIT_B");
         sp.opts.push_back("-DRTX_LB_SPLIT_B=4");
     }
@@ -2183,6 +2185,7 @@ struct JitSlot {
     std::shared_future<std::string> fut;  // the compile (pending)
     std::string dkey;                     // the device key it loads under (pending)
     bool baked = false;
+    bool lds = true;  // a split pass: its rays on the LDS stack (else registers, no LDS)
 };
 
 namespace {
@@ -2206,13 +2209,13 @@ void jit_render_kernel(int device, const SceneView& v, const KParams& kp, const 
 // The specialized split pass (pass 0 trace, 1 shadow) of a hierarchy scene whose node table
 // is `tables` (jit_csg_tables; "" or option jit_csg 0: the precompiled passes run).
 void jit_split_kernel(int device, const std::string& tables, bool mesh, bool sec, bool cnt, bool jit, int pass,
-                      JitSlot& r) {
+                      bool rayreg, JitSlot& r) {
     r.fn = nullptr;
     r.pending = false;
     if (!jit_enabled() || !opt_on(OPT_JIT_CSG) || tables.empty()) return;
     const std::string arch = device_arch(device);
     if (arch.empty()) return;
-    jit_start(device, jit_split_spec(arch, tables, mesh, sec, cnt, jit, pass), r);
+    jit_start(device, jit_split_spec(arch, tables, mesh, sec, cnt, jit, pass, rayreg), r);
 }
 
 // Resolves slot r for spec sp: the kernel from memory or the disk cache, or a compile on a
@@ -3337,9 +3340,10 @@ int render_split(rtx_scene* s, Launch L, const KParams* kp, size_t hbytes, hipSt
             // option jit_csg 2 / 3: the camera's boxes / and the object records as literals too
             const int bake = opt(OPT_JIT_CSG) >= 3.0 ? 3 : opt(OPT_JIT_CSG) >= 2.0 ? 2 : 0;
             const bool can = !s->csg_tables.empty() && s->tr_valid && s->tr_bounds.size() == s->h_nodes.size();
+            r.lds = (((int)opt(OPT_CSG_RAYS) >> pass) & 1) == 0;
             jit_split_kernel(s->device,
                              bake && can ? s->csg_tables + jit_csg_baked(s->tr_bounds, s->h_objs, bake) : s->csg_tables,
-                             s->has_mesh, s->has_secondary, cnt, (sel & 1) != 0, pass, r);
+                             s->has_mesh, s->has_secondary, cnt, (sel & 1) != 0, pass, !r.lds, r);
             if (r.pending && !opt_on(OPT_JIT_ASYNC) && !capturing) jit_poll(r, true);
             r.done = true;
         } else if (r.pending && !capturing) {
@@ -3357,8 +3361,8 @@ int render_split(rtx_scene* s, Launch L, const KParams* kp, size_t hbytes, hipSt
             Launch La = Lc;
             SplitBuf sbb = sb;
             void* args[] = {(void*)&kpp, (void*)&La, (void*)&sbb};
-            // (rays in registers: the specialized passes use no LDS stack, RTX_CSG_RAYREG)
-            const unsigned lds = RTX_CSG_RAYREG ? 0u : (unsigned)r.lds_bytes;
+            // (rays in registers: no LDS stack, option csg_rays)
+            const unsigned lds = sk[pass]->lds ? (unsigned)r.lds_bytes : 0u;
             return hipModuleLaunchKernel(sk[pass]->fn, r.nblocks, 1, 1, B, 1, 1, lds, r.stream, args, nullptr);
         }
         return s->has_mesh ? launch_split_m1(sel, pass, r, Lc, sb) : launch_split_m0(sel, pass, r, Lc, sb);
