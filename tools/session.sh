@@ -47,7 +47,9 @@ for s in ${STEPS:-tests smoke bench rocprof}; do
     configs)
       for c in $CFGS; do
         pj=""; [ -f "$OUT/pmc_$c.json" ] && pj="--pmc-json $OUT/pmc_$c.json"
-        step bench_$c 600 python bench.py --config $c --steps ${BSTEPS:-20} --warmup 3 $(cpu_flag) $pj || exit 1
+        st=${BSTEPS:-20}; wu=3  # (microsecond frames: 300 of them, past the tile schedule's first frames)
+        case $c in tsp1080|tm1080|mr1080|blob1080) st=${BSTEPS_FAST:-300}; wu=20 ;; ns2) st=${BSTEPS_NS2:-5} ;; esac
+        step bench_$c 600 python bench.py --config $c --steps $st --warmup $wu $(cpu_flag) $pj || exit 1
         grep '^{' "$OUT/bench_$c.log" > "$OUT/bench_$c.json"
       done ;;
     ab)
