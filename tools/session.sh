@@ -37,7 +37,7 @@ for s in ${STEPS:-tests smoke bench rocprof}; do
     tests)
       if [ -n "${KEXPR:-}" ]; then kx=(-k "$KEXPR"); else kx=(); fi
       step pytest_gpu ${TESTS_TIMEOUT:-900} python -u -m pytest ${TESTS:-tests} "${kx[@]}" -m gpu -x -q -p no:cacheprovider \
-        --timeout 120 --timeout-method thread
+        --timeout 120 --timeout-method thread ${DURATIONS:+--durations=$DURATIONS}
       rc=$?; [ $rc -eq 0 ] || [ "${KEEP_GOING:-0}" = 1 -a $rc -eq 1 ] || exit 1 ;;
     smoke)
       step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
