@@ -1827,15 +1827,35 @@ struct JitSpec {
     bool baked = false;  // the source carries the scene's record values
 };
 
+// What the scene-specialized kernels pin of a scene (object and light counts, static
+// scene, light kinds, pow loop length, a uniform integer hardness) and -- camera -- of its
+// camera (sample counts: the 1-spp loops vanish; divisor kind, jitter mode).
+void jit_fixed_opts(const SceneView& v, const KParams& kp, const SceneTraits& tr, bool camera,
+                    std::vector<std::string>& opts) {
+    for (const std::string& o :
+         {std::string("-DRTX_FIXED_COUNTS"), "-DRTX_FIXED_NP=" + std::to_string(v.n_plane),
+          "-DRTX_FIXED_NS=" + std::to_string(v.n_sphere), "-DRTX_FIXED_NB=" + std::to_string(v.n_box),
+          "-DRTX_FIXED_NM=" + std::to_string(v.n_mesh), "-DRTX_FIXED_NL=" + std::to_string(v.n_lights),
+          "-DRTX_FACE_CULL_MODE=" + std::to_string(tr.fc_mode),
+          "-DRTX_FIXED_STATIC=" + std::to_string(tr.any_speed ? 0 : 1),
+          "-DRTX_FIXED_LDIR=" + std::to_string(tr.light_dir_mask) + "u",
+          "-DRTX_FIXED_POWBITS=" + std::to_string(v.pow_bits)})
+        opts.push_back(o);
+    if (tr.uniform_hard >= 0) opts.push_back("-DRTX_FIXED_HARD=" + std::to_string(tr.uniform_hard));
+    if (!camera) return;
+    for (const std::string& o :
+         {std::string("-DRTX_FIXED_SAMPLES"), "-DRTX_FIXED_NDOF=" + std::to_string(kp.n_dof),
+          "-DRTX_FIXED_NAA=" + std::to_string(kp.n_aa), "-DRTX_FIXED_NTIMES=" + std::to_string(kp.n_times),
+          "-DRTX_FIXED_DIVPOW2=" + std::to_string(kp.div_pow2), "-DRTX_FIXED_JMODE=" + std::to_string(kp.jitter)})
+        opts.push_back(o);
+}
+
 // The specialized kernel of a scene and camera for arch (false: the generic kernel runs).
 // Host code only, so the tests' host build can print it (tools/jit_offline.py compiles it
 // to ISA without a GPU).
 bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, const SceneTraits& tr, bool mesh,
               bool sec, bool ext, bool cnt, bool jit, bool spp, bool out8, const std::string& baked, JitSpec& out) {
     const int fc_mode = tr.fc_mode;
-    const bool any_speed = tr.any_speed;
-    const uint32_t ldir = tr.light_dir_mask;
-    const int uniform_hard = tr.uniform_hard;
     if (v.n_plane + v.n_sphere + v.n_box + v.n_mesh > 32 || v.n_lights > 8) return false;  // code size
     // CSG/texture kernels: the unrolled loops raise their (already high) register
     // pressure and the specialized kernel measured slower (NovelScene1 105 -> 134 ms)
@@ -1847,28 +1867,11 @@ bool jit_spec(const std::string& arch, const SceneView& v, const KParams& kp, co
     // spills) and run faster: TSP 1080p 24.1 -> 21.5 us, MirrorRefraction 40.2 -> 38.3 us,
     // TorusMesh 48.9 -> 46.7 us, DepthOfField 4K 4.62 -> 4.38 ms (profiles/r05/noslp/).
     std::vector<std::string> opts = {"--offload-arch=" + arch, "-O3", "-std=c++17", "-ffp-contract=off",
-                                     "-fno-slp-vectorize", "-DRTX_FIXED_COUNTS",
-                                     "-DRTX_FIXED_NP=" + std::to_string(v.n_plane),
-                                     "-DRTX_FIXED_NS=" + std::to_string(v.n_sphere),
-                                     "-DRTX_FIXED_NB=" + std::to_string(v.n_box),
-                                     "-DRTX_FIXED_NM=" + std::to_string(v.n_mesh),
-                                     "-DRTX_FIXED_NL=" + std::to_string(v.n_lights),
-                                     "-DRTX_FACE_CULL_MODE=" + std::to_string(fc_mode),
-                                     // the camera's sample counts (the 1-spp loops vanish)
-                                     "-DRTX_FIXED_SAMPLES",
-                                     "-DRTX_FIXED_NDOF=" + std::to_string(kp.n_dof),
-                                     "-DRTX_FIXED_NAA=" + std::to_string(kp.n_aa),
-                                     "-DRTX_FIXED_NTIMES=" + std::to_string(kp.n_times),
-                                     // static scene, light kinds, pow loop length, divisor kind
-                                     "-DRTX_FIXED_STATIC=" + std::to_string(any_speed ? 0 : 1),
-                                     "-DRTX_FIXED_LDIR=" + std::to_string(ldir) + "u",
-                                     "-DRTX_FIXED_POWBITS=" + std::to_string(v.pow_bits),
-                                     "-DRTX_FIXED_DIVPOW2=" + std::to_string(kp.div_pow2),
-                                     "-DRTX_FIXED_JMODE=" + std::to_string(kp.jitter)};
+                                     "-fno-slp-vectorize"};
+    jit_fixed_opts(v, kp, tr, true, opts);
     // the strip width too: the tile index arithmetic becomes multiplications by constants
     // (TSP 1080p 27.85 -> 27.37 us, profiles/r03/ncols/; one compile per strip width)
     if (!spp) opts.push_back("-DRTX_FIXED_NCOLS=" + std::to_string(kp.ncols));
-    if (uniform_hard >= 0) opts.push_back("-DRTX_FIXED_HARD=" + std::to_string(uniform_hard));
     if (!spp && !ext && kp.tile_time != nullptr) opts.push_back("-DRTX_TILE_SCHED=1");
     if (!spp && !ext && kp.po_valid) opts.push_back("-DRTX_PRIM_ORIGIN=1");
     if (out8) opts.push_back("-DRTX_OUT8=1");  // uint8 framebuffer (rtx_render_rgb8)
@@ -2059,9 +2062,13 @@ std::string jit_csg_baked(const std::vector<DBound>& bounds, const std::vector<D
 // The split pass kernel specialized on a node table (rtx_split.h split_trace / split_shadow,
 // with the static traversals): the library's own kernel build otherwise.
 JitSpec jit_split_spec(const std::string& arch, const std::string& tables, bool mesh, bool sec, bool cnt, bool jit,
-                       int pass, bool rayreg) {
+                       int pass, bool rayreg, const std::vector<std::string>& fixed) {
     JitSpec sp;
     sp.opts = {"--offload-arch=" + arch, "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize"};
+    // the scene's counts (jit_fixed_opts; NovelScene1 11.41 -> 11.31 ms, profiles/r06/s17/ f1).
+    // Not the camera's: 11.18 ms, but then every camera with other sample counts compiles
+    // its own ~20 s pair of passes (the GPU suite's NovelScene cameras: 8.7 -> 13+ min)
+    sp.opts.insert(sp.opts.end(), fixed.begin(), fixed.end());
     for (const char* m : kLibMacros) sp.opts.push_back(m);
     // rays in registers, or the LDS stack (option csg_rays; the launch sizes the LDS from it)
     sp.opts.push_back(rayreg ? "-DRTX_CSG_RAYREG=1" : "-DRTX_CSG_RAYREG=0");
@@ -2209,13 +2216,13 @@ void jit_render_kernel(int device, const SceneView& v, const KParams& kp, const 
 // The specialized split pass (pass 0 trace, 1 shadow) of a hierarchy scene whose node table
 // is `tables` (jit_csg_tables; "" or option jit_csg 0: the precompiled passes run).
 void jit_split_kernel(int device, const std::string& tables, bool mesh, bool sec, bool cnt, bool jit, int pass,
-                      bool rayreg, JitSlot& r) {
+                      bool rayreg, const std::vector<std::string>& fixed, JitSlot& r) {
     r.fn = nullptr;
     r.pending = false;
     if (!jit_enabled() || !opt_on(OPT_JIT_CSG) || tables.empty()) return;
     const std::string arch = device_arch(device);
     if (arch.empty()) return;
-    jit_start(device, jit_split_spec(arch, tables, mesh, sec, cnt, jit, pass, rayreg), r);
+    jit_start(device, jit_split_spec(arch, tables, mesh, sec, cnt, jit, pass, rayreg, fixed), r);
 }
 
 // Resolves slot r for spec sp: the kernel from memory or the disk cache, or a compile on a
@@ -3341,9 +3348,11 @@ int render_split(rtx_scene* s, Launch L, const KParams* kp, size_t hbytes, hipSt
             const int bake = opt(OPT_JIT_CSG) >= 3.0 ? 3 : opt(OPT_JIT_CSG) >= 2.0 ? 2 : 0;
             const bool can = !s->csg_tables.empty() && s->tr_valid && s->tr_bounds.size() == s->h_nodes.size();
             r.lds = (((int)opt(OPT_CSG_RAYS) >> pass) & 1) == 0;
+            std::vector<std::string> fixed;
+            jit_fixed_opts(s->view, s->kp, s->traits, false, fixed);
             jit_split_kernel(s->device,
                              bake && can ? s->csg_tables + jit_csg_baked(s->tr_bounds, s->h_objs, bake) : s->csg_tables,
-                             s->has_mesh, s->has_secondary, cnt, (sel & 1) != 0, pass, !r.lds, r);
+                             s->has_mesh, s->has_secondary, cnt, (sel & 1) != 0, pass, !r.lds, fixed, r);
             if (r.pending && !opt_on(OPT_JIT_ASYNC) && !capturing) jit_poll(r, true);
             r.done = true;
         } else if (r.pending && !capturing) {

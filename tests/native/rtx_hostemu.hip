@@ -562,8 +562,9 @@ extern "C" int64_t rtx_hostemu_jit_split(const rtx_scene_desc* sd, int32_t pass,
     if (tables.empty()) return -1;
     if (opt(OPT_JIT_CSG) >= 2.0)  // (the boxes of motion time 0)
         tables += jit_csg_baked(compute_bounds(H.nodes, H.objs, H.tris, 0.0, 0.0), H.objs, opt(OPT_JIT_CSG) >= 3.0 ? 3 : 2);
+    // (without the camera's counts, jit_fixed_opts: render_split adds them per camera)
     const JitSpec sp = jit_split_spec("gfx950", tables, H.has_mesh, H.has_secondary, cnt != 0, jit != 0, pass,
-                                      ((int)opt(OPT_CSG_RAYS) >> pass) & 1);
+                                      ((int)opt(OPT_CSG_RAYS) >> pass) & 1, std::vector<std::string>());
     std::string s = sp.name + "\n";
     for (const auto& o : sp.opts) s += o + "\n";
     s += "\n" + sp.src;
