@@ -74,7 +74,7 @@ enum Opt {
     OPT_SPLIT, OPT_SPLIT_BYTES, OPT_SPLIT_RATIO, OPT_BINS, OPT_HEAVY_TILES, OPT_LENS_BINS, OPT_LGRID, OPT_DSGRID, OPT_DSGRID_MIN,
     OPT_SELF_SKIP, OPT_TILE_SCHED, OPT_XCD_MAP, OPT_TILE_BLOCK, OPT_PRIM_ORIGIN, OPT_SPP, OPT_SPP_MIN, OPT_JIT, OPT_JIT_BAKE, OPT_JIT_EXT,
     OPT_JIT_DUMP, OPT_JIT_IDLE_BAKED, OPT_JIT_DISK_BAKED, OPT_JIT_CACHE, OPT_JIT_FLAGS, OPT_JIT_ILP, OPT_JIT_ASYNC,
-    OPT_DEV_BINS, OPT_CHUNK_MODE, OPT_BIN_LDS, OPT_JIT_CSG, OPT_CSG_RAYS, OPT_SETUP_LOG, OPT_COUNT
+    OPT_DEV_BINS, OPT_CHUNK_MODE, OPT_BIN_LDS, OPT_JIT_CSG, OPT_CSG_RAYS, OPT_CSG_SHADE, OPT_SETUP_LOG, OPT_COUNT
 };
 struct OptDef {
     const char* name;
@@ -113,6 +113,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"bin_lds", 0, false},                    // primary-ray face lists staged in LDS (specialized mesh kernels)
     {"jit_csg", 1, false},                    // split hierarchy passes specialized on the CSG trees (2: + boxes, 3: + objects)
     {"csg_rays", 3, false},                   // their rays in registers (bit 0: trace, bit 1: shadow), else the LDS stack
+    {"csg_shade", 0, false},                  // the shade pass compiled with them (measured no faster)
     {"setup_log", 0, false},                  // print the host time of each rtx_camera_set step
 };
 struct OptVal {
@@ -2089,6 +2090,10 @@ JitSpec jit_split_spec(const std::string& arch, const std::string& tables, bool 
         sp.name = "rtx_jit_split_trace_";
         for (bool f : {mesh, sec, cnt, jit}) sp.name += f ? '1' : '0';
         args += std::string(", ") + b(sec) + ", " + b(cnt) + ", " + b(jit) + ">";
+    } else if (pass == 2) {
+        sp.name = "rtx_jit_split_shade_";
+        for (bool f : {mesh, sec}) sp.name += f ? '1' : '0';
+        args += std::string(", ") + b(sec) + ">";
     } else {
         sp.name = "rtx_jit_split_shadow_";
         for (bool f : {mesh, cnt}) sp.name += f ? '1' : '0';
@@ -2100,9 +2105,9 @@ JitSpec jit_split_spec(const std::string& arch, const std::string& tables, bool 
     const std::string tools_guard = "#undef RTX_TOOLS_BUILD\n";
 #endif
     sp.src = tools_guard + tables + "#include \"rtx_split.h\"\nextern \"C\" __global__ __launch_bounds__(rtx::kBlock<true>, " +
-             (pass == 0 ? "RTX_LB_SPLIT_A" : "RTX_LB_SPLIT_B") + ") void " + sp.name +
+             (pass == 0 ? "RTX_LB_SPLIT_A" : pass == 1 ? "RTX_LB_SPLIT_B" : "5") + ") void " + sp.name +
              "(const rtx::KParams* __restrict__ Pp, const rtx::Launch L, rtx::SplitBuf sb) {\n  rtx::" +
-             (pass == 0 ? "split_trace" : "split_shadow") + args + "(Pp, L, sb);\n}\n";
+             (pass == 0 ? "split_trace" : pass == 1 ? "split_shadow" : "split_shade") + args + "(Pp, L, sb);\n}\n";
     sp.baked = true;  // (the scene's own kernel: pruned from memory and disk as the baked ones)
     return sp;
 }
@@ -2357,9 +2362,9 @@ struct rtx_scene {
     void* d_dsg_cells = nullptr;
     // the kernel resolved for each (counters, jitter, sample-parallel) variant of the
     // current camera: looked up (and compiled) once per camera, not per frame; nullptr
-    // after a lookup means the generic kernel; 16-23: the split hierarchy passes
+    // after a lookup means the generic kernel; 16-27: the split hierarchy passes
     // (16 + 4 pass + 2 counters + jitter, jit_split_kernel)
-    JitSlot resolved[24];
+    JitSlot resolved[28];
     std::string last_kernel;  // name of the kernel the last render call launched
     std::string jit_baked;    // the scene records as constant arrays (jit_baked_records)
     std::string csg_tables;   // the hierarchy node table (jit_csg_tables)
@@ -3339,15 +3344,20 @@ int render_split(rtx_scene* s, Launch L, const KParams* kp, size_t hbytes, hipSt
         RTX_HIP(hipStreamWaitEvent(st, s->split_done, 0));
     // the trace and shadow passes specialized on the scene's CSG trees, when compiled
     // (jit_split_kernel; the precompiled passes render meanwhile: the same bytes)
-    JitSlot* sk[2];
-    for (int pass = 0; pass < 2; ++pass) {
-        JitSlot& r = s->resolved[16 + 4 * pass + (cnt ? 2 : 0) + ((sel & 1) ? 1 : 0)];
+    JitSlot* sk[3];
+    for (int pass = 0; pass < 3; ++pass) {
+        // (the shade pass has no counter or jitter variants: one slot; option csg_shade)
+        JitSlot& r = s->resolved[pass == 2 ? 24 : 16 + 4 * pass + (cnt ? 2 : 0) + ((sel & 1) ? 1 : 0)];
+        if (pass == 2 && !r.done && !opt_on(OPT_CSG_SHADE)) {
+            r.done = true;  // (the precompiled shade pass)
+            r.fn = nullptr;
+        }
         if (!r.done) {
             r.block = B;
             // option jit_csg 2 / 3: the camera's boxes / and the object records as literals too
             const int bake = opt(OPT_JIT_CSG) >= 3.0 ? 3 : opt(OPT_JIT_CSG) >= 2.0 ? 2 : 0;
             const bool can = !s->csg_tables.empty() && s->tr_valid && s->tr_bounds.size() == s->h_nodes.size();
-            r.lds = (((int)opt(OPT_CSG_RAYS) >> pass) & 1) == 0;
+            r.lds = pass < 2 && (((int)opt(OPT_CSG_RAYS) >> pass) & 1) == 0;
             std::vector<std::string> fixed;
             jit_fixed_opts(s->view, s->kp, s->traits, false, fixed);
             jit_split_kernel(s->device,
@@ -3365,7 +3375,7 @@ int render_split(rtx_scene* s, Launch L, const KParams* kp, size_t hbytes, hipSt
         for (bool f : {s->has_mesh, s->has_secondary, cnt, (sel & 1) != 0}) s->last_kernel += f ? '1' : '0';
     }
     auto launch = [&](int pass, const RenderLaunch& r, const Launch& Lc, const SplitBuf& sb) {
-        if (pass < 2 && sk[pass]->fn && jit_enabled()) {
+        if (sk[pass]->fn && jit_enabled()) {
             const KParams* kpp = r.kp;
             Launch La = Lc;
             SplitBuf sbb = sb;
